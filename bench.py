@@ -1,0 +1,213 @@
+"""bench.py — Msamples/s through the WBFM demod chain on 1..8 MI355X.
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`, one process
+per GPU under torch.distributed.run for N > 1. A step is one pass of the hot
+path over one block of synthetic IQ already resident in HBM: per GPU, one
+C2-sized channel (2^26 cf32 @ 10 Msps, its own tuning offset; BASELINE.json
+configs[1]). Channels are independent: no collective on the data path
+("scaling": "weak"); the only collectives are the timing barrier / max.
+
+The roofline object prices the one kernel the chain runs (k_wbfm) with HIP
+events on the stream it is launched on: algorithmic bytes per launch
+(8 B cf32 in + 4 B f32 audio out per 8 inputs = 8.5 B per input sample, SURVEY
+§8d) / average kernel time, against the 8.0 TB/s HBM3E peak. The cpu_baseline
+is the scalar oracle ("port" of the reference Rust, 1 thread, the reference is
+single-threaded) timed on this host on a bounded prefix of the same input.
+
+Other workloads (--config c3|c4|c5) are available for DESIGN.md tables; the
+driver's default line is c2.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "orion-sdr_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (device memory, streams, torch.distributed: plumbing)
+
+import orion_sdr  # noqa: E402  (the HIP engine; raises if the library is missing)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "Msamples/s through WBFM demod chain (NCO+decim+FM discrim) at 1/2/4/8 MI355X"
+OFFSETS = [1.5e6, -2.25e6, 0.75e6, -3.5e6, 2.75e6, -0.5e6, 3.75e6, -1.25e6]
+
+
+def wbfm_iq(n, f_off, dev, seed, fs=10e6):
+    """C2 synthetic IQ generated on the device: FM (dev 75 kHz) of
+    0.5 sin(1 kHz) + 0.3 sin(7 kHz) at +f_off, plus complex AWGN (P = 0.0025)."""
+    t = torch.arange(n, device=dev, dtype=torch.float64) / fs
+    aud = 0.5 * torch.sin(2 * np.pi * 1e3 * t) + 0.3 * torch.sin(2 * np.pi * 7e3 * t)
+    ph = torch.cumsum(2 * np.pi * 75e3 / fs * aud, 0) + 2 * np.pi * f_off * t
+    del aud
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    x = torch.polar(torch.ones_like(ph), ph).to(torch.complex64)
+    del ph, t
+    x += (torch.randn(n, dtype=torch.complex64, device=dev, generator=g) * np.sqrt(0.0025)).to(torch.complex64)
+    return x
+
+
+def make_workload(cfg, rank, dev, n_override=None):
+    """Returns (block, x, out, samples_per_step, bytes_per_sample, description)."""
+    if cfg == "c2":
+        n = n_override or (1 << 26)
+        blk = orion_sdr.WbfmChain(f_off=OFFSETS[rank % len(OFFSETS)])
+        x = wbfm_iq(n, OFFSETS[rank % len(OFFSETS)], dev, 0x1234 + rank)
+        desc = dict(workload="C2 WBFM chain: Rotator(-f_off) -> FirDecimator(10e6, 8, 200e3, 79e3; 127 taps) -> "
+                    "FmQuadratureDemod(1.25e6, 75e3, 15e3) -> FirLowpass(1.25e6, 15e3, 10e3; 125 taps)",
+                    fs_hz=10e6, samples_per_step_per_gpu=n, channels_per_gpu=1)
+        return blk, x, n, 8.5, desc
+    if cfg == "c4":
+        nch, n = 8, n_override or (1 << 24)
+        offs = [OFFSETS[(rank * nch + c) % len(OFFSETS)] * (1 + 0.01 * c) for c in range(nch)]
+        blk = orion_sdr.WbfmChain(f_off=offs)
+        x = torch.stack([wbfm_iq(n, f, dev, 0x1234 + rank * nch + c) for c, f in enumerate(offs)]).contiguous()
+        desc = dict(workload="C4 WBFM chain, 8 independent channels per GPU", samples_per_step_per_gpu=nch * n,
+                    channels_per_gpu=nch)
+        return blk, x, nch * n, 8.5, desc
+    if cfg == "c3":
+        nch, n = 256, n_override or (1 << 20)
+        blk = orion_sdr.FirDecimator(10e6, 8, 190e3, 39370.0, channels=nch)
+        g = torch.Generator(device=dev)
+        g.manual_seed(77 + rank)
+        x = torch.randn(nch, n, dtype=torch.complex64, device=dev, generator=g)
+        desc = dict(workload="C3 batched FirDecimator, 256 channels x 255 taps, M=8", samples_per_step_per_gpu=nch * n,
+                    channels_per_gpu=nch)
+        return blk, x, nch * n, 9.0, desc
+    if cfg == "c5":
+        nch, n = 128, n_override or (1 << 20)
+        blk = orion_sdr.SsbProductDemod(48e3, 1500.0, 2800.0, channels=nch)
+        g = torch.Generator(device=dev)
+        g.manual_seed(99 + rank)
+        t = torch.arange(n, device=dev, dtype=torch.float64) / 48e3
+        base = torch.polar(torch.ones_like(t), 2 * np.pi * 2700.0 * t).to(torch.complex64) * 0.4
+        x = (base.unsqueeze(0) + 0.03 * torch.randn(nch, n, dtype=torch.complex64, device=dev, generator=g)).contiguous()
+        desc = dict(workload="C5 SsbProductDemod, 128 channels per GPU @ 48 ksps", samples_per_step_per_gpu=nch * n,
+                    channels_per_gpu=nch)
+        return blk, x, nch * n, 12.0, desc
+    raise SystemExit(f"unknown --config {cfg}")
+
+
+def cpu_baseline(x_dev, cfg, seconds_target, max_samples):
+    """Scalar oracle ("port") on this host, 1 thread, bounded prefix of the input."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    if cfg not in ("c2",):
+        return None
+    n = min(max_samples, x_dev.shape[-1])
+    xh = x_dev[:n].cpu().numpy()
+    probe = 1 << 18
+    t0 = time.perf_counter()
+    O.wbfm(xh[:probe], f_off=OFFSETS[0])
+    rate = probe / (time.perf_counter() - t0)
+    n = int(min(n, max(probe, rate * seconds_target)))
+    n -= n % 8
+    t0 = time.perf_counter()
+    ref = O.wbfm(xh[:n], f_off=OFFSETS[0])
+    dt = time.perf_counter() - t0
+    return dict(value=round(n / dt / 1e6, 4), unit="Msamples/s", cores=1, kind="port",
+                sample=f"first {n} samples (2^{np.log2(n):.2f}) of the rank-0 C2 input, oracle/orion_oracle.c "
+                       f"o_run_wbfm, one call, 1 thread, {os.uname().nodename}",
+                seconds=round(dt, 2)), xh[:n], ref
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--n", type=int, default=0, help="override samples per channel")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-max-samples", type=int, default=1 << 24)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+
+    blk, x, samples, bps, desc = make_workload(args.config, rank, dev, args.n or None)
+    nout = blk.out_len(x.shape[-1])
+    out_shape = (nout,) if x.dim() == 1 else (x.shape[0], nout)
+    out_dtype = torch.float32 if args.config != "c3" else torch.complex64
+    out = torch.empty(out_shape, dtype=out_dtype, device=dev)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        blk.process_device(x, out, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    # kernel timing: HIP events on the stream the kernel is launched on
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+    total = samples * world * args.steps
+    value = total / elapsed / 1e6
+    achieved = samples * bps / (kern_ms * 1e-3) / 1e9  # GB/s, one launch per step
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": dict(desc, parallelism=f"channel-sharded x{world}, no data-path collective"),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "k_wbfm" if args.config in ("c2", "c4") else ("k_decim8" if args.config == "c3"
+                                                                            else "k_scan_*"),
+                     "kernel_ms": round(kern_ms, 4), "bytes_per_sample": bps},
+        "cpu_baseline": None,
+    }
+    traffic_file = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(traffic_file):
+        tr = json.load(open(traffic_file))
+        if tr.get("samples_per_launch") == samples:
+            line["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
+    if rank == 0 and world == 1 and not args.no_cpu and args.config == "c2":
+        res = cpu_baseline(x, args.config, args.cpu_seconds, args.cpu_max_samples)
+        if res:
+            cb, xh, ref = res
+            fresh = orion_sdr.WbfmChain(f_off=OFFSETS[0])
+            got = fresh.process(xh)
+            den = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
+            cb["gpu_vs_cpu_nrmse"] = float(np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2)) / den)
+            line["cpu_baseline"] = cb
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,140 @@
+/*
+ * orion_sdr_amd.h — C ABI of the MI355X (gfx950) streaming DSP engine.
+ *
+ * Drop-in boundary for skynavga/orion-sdr's analog sample-stream path. Every
+ * entry point replaces one reference interface (cited file:line, reference
+ * v0.0.63). Plain pointers and sizes only: no HIP or torch types cross this
+ * boundary (streams are passed as `void*` = hipStream_t, NULL = default stream).
+ *
+ * Contract (src/core.rs:6-22, trait Block):
+ *  - A handle is one stateful Block instance; it keeps its streaming state
+ *    (delay lines, oscillator phase, IIR state, discriminator history) across
+ *    calls, so k calls on consecutive chunks equal one call on the whole.
+ *  - orion_block_process*: 1:1 blocks consume n = min(n_in, out_cap) samples;
+ *    FirDecimator and the WBFM chain consume all n_in and write
+ *    min(ceil(n_in/m), out_cap) (dsp/decim.rs:66-75). The decimation phase
+ *    restarts at every call, as in the reference (decim.rs:68-71).
+ *  - Return 0 on success, a negative ORION_E_* code otherwise (the reference
+ *    never fails on lengths; errors here are HIP/argument failures only).
+ *  - Types: cf32 = interleaved {float re, im} (num_complex::Complex32), f32.
+ *  - Multi-channel handles (nch > 1) read in[ch*n_in + i] and write
+ *    out[ch*out_cap + j]; channels are independent streams.
+ */
+#ifndef ORION_SDR_AMD_H
+#define ORION_SDR_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORION_OK 0
+#define ORION_E_NULL (-1)
+#define ORION_E_HIP (-2)
+#define ORION_E_ARG (-3)
+#define ORION_E_TYPE (-4)
+#define ORION_E_UNSUPPORTED (-5)
+
+#define ORION_DT_C32 0
+#define ORION_DT_F32 1
+
+/* core.rs:6-10 */
+typedef struct {
+  size_t in_read;
+  size_t out_written;
+} orion_work_report;
+
+typedef struct orion_block orion_block;
+
+/* ---- library ---------------------------------------------------------- */
+const char* orion_version(void);
+const char* orion_last_error(void);          /* thread-local message of the last failure */
+int orion_device_count(void);
+int orion_set_device(int device);
+int orion_synchronize(void* stream);
+
+/* ---- constructors (one per reference constructor) ---------------------- */
+/* dsp/rotator.rs:16-26 Rotator::new(freq_hz, fs); Block-like rotate_block (:74-85). cf32->cf32 */
+orion_block* orion_rotator_new(float freq_hz, float fs);
+/* dsp/decim.rs:24-37 FirDecimator::new(fs, m, cutoff_hz, trans_hz). cf32->cf32 */
+orion_block* orion_fir_decimator_new(float fs, size_t m, float cutoff_hz, float trans_hz);
+/* Batched FirDecimator: nch independent channels sharing one design. */
+orion_block* orion_fir_decimator_batch_new(float fs, size_t m, float cutoff_hz, float trans_hz,
+                                           size_t nch);
+/* dsp/fir.rs:16-44 FirLowpass::design(fs, pass_hz, trans_hz); process :47-54. f32->f32 */
+orion_block* orion_fir_lowpass_new(float fs, float pass_hz, float trans_hz);
+/* dsp/fir.rs:186-188 FirLowpassIq::design(num_taps, cutoff_norm, stopband_db). cf32->cf32 */
+orion_block* orion_fir_lowpass_iq_design(size_t num_taps, float cutoff_norm, float stopband_db);
+/* dsp/fir.rs:193-204 FirLowpassIq::from_taps(taps) (empty -> [1.0]). */
+orion_block* orion_fir_lowpass_iq_from_taps(const float* taps, size_t n);
+/* dsp/fir.rs:260-276 FirLowpassIq::filter_aligned(io) on device memory (resets state). */
+int orion_fir_lowpass_iq_filter_aligned_device(orion_block* b, void* io_dev, size_t n, void* stream);
+/* Host-memory variant of filter_aligned (synchronous). */
+int orion_fir_lowpass_iq_filter_aligned(orion_block* b, void* io, size_t n);
+/* dsp/iir.rs:49-71 LpCascade::design(fs, fc) as a f32->f32 block (:79-83). */
+orion_block* orion_lp_cascade_new(float fs, float fc);
+/* dsp/dc.rs:15-21 DcBlocker::new(fs, cut_hz); Block impl :40-58. f32->f32 */
+orion_block* orion_dc_blocker_new(float fs, float cut_hz);
+/* demodulate/fm.rs:22-32 FmQuadratureDemod::new(fs, dev_hz, audio_bw_hz). cf32->f32 */
+orion_block* orion_fm_quadrature_demod_new(float fs, float dev_hz, float audio_bw_hz);
+/* demodulate/fm.rs:34-37 with_translate(freq_hz) (before the first process call). */
+int orion_fm_quadrature_demod_with_translate(orion_block* b, float freq_hz);
+/* demodulate/pm.rs:22-32 PmQuadratureDemod::new(fs, k, audio_bw_hz). cf32->f32 */
+orion_block* orion_pm_quadrature_demod_new(float fs, float k, float audio_bw_hz);
+/* demodulate/ssb.rs:15-20 SsbProductDemod::new(fs, bfo_hz, audio_bw_hz). cf32->f32 */
+orion_block* orion_ssb_product_demod_new(float fs, float bfo_hz, float audio_bw_hz);
+/* Batched SsbProductDemod: nch independent channels. */
+orion_block* orion_ssb_product_demod_batch_new(float fs, float bfo_hz, float audio_bw_hz, size_t nch);
+/* demodulate/am.rs:24-30 AmEnvelopeDemod::new(fs, audio_bw_hz). cf32->f32 */
+orion_block* orion_am_envelope_demod_new(float fs, float audio_bw_hz);
+/* demodulate/am.rs:33-36 with_abs_approx(k1, k2). */
+int orion_am_envelope_demod_with_abs_approx(orion_block* b, float k1, float k2);
+/* demodulate/cw.rs:15-25 CwEnvelopeDemod::new(fs, tone_hz, env_bw_hz); set_gain :26-28. */
+orion_block* orion_cw_envelope_demod_new(float fs, float tone_hz, float env_bw_hz);
+int orion_cw_envelope_demod_set_gain(orion_block* b, float g);
+
+/* The WBFM chain composed per docs/demodulate.md:128-133 (no single reference
+ * type): Rotator(-f_off, fs) -> FirDecimator(fs, m, dec_cutoff, dec_trans) ->
+ * FmQuadratureDemod(fs/m, dev_hz, audio_bw) -> FirLowpass(fs/m, audio_pass,
+ * audio_trans). cf32 -> f32, fused into one gfx950 kernel (m must be 8). */
+typedef struct {
+  float fs, f_off, dec_cutoff, dec_trans, dev_hz, audio_bw, audio_pass, audio_trans;
+  size_t m;
+} orion_wbfm_params;
+orion_block* orion_wbfm_chain_new(const orion_wbfm_params* p);
+/* nch channels sharing the design, each with its own tuning offset f_off[ch]. */
+orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float* f_off, size_t nch);
+/* Tuning knob: decimated outputs per workgroup and IIR warm-up length. */
+int orion_wbfm_chain_set_tiling(orion_block* b, int outputs_per_wg, int warmup);
+
+/* ---- Block contract (core.rs:12-22) ------------------------------------ */
+/* Host buffers (synchronous). */
+int orion_block_process(orion_block* b, const void* in, size_t n_in, void* out, size_t out_cap,
+                        orion_work_report* wr);
+/* Device buffers (asynchronous on `stream`). */
+int orion_block_process_device(orion_block* b, const void* in_dev, size_t n_in, void* out_dev,
+                               size_t out_cap, void* stream, orion_work_report* wr);
+int orion_block_reset(orion_block* b);
+void orion_block_free(orion_block* b);
+int orion_block_in_type(const orion_block* b);
+int orion_block_out_type(const orion_block* b);
+size_t orion_block_out_len(const orion_block* b, size_t n_in);
+size_t orion_block_channels(const orion_block* b);
+const char* orion_block_name(const orion_block* b);
+/* Designed coefficients, for parity tests: which = 0 primary taps, 1 audio taps. */
+int orion_block_taps(const orion_block* b, int which, float* out, size_t cap, size_t* n);
+
+/* ---- designs (host only; bit-exact with the reference constructors) ----- */
+size_t orion_fir_lowpass_design(float fs, float pass_hz, float trans_hz, float* taps, size_t cap); /* fir.rs:16-44 */
+size_t orion_kaiser_lowpass_taps(size_t num_taps, float cutoff_norm, float stopband_db, float* taps,
+                                 size_t cap);                                                     /* fir.rs:113-141 */
+float orion_kaiser_transition_norm(size_t num_taps, float stopband_db);                           /* fir.rs:147-150 */
+size_t orion_kaiser_num_taps(float transition_norm, float stopband_db);                           /* fir.rs:154-157 */
+void orion_lp_cascade_design(float fs, float fc, float out5[5]);                                  /* iir.rs:49-71 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORION_SDR_AMD_H */

@@ -1,0 +1,421 @@
+// blocks.cpp — Block implementations over the gfx950 kernels (host side).
+#include "blocks.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace orion {
+
+// ------------------------------------------------------------------ DevBuf --
+DevBuf::~DevBuf() {
+  if (p_) (void)hipFree(p_);
+}
+void DevBuf::resize(size_t bytes) {
+  if (bytes <= n_) return;
+  if (p_) ORION_HIP(hipFree(p_));
+  p_ = nullptr;
+  n_ = 0;
+  ORION_HIP(hipMalloc(&p_, bytes < 256 ? 256 : bytes));
+  n_ = bytes < 256 ? 256 : bytes;
+}
+void DevBuf::zero(hipStream_t s) {
+  if (p_) ORION_HIP(hipMemsetAsync(p_, 0, n_, s));
+}
+void DevBuf::upload(const void* h, size_t bytes, hipStream_t s) {
+  resize(bytes);
+  ORION_HIP(hipMemcpyAsync(p_, h, bytes, hipMemcpyHostToDevice, s));
+  ORION_HIP(hipStreamSynchronize(s));
+}
+
+// ------------------------------------------------------------------- Block --
+Block::~Block() {
+  if (hs_) (void)hipStreamDestroy(hs_);
+}
+hipStream_t Block::host_stream() {
+  if (!hs_) ORION_HIP(hipStreamCreateWithFlags(&hs_, hipStreamNonBlocking));
+  return hs_;
+}
+
+WorkReport Block::process_host(const void* in, size_t n_in, void* out, size_t out_cap) {
+  hipStream_t s = host_stream();
+  const int nch = channels();
+  const size_t ib = dt_size(in_type()), ob = dt_size(out_type());
+  stage_in_.resize(std::max<size_t>(1, n_in * nch * ib));
+  stage_out_.resize(std::max<size_t>(1, out_cap * nch * ob));
+  if (n_in) ORION_HIP(hipMemcpyAsync(stage_in_.as<void>(), in, n_in * nch * ib, hipMemcpyHostToDevice, s));
+  WorkReport w = process_device(stage_in_.as<void>(), n_in, stage_out_.as<void>(), out_cap, s);
+  if (nch == 1) {
+    if (w.out_written)
+      ORION_HIP(hipMemcpyAsync(out, stage_out_.as<void>(), w.out_written * ob, hipMemcpyDeviceToHost, s));
+  } else if (w.out_written) {
+    ORION_HIP(hipMemcpy2DAsync(out, out_cap * ob, stage_out_.as<void>(), out_cap * ob,
+                               w.out_written * ob, nch, hipMemcpyDeviceToHost, s));
+  }
+  ORION_HIP(hipStreamSynchronize(s));
+  return w;
+}
+
+namespace {
+
+Taps256 taps256(const std::vector<float>& g) {
+  Taps256 t{};
+  for (size_t i = 0; i < g.size() && i < 256; ++i) t.g[i] = g[i];
+  return t;
+}
+
+// FirLowpass::dot pairs taps[L-1] with the newest sample and taps[t] with
+// x[n-1-t] (dsp/fir.rs:57-66). As a standard FIR y[n] = sum_k g[k] x[n-k]:
+// g[0] = taps[L-1], g[k] = taps[k-1].
+std::vector<float> fir_lowpass_as_standard(const std::vector<float>& h) {
+  std::vector<float> g(h.size());
+  g[0] = h.back();
+  for (size_t k = 1; k < h.size(); ++k) g[k] = h[k - 1];
+  return g;
+}
+
+int padded_hist(int K) {
+  if (K <= 64) return 64;
+  if (K <= 128) return 128;
+  if (K <= 256) return 256;
+  return K;
+}
+
+// -------------------------------------------------------------- Rotator ----
+class RotatorBlock final : public Block {
+ public:
+  RotatorBlock(float f, float fs) : osc_(oscillator(f, fs)) {
+    const auto tab = phasor_table(osc_.theta, kRotTile);
+    tab_.upload(tab.data(), tab.size() * sizeof(float));
+  }
+  const char* name() const override { return "Rotator"; }
+  Dt in_type() const override { return Dt::C32; }
+  Dt out_type() const override { return Dt::C32; }
+  WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
+    const size_t n = std::min(n_in, out_cap);  // rotator.rs:76
+    launch_rotator(static_cast<const f2*>(in), static_cast<f2*>(out), static_cast<long long>(n), k_,
+                   osc_.step_q64, tab_.as<f2>(), s);
+    k_ += n;
+    return {n, n};
+  }
+  void reset() override { k_ = 0; }  // Rotator::reset_phase (rotator.rs:29-32)
+  std::vector<float> taps(int) const override { return {osc_.w_re, osc_.w_im}; }
+
+ private:
+  Oscillator osc_;
+  DevBuf tab_;
+  uint64_t k_ = 0;
+};
+
+// --------------------------------------------------------- FirDecimator ----
+class DecimBlock final : public Block {
+ public:
+  DecimBlock(float fs, size_t m, float cutoff, float trans, int nch) : m_(m < 1 ? 1 : m), nch_(nch) {
+    h_ = fir_lowpass_taps(fs, cutoff, trans);  // decim.rs:25-26: FirLowpass::design
+    g_ = fir_lowpass_as_standard(h_);
+    K_ = static_cast<int>(g_.size());
+    // Fast polyphase path (M = 8, Q in {16, 32}) wants taps phase-major.
+    if (m_ == 8 && K_ <= 256) {
+      const int Q = K_ <= 128 ? 16 : 32;
+      std::vector<float> pm(8 * Q, 0.0f);
+      for (int k = 0; k < K_; ++k) pm[(k % 8) * Q + k / 8] = g_[k];
+      fast_ = taps256(pm);
+      hist_len_ = 8 * Q;
+    } else {
+      hist_len_ = K_;
+    }
+    g_dev_.upload(g_.data(), g_.size() * sizeof(float));
+    for (auto& h : hist_) {
+      h.resize(static_cast<size_t>(hist_len_) * nch_ * sizeof(f2));
+      h.zero();
+    }
+    ORION_HIP(hipDeviceSynchronize());
+  }
+  const char* name() const override { return "FirDecimator"; }
+  Dt in_type() const override { return Dt::C32; }
+  Dt out_type() const override { return Dt::C32; }
+  int channels() const override { return nch_; }
+  size_t out_len(size_t n) const override { return (n + m_ - 1) / m_; }
+  WorkReport process_device(const void* in, size_t n, void* out, size_t out_cap, hipStream_t s) override {
+    if (n == 0) return {0, 0};
+    const size_t n_write = std::min(out_len(n), out_cap);  // decim.rs:66-67
+    const f2* x = static_cast<const f2*>(in);
+    launch_decim_batch(x, static_cast<long long>(n), static_cast<long long>(n), hist_[cur_].as<f2>(),
+                       hist_len_, static_cast<f2*>(out), static_cast<long long>(out_cap),
+                       static_cast<long long>(n_write), nch_, static_cast<int>(m_), K_, fast_,
+                       g_dev_.as<float>(), s);
+    for (int ch = 0; ch < nch_; ++ch)
+      launch_hist_update_c(x + ch * n, static_cast<long long>(n), hist_[cur_].as<f2>() + ch * hist_len_,
+                           hist_[cur_ ^ 1].as<f2>() + ch * hist_len_, hist_len_, s);
+    cur_ ^= 1;
+    return {n, n_write};  // all input consumed, decim.rs:72-75
+  }
+  void reset() override {
+    for (auto& h : hist_) h.zero();
+    ORION_HIP(hipDeviceSynchronize());
+  }
+  std::vector<float> taps(int) const override { return h_; }
+
+ private:
+  size_t m_;
+  int nch_;
+  std::vector<float> h_, g_;
+  int K_ = 0, hist_len_ = 0;
+  Taps256 fast_{};
+  DevBuf g_dev_, hist_[2];
+  int cur_ = 0;
+};
+
+// ----------------------------------------------------------- FirLowpass ----
+class FirRealBlock final : public Block {
+ public:
+  FirRealBlock(float fs, float pass, float trans) {
+    h_ = fir_lowpass_taps(fs, pass, trans);
+    g_ = fir_lowpass_as_standard(h_);
+    K_ = static_cast<int>(g_.size());
+    hist_len_ = padded_hist(K_);
+    std::vector<float> gp(std::max(K_, 256), 0.0f);
+    std::copy(g_.begin(), g_.end(), gp.begin());
+    fast_ = taps256(gp);
+    g_dev_.upload(g_.data(), g_.size() * sizeof(float));
+    for (auto& h : hist_) {
+      h.resize(hist_len_ * sizeof(float));
+      h.zero();
+    }
+    ORION_HIP(hipDeviceSynchronize());
+  }
+  const char* name() const override { return "FirLowpass"; }
+  Dt in_type() const override { return Dt::F32; }
+  Dt out_type() const override { return Dt::F32; }
+  WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
+    const size_t n = std::min(n_in, out_cap);  // fir.rs:48
+    if (n == 0) return {0, 0};
+    const float* x = static_cast<const float*>(in);
+    launch_fir_real(x, static_cast<long long>(n), hist_[cur_].as<float>(), hist_len_, static_cast<float*>(out),
+                    K_, fast_, g_dev_.as<float>(), s);
+    launch_hist_update_r(x, static_cast<long long>(n), hist_[cur_].as<float>(), hist_[cur_ ^ 1].as<float>(),
+                         hist_len_, s);
+    cur_ ^= 1;
+    return {n, n};
+  }
+  void reset() override {
+    for (auto& h : hist_) h.zero();
+    ORION_HIP(hipDeviceSynchronize());
+  }
+  std::vector<float> taps(int) const override { return h_; }
+
+ private:
+  std::vector<float> h_, g_;
+  int K_ = 0, hist_len_ = 0;
+  Taps256 fast_{};
+  DevBuf g_dev_, hist_[2];
+  int cur_ = 0;
+};
+
+// --------------------------------------------------------- FirLowpassIq ----
+class FirIqBlock final : public Block {
+ public:
+  explicit FirIqBlock(std::vector<float> taps) : h_(std::move(taps)) {
+    if (h_.empty()) h_.push_back(1.0f);  // fir.rs:195-197
+    K_ = static_cast<int>(h_.size());
+    hist_len_ = padded_hist(K_);
+    std::vector<float> gp(std::max(K_, 256), 0.0f);
+    std::copy(h_.begin(), h_.end(), gp.begin());  // taps[0] <-> newest (fir.rs:233-235)
+    fast_ = taps256(gp);
+    g_dev_.upload(h_.data(), h_.size() * sizeof(float));
+    for (auto& h : hist_) {
+      h.resize(hist_len_ * sizeof(f2));
+      h.zero();
+    }
+    zeros_.resize(hist_len_ * sizeof(f2));
+    zeros_.zero();
+    ORION_HIP(hipDeviceSynchronize());
+  }
+  const char* name() const override { return "FirLowpassIq"; }
+  Dt in_type() const override { return Dt::C32; }
+  Dt out_type() const override { return Dt::C32; }
+  WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
+    const size_t n = std::min(n_in, out_cap);  // fir.rs:288
+    if (n == 0) return {0, 0};
+    const f2* x = static_cast<const f2*>(in);
+    launch_fir_iq(x, static_cast<long long>(n), hist_[cur_].as<f2>(), hist_len_, static_cast<f2*>(out),
+                  static_cast<long long>(n), 0, K_, fast_, g_dev_.as<float>(), s);
+    launch_hist_update_c(x, static_cast<long long>(n), hist_[cur_].as<f2>(), hist_[cur_ ^ 1].as<f2>(),
+                         hist_len_, s);
+    cur_ ^= 1;
+    return {n, n};
+  }
+  void reset() override {
+    for (auto& h : hist_) h.zero();
+    ORION_HIP(hipDeviceSynchronize());
+  }
+  std::vector<float> taps(int) const override { return h_; }
+  // fir.rs:260-276: reset, then y[i] = streamed[i + d] over x padded with zeros.
+  void aligned(void* io, size_t n, hipStream_t s) {
+    reset();
+    if (n == 0) return;
+    scratch_.resize(n * sizeof(f2));
+    ORION_HIP(hipMemcpyAsync(scratch_.as<void>(), io, n * sizeof(f2), hipMemcpyDeviceToDevice, s));
+    const long long d = (K_ - 1) / 2;
+    launch_fir_iq(scratch_.as<f2>(), static_cast<long long>(n), zeros_.as<f2>(), hist_len_, static_cast<f2*>(io),
+                  static_cast<long long>(n), d, K_, fast_, g_dev_.as<float>(), s);
+    // The reference leaves the delay line holding the last K samples it pushed
+    // (x[n-K+d+1 .. n-1] then d zeros); a following streaming call sees them.
+    // Reproduce by rebuilding the history from [x | d zeros].
+    tail_.resize((n + d) * sizeof(f2) + 16);
+    ORION_HIP(hipMemsetAsync(tail_.as<void>(), 0, (n + d) * sizeof(f2), s));
+    ORION_HIP(hipMemcpyAsync(tail_.as<void>(), scratch_.as<void>(), n * sizeof(f2), hipMemcpyDeviceToDevice, s));
+    launch_hist_update_c(tail_.as<f2>(), static_cast<long long>(n + d), zeros_.as<f2>(), hist_[cur_ ^ 1].as<f2>(),
+                         hist_len_, s);
+    cur_ ^= 1;
+  }
+
+ private:
+  std::vector<float> h_;
+  int K_ = 0, hist_len_ = 0;
+  Taps256 fast_{};
+  DevBuf g_dev_, hist_[2], zeros_, scratch_, tail_;
+  int cur_ = 0;
+};
+
+// ------------------------------------------------------------ WBFM chain ----
+class WbfmBlock final : public Block {
+ public:
+  WbfmBlock(const WbfmParams& p, const std::vector<float>& f_off) : p_(p), nch_(static_cast<int>(f_off.size())) {
+    if (p.m != 8) throw std::invalid_argument("fused WBFM chain requires m = 8");
+    if (nch_ < 1) throw std::invalid_argument("WBFM chain needs >= 1 channel");
+    h_dec_ = fir_lowpass_taps(p.fs, p.dec_cutoff, p.dec_trans);
+    const float fs2 = p.fs / static_cast<float>(p.m);
+    h_aud_ = fir_lowpass_taps(fs2, p.audio_pass, p.audio_trans);
+    if (h_dec_.size() > 128 || h_aud_.size() > 128)
+      throw std::invalid_argument("fused WBFM chain supports <= 128 decimator and audio taps");
+    std::memset(&c_, 0, sizeof(c_));
+    const auto g = fir_lowpass_as_standard(h_dec_);
+    for (size_t k = 0; k < g.size(); ++k) c_.g[(k % 8) * kWbfmQ + k / 8] = g[k];
+    const auto a = fir_lowpass_as_standard(h_aud_);
+    for (size_t k = 0; k < a.size(); ++k) c_.a[k] = a[k];
+    const BiquadCoeffs bq = lp_cascade_design(fs2, p.audio_bw * 0.9f);  // fm.rs:24
+    c_.b0 = bq.b0; c_.b1 = bq.b1; c_.b2 = bq.b2; c_.a1 = bq.a1; c_.a2 = bq.a2;
+    c_.k = 1.0f / std::max(p.dev_hz, 1.0f);  // fm.rs:23
+    const StateSpace ss = lp_cascade_ss(bq);
+    auto m8 = mat_pow(ss.A, 4, 8);
+    for (int i = 0; i < 16; ++i) c_.m8[i] = static_cast<float>(m8[i]);
+    auto pwm = m8;
+    for (int s = 0; s < 6; ++s) {
+      for (int i = 0; i < 16; ++i) c_.pw[s * 16 + i] = static_cast<float>(pwm[i]);
+      pwm = mat_mul(pwm, pwm, 4);
+    }
+    std::vector<uint64_t> steps(nch_);
+    std::vector<float> tabs;
+    tabs.reserve(static_cast<size_t>(nch_) * kWbfmNS * 2);
+    for (int ch = 0; ch < nch_; ++ch) {
+      const Oscillator o = oscillator(-f_off[ch], p.fs);  // Rotator::new(-f_off, fs)
+      steps[ch] = o.step_q64;
+      const auto t = phasor_table(o.theta, kWbfmNS);
+      tabs.insert(tabs.end(), t.begin(), t.end());
+    }
+    step_.upload(steps.data(), steps.size() * sizeof(uint64_t));
+    tab_.upload(tabs.data(), tabs.size() * sizeof(float));
+    for (int i = 0; i < 2; ++i) {
+      carry_[i].resize(static_cast<size_t>(nch_) * kWbfmCarry * sizeof(float));
+      hist_[i].resize(static_cast<size_t>(nch_) * kWbfmHist * sizeof(f2));
+    }
+    reset();
+  }
+  const char* name() const override { return "WbfmChain"; }
+  Dt in_type() const override { return Dt::C32; }
+  Dt out_type() const override { return Dt::F32; }
+  int channels() const override { return nch_; }
+  size_t out_len(size_t n) const override { return (n + p_.m - 1) / p_.m; }
+  WorkReport process_device(const void* in, size_t n, void* out, size_t out_cap, hipStream_t s) override {
+    if (n == 0) return {0, 0};
+    const size_t n_dec = std::min(out_len(n), out_cap);
+    const int nxt = cur_ ^ 1;
+    if (n_dec == 0) {  // decimator consumed input, demod saw nothing (core.rs chain semantics)
+      const f2* x = static_cast<const f2*>(in);
+      for (int ch = 0; ch < nch_; ++ch)
+        launch_hist_update_c(x + ch * n, static_cast<long long>(n), hist_[cur_].as<f2>() + ch * kWbfmHist,
+                             hist_[nxt].as<f2>() + ch * kWbfmHist, kWbfmHist, s);
+      ORION_HIP(hipMemcpyAsync(carry_[nxt].as<void>(), carry_[cur_].as<void>(), carry_[cur_].size(),
+                               hipMemcpyDeviceToDevice, s));
+    } else {
+      WbfmArgs a{};
+      a.x = static_cast<const f2*>(in);
+      a.x_stride = static_cast<long long>(n);
+      a.n = static_cast<long long>(n);
+      a.y = static_cast<float*>(out);
+      a.y_stride = static_cast<long long>(out_cap);
+      a.n_dec = static_cast<long long>(n_dec);
+      a.k0 = static_cast<long long>(k0_);
+      a.step = step_.as<uint64_t>();
+      a.tab = tab_.as<f2>();
+      a.carry_in = carry_[cur_].as<float>();
+      a.carry_out = carry_[nxt].as<float>();
+      a.hist_in = hist_[cur_].as<f2>();
+      a.hist_out = hist_[nxt].as<f2>();
+      a.A = A_;
+      a.wpre = wpre_;
+      launch_wbfm(a, c_, nch_, s);
+    }
+    cur_ = nxt;
+    k0_ += n;
+    return {n, n_dec};
+  }
+  void reset() override {
+    std::vector<float> c0(static_cast<size_t>(nch_) * kWbfmCarry, 0.0f);
+    for (int ch = 0; ch < nch_; ++ch) c0[ch * kWbfmCarry + 4] = 1.0f;  // prev = 1+0j (fm.rs:29)
+    for (int i = 0; i < 2; ++i) {
+      carry_[i].upload(c0.data(), c0.size() * sizeof(float));
+      hist_[i].zero();
+    }
+    ORION_HIP(hipDeviceSynchronize());
+    cur_ = 0;
+    k0_ = 0;
+  }
+  std::vector<float> taps(int which) const override { return which == 0 ? h_dec_ : h_aud_; }
+  void set_tiling(int A, int wpre) {
+    if (A < 1 || wpre < 0) throw std::invalid_argument("bad tiling");
+    A_ = A;
+    wpre_ = wpre;
+  }
+
+ private:
+  WbfmParams p_;
+  int nch_;
+  std::vector<float> h_dec_, h_aud_;
+  WbfmConst c_;
+  DevBuf step_, tab_, carry_[2], hist_[2];
+  int cur_ = 0;
+  uint64_t k0_ = 0;
+  int A_ = 33 * kWbfmT - 640;  // 16256 outputs per workgroup: 33 full sub-tiles incl. warm-up
+  int wpre_ = 640;             // 512 IIR warm-up + 128 audio-FIR history
+};
+
+}  // namespace
+
+std::unique_ptr<Block> make_rotator(float f, float fs) { return std::make_unique<RotatorBlock>(f, fs); }
+std::unique_ptr<Block> make_fir_decimator(float fs, size_t m, float cutoff, float trans, int nch) {
+  return std::make_unique<DecimBlock>(fs, m, cutoff, trans, nch);
+}
+std::unique_ptr<Block> make_fir_lowpass(float fs, float pass, float trans) {
+  return std::make_unique<FirRealBlock>(fs, pass, trans);
+}
+std::unique_ptr<Block> make_fir_lowpass_iq(const std::vector<float>& taps) {
+  return std::make_unique<FirIqBlock>(taps);
+}
+int fir_lowpass_iq_filter_aligned(Block* b, void* io, size_t n, hipStream_t s) {
+  auto* f = dynamic_cast<FirIqBlock*>(b);
+  if (!f) return -4;
+  f->aligned(io, n, s);
+  return 0;
+}
+std::unique_ptr<Block> make_wbfm_chain(const WbfmParams& p, const std::vector<float>& f_off) {
+  return std::make_unique<WbfmBlock>(p, f_off);
+}
+void wbfm_set_tiling(Block* b, int A, int wpre) {
+  auto* w = dynamic_cast<WbfmBlock*>(b);
+  if (!w) throw std::invalid_argument("not a WBFM chain");
+  w->set_tiling(A, wpre);
+}
+
+}  // namespace orion

@@ -1,0 +1,101 @@
+// blocks.hpp — C++ mirror of the reference Block contract over the gfx950 kernels.
+//
+// Reference: trait Block { fn process(&mut self, &[In], &mut [Out]) -> WorkReport }
+// (src/core.rs:6-22). Each class owns its device-resident streaming state
+// (delay-line history, oscillator sample count, IIR carry, discriminator
+// history), so k calls on consecutive chunks equal one call on the
+// concatenation — the reference's "resume" semantics.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "design.hpp"
+#include "kernels.hpp"
+
+namespace orion {
+
+enum class Dt : int { C32 = 0, F32 = 1 };
+inline size_t dt_size(Dt d) { return d == Dt::C32 ? 8 : 4; }
+
+struct WorkReport {
+  size_t in_read = 0;
+  size_t out_written = 0;
+};
+
+// RAII device allocation.
+class DevBuf {
+ public:
+  DevBuf() = default;
+  explicit DevBuf(size_t bytes) { resize(bytes); }
+  ~DevBuf();
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  void resize(size_t bytes);      // discards contents when it grows
+  void zero(hipStream_t s = nullptr);
+  void upload(const void* h, size_t bytes, hipStream_t s = nullptr);
+  template <class T> T* as() const { return static_cast<T*>(p_); }
+  size_t size() const { return n_; }
+
+ private:
+  void* p_ = nullptr;
+  size_t n_ = 0;
+};
+
+class Block {
+ public:
+  virtual ~Block();
+  virtual const char* name() const = 0;
+  virtual Dt in_type() const = 0;
+  virtual Dt out_type() const = 0;
+  // Outputs produced for n inputs when out_cap is unbounded.
+  virtual size_t out_len(size_t n_in) const { return n_in; }
+  // Device buffers, asynchronous on `s` (no allocation, no sync: graph-capturable
+  // once staging has been sized). Channels: blocks built for nch > 1 read
+  // in[ch*n_in + i] and write out[ch*out_cap + j].
+  virtual WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap,
+                                    hipStream_t s) = 0;
+  // Host buffers: stage through device memory, synchronous.
+  WorkReport process_host(const void* in, size_t n_in, void* out, size_t out_cap);
+  virtual void reset() = 0;
+  virtual int channels() const { return 1; }
+  // Designed coefficients (for tests): which = 0 primary taps, 1 secondary.
+  virtual std::vector<float> taps(int which) const { (void)which; return {}; }
+
+ protected:
+  hipStream_t host_stream();
+  DevBuf stage_in_, stage_out_;
+
+ private:
+  hipStream_t hs_ = nullptr;
+};
+
+// dsp/rotator.rs:8-95 (rotate_block). C32 -> C32.
+std::unique_ptr<Block> make_rotator(float freq_hz, float fs);
+// dsp/decim.rs:10-77. C32 -> C32, out = ceil(n/m) (decimation phase restarts
+// every call, decim.rs:66-71 — reproduced).
+std::unique_ptr<Block> make_fir_decimator(float fs, size_t m, float cutoff_hz, float trans_hz,
+                                          int nch = 1);
+// dsp/fir.rs:7-67. F32 -> F32.
+std::unique_ptr<Block> make_fir_lowpass(float fs, float pass_hz, float trans_hz);
+// dsp/fir.rs:176-297 (from_taps; empty -> [1.0]). C32 -> C32.
+std::unique_ptr<Block> make_fir_lowpass_iq(const std::vector<float>& taps);
+// FirLowpassIq::filter_aligned (fir.rs:260-276) on device memory, in place allowed
+// via a scratch copy. Resets the block's streaming state first, like the reference.
+int fir_lowpass_iq_filter_aligned(Block* b, void* io_dev, size_t n, hipStream_t s);
+
+// The WBFM chain (docs/demodulate.md:128-133): Rotator(-f_off) -> FirDecimator
+// (fs, m=8, dec_cutoff, dec_trans) -> FmQuadratureDemod(fs/8, dev, audio_bw) ->
+// FirLowpass(fs/8, audio_pass, audio_trans). C32 -> F32, out = ceil(n/8).
+struct WbfmParams {
+  float fs, dec_cutoff, dec_trans, dev_hz, audio_bw, audio_pass, audio_trans;
+  size_t m;
+};
+std::unique_ptr<Block> make_wbfm_chain(const WbfmParams& p, const std::vector<float>& f_off);
+void wbfm_set_tiling(Block* b, int outputs_per_wg, int warmup);
+
+}  // namespace orion

@@ -1,0 +1,225 @@
+// capi.cpp — extern "C" boundary (include/orion_sdr_amd.h) over the Block layer.
+#include "../../include/orion_sdr_amd.h"
+
+#include <cstring>
+#include <exception>
+#include <memory>
+#include <string>
+
+#include "blocks.hpp"
+#include "scan_blocks.hpp"
+
+struct orion_block {
+  std::unique_ptr<orion::Block> impl;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char* what) {
+  g_err = what ? what : "unknown error";
+  return code;
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const orion::HipError& e) {
+    return fail(ORION_E_HIP, e.what());
+  } catch (const std::invalid_argument& e) {
+    return fail(ORION_E_ARG, e.what());
+  } catch (const std::exception& e) {
+    return fail(ORION_E_HIP, e.what());
+  }
+}
+
+template <class F>
+orion_block* make(F&& f) {
+  try {
+    auto b = new orion_block;
+    b->impl = f();
+    return b;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return nullptr;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+const char* orion_version(void) { return "orion-sdr-amd 0.1.0 (gfx950)"; }
+const char* orion_last_error(void) { return g_err.c_str(); }
+
+int orion_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+int orion_set_device(int d) {
+  return guarded([&] {
+    ORION_HIP(hipSetDevice(d));
+    return ORION_OK;
+  });
+}
+int orion_synchronize(void* stream) {
+  return guarded([&] {
+    ORION_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return ORION_OK;
+  });
+}
+
+orion_block* orion_rotator_new(float freq_hz, float fs) {
+  return make([&] { return orion::make_rotator(freq_hz, fs); });
+}
+orion_block* orion_fir_decimator_new(float fs, size_t m, float cutoff_hz, float trans_hz) {
+  return make([&] { return orion::make_fir_decimator(fs, m, cutoff_hz, trans_hz, 1); });
+}
+orion_block* orion_fir_decimator_batch_new(float fs, size_t m, float cutoff_hz, float trans_hz, size_t nch) {
+  return make([&] { return orion::make_fir_decimator(fs, m, cutoff_hz, trans_hz, static_cast<int>(nch)); });
+}
+orion_block* orion_fir_lowpass_new(float fs, float pass_hz, float trans_hz) {
+  return make([&] { return orion::make_fir_lowpass(fs, pass_hz, trans_hz); });
+}
+orion_block* orion_fir_lowpass_iq_design(size_t num_taps, float cutoff_norm, float stopband_db) {
+  return make([&] { return orion::make_fir_lowpass_iq(orion::kaiser_lowpass_taps(num_taps, cutoff_norm, stopband_db)); });
+}
+orion_block* orion_fir_lowpass_iq_from_taps(const float* taps, size_t n) {
+  return make([&] { return orion::make_fir_lowpass_iq(std::vector<float>(taps, taps + (taps ? n : 0))); });
+}
+int orion_fir_lowpass_iq_filter_aligned_device(orion_block* b, void* io, size_t n, void* stream) {
+  if (!b || (!io && n)) return fail(ORION_E_NULL, "null argument");
+  return guarded([&] { return orion::fir_lowpass_iq_filter_aligned(b->impl.get(), io, n, static_cast<hipStream_t>(stream)); });
+}
+int orion_fir_lowpass_iq_filter_aligned(orion_block* b, void* io, size_t n) {
+  if (!b || (!io && n)) return fail(ORION_E_NULL, "null argument");
+  return guarded([&] {
+    orion::DevBuf d(n * 8 + 8);
+    if (n) ORION_HIP(hipMemcpy(d.as<void>(), io, n * 8, hipMemcpyHostToDevice));
+    const int rc = orion::fir_lowpass_iq_filter_aligned(b->impl.get(), d.as<void>(), n, nullptr);
+    if (rc) return rc;
+    if (n) ORION_HIP(hipMemcpy(io, d.as<void>(), n * 8, hipMemcpyDeviceToHost));
+    ORION_HIP(hipDeviceSynchronize());
+    return ORION_OK;
+  });
+}
+orion_block* orion_lp_cascade_new(float fs, float fc) {
+  return make([&] { return orion::make_lp_cascade(fs, fc); });
+}
+orion_block* orion_dc_blocker_new(float fs, float cut_hz) {
+  return make([&] { return orion::make_dc_blocker(fs, cut_hz); });
+}
+orion_block* orion_fm_quadrature_demod_new(float fs, float dev_hz, float audio_bw_hz) {
+  return make([&] { return orion::make_fm_demod(fs, dev_hz, audio_bw_hz); });
+}
+int orion_fm_quadrature_demod_with_translate(orion_block* b, float freq_hz) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] { return orion::fm_demod_with_translate(b->impl.get(), freq_hz); });
+}
+orion_block* orion_pm_quadrature_demod_new(float fs, float k, float audio_bw_hz) {
+  return make([&] { return orion::make_pm_demod(fs, k, audio_bw_hz); });
+}
+orion_block* orion_ssb_product_demod_new(float fs, float bfo_hz, float audio_bw_hz) {
+  return make([&] { return orion::make_ssb_demod(fs, bfo_hz, audio_bw_hz, 1); });
+}
+orion_block* orion_ssb_product_demod_batch_new(float fs, float bfo_hz, float audio_bw_hz, size_t nch) {
+  return make([&] { return orion::make_ssb_demod(fs, bfo_hz, audio_bw_hz, static_cast<int>(nch)); });
+}
+orion_block* orion_am_envelope_demod_new(float fs, float audio_bw_hz) {
+  return make([&] { return orion::make_am_demod(fs, audio_bw_hz); });
+}
+int orion_am_envelope_demod_with_abs_approx(orion_block* b, float k1, float k2) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] { return orion::am_demod_with_abs_approx(b->impl.get(), k1, k2); });
+}
+orion_block* orion_cw_envelope_demod_new(float fs, float tone_hz, float env_bw_hz) {
+  return make([&] { return orion::make_cw_demod(fs, tone_hz, env_bw_hz); });
+}
+int orion_cw_envelope_demod_set_gain(orion_block* b, float g) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] { return orion::cw_demod_set_gain(b->impl.get(), g); });
+}
+
+static orion::WbfmParams wbfm_params(const orion_wbfm_params* p) {
+  return {p->fs, p->dec_cutoff, p->dec_trans, p->dev_hz, p->audio_bw, p->audio_pass, p->audio_trans, p->m};
+}
+orion_block* orion_wbfm_chain_new(const orion_wbfm_params* p) {
+  if (!p) { g_err = "null params"; return nullptr; }
+  return make([&] { return orion::make_wbfm_chain(wbfm_params(p), {p->f_off}); });
+}
+orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float* f_off, size_t nch) {
+  if (!p || !f_off || nch == 0) { g_err = "null params / no channels"; return nullptr; }
+  return make([&] { return orion::make_wbfm_chain(wbfm_params(p), std::vector<float>(f_off, f_off + nch)); });
+}
+int orion_wbfm_chain_set_tiling(orion_block* b, int A, int wpre) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    orion::wbfm_set_tiling(b->impl.get(), A, wpre);
+    return ORION_OK;
+  });
+}
+
+int orion_block_process(orion_block* b, const void* in, size_t n_in, void* out, size_t out_cap,
+                        orion_work_report* wr) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  if ((!in && n_in) || (!out && out_cap)) return fail(ORION_E_NULL, "null buffer");
+  return guarded([&] {
+    const orion::WorkReport w = b->impl->process_host(in, n_in, out, out_cap);
+    if (wr) { wr->in_read = w.in_read; wr->out_written = w.out_written; }
+    return ORION_OK;
+  });
+}
+int orion_block_process_device(orion_block* b, const void* in, size_t n_in, void* out, size_t out_cap,
+                               void* stream, orion_work_report* wr) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  if ((!in && n_in) || (!out && out_cap)) return fail(ORION_E_NULL, "null buffer");
+  return guarded([&] {
+    const orion::WorkReport w = b->impl->process_device(in, n_in, out, out_cap, static_cast<hipStream_t>(stream));
+    if (wr) { wr->in_read = w.in_read; wr->out_written = w.out_written; }
+    return ORION_OK;
+  });
+}
+int orion_block_reset(orion_block* b) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    b->impl->reset();
+    return ORION_OK;
+  });
+}
+void orion_block_free(orion_block* b) { delete b; }
+int orion_block_in_type(const orion_block* b) { return b ? static_cast<int>(b->impl->in_type()) : ORION_E_NULL; }
+int orion_block_out_type(const orion_block* b) { return b ? static_cast<int>(b->impl->out_type()) : ORION_E_NULL; }
+size_t orion_block_out_len(const orion_block* b, size_t n) { return b ? b->impl->out_len(n) : 0; }
+size_t orion_block_channels(const orion_block* b) { return b ? static_cast<size_t>(b->impl->channels()) : 0; }
+const char* orion_block_name(const orion_block* b) { return b ? b->impl->name() : ""; }
+int orion_block_taps(const orion_block* b, int which, float* out, size_t cap, size_t* n) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  const auto t = b->impl->taps(which);
+  if (n) *n = t.size();
+  if (out) std::memcpy(out, t.data(), std::min(cap, t.size()) * sizeof(float));
+  return ORION_OK;
+}
+
+size_t orion_fir_lowpass_design(float fs, float pass_hz, float trans_hz, float* taps, size_t cap) {
+  const auto t = orion::fir_lowpass_taps(fs, pass_hz, trans_hz);
+  if (taps) std::memcpy(taps, t.data(), std::min(cap, t.size()) * sizeof(float));
+  return t.size();
+}
+size_t orion_kaiser_lowpass_taps(size_t num_taps, float cutoff_norm, float stopband_db, float* taps, size_t cap) {
+  const auto t = orion::kaiser_lowpass_taps(num_taps, cutoff_norm, stopband_db);
+  if (taps) std::memcpy(taps, t.data(), std::min(cap, t.size()) * sizeof(float));
+  return t.size();
+}
+float orion_kaiser_transition_norm(size_t num_taps, float stopband_db) {
+  return orion::kaiser_transition_norm(num_taps, stopband_db);
+}
+size_t orion_kaiser_num_taps(float transition_norm, float stopband_db) {
+  return orion::kaiser_num_taps(transition_norm, stopband_db);
+}
+void orion_lp_cascade_design(float fs, float fc, float out5[5]) {
+  const auto c = orion::lp_cascade_design(fs, fc);
+  out5[0] = c.b0; out5[1] = c.b1; out5[2] = c.b2; out5[3] = c.a1; out5[4] = c.a2;
+}
+
+}  // extern "C"

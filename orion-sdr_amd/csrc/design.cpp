@@ -1,0 +1,239 @@
+// design.cpp — built with -ffp-contract=off (see design.hpp). Host only.
+#include "design.hpp"
+
+#include <cfloat>
+#include <cmath>
+
+namespace orion {
+
+namespace {
+constexpr float kTau = 6.28318530717958647692f;  // core::f32::consts::TAU
+constexpr float kPi = 3.14159265358979323846f;   // core::f32::consts::PI
+inline float fmax_rs(float a, float b) { return a > b ? a : (b > a ? b : a); }  // f32::max
+inline float clamp_rs(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+}  // namespace
+
+std::vector<float> fir_lowpass_taps(float fs, float pass_hz, float trans_hz) {
+  // dsp/fir.rs:17-19: clamp the pass band and transition, odd tap count >= 31.
+  pass_hz = fmax_rs(pass_hz, 10.0f);
+  trans_hz = fmax_rs(trans_hz, pass_hz * 0.2f);
+  size_t ntaps = static_cast<size_t>(std::ceil(fs / trans_hz));
+  if (ntaps < 31) ntaps = 31;
+  ntaps |= 1u;
+  std::vector<float> taps(ntaps);
+  const float fc = pass_hz / fs;
+  const long half = static_cast<long>(ntaps) / 2;
+  for (size_t n = 0; n < ntaps; ++n) {
+    const long m = static_cast<long>(n) - half;
+    float sinc;
+    if (m == 0) {
+      sinc = 2.0f * fc;
+    } else {
+      const float x = kPi * static_cast<float>(m);
+      const float arg = 2.0f * kPi * fc * static_cast<float>(m);
+      sinc = (2.0f * fc) * std::sin(arg) / x;  // fir.rs:29 evaluation order
+    }
+    const float w = 0.5f - 0.5f * std::cos(2.0f * kPi * static_cast<float>(n) /
+                                           (static_cast<float>(ntaps) - 1.0f));
+    taps[n] = sinc * w;
+  }
+  float s = 0.0f;  // Iterator::sum over f32: sequential left fold
+  for (float t : taps) s += t;
+  for (float& t : taps) t /= s;
+  return taps;
+}
+
+static float kaiser_beta(float a) {  // fir.rs:74-82
+  if (a > 50.0f) return 0.1102f * (a - 8.7f);
+  if (a >= 21.0f) return 0.5842f * std::pow(a - 21.0f, 0.4f) + 0.07886f * (a - 21.0f);
+  return 0.0f;
+}
+
+static float bessel_i0(float x) {  // fir.rs:86-99
+  const float half = 0.5f * x;
+  float term = 1.0f, sum = 1.0f;
+  for (unsigned k = 1; k <= 40; ++k) {
+    term *= half / static_cast<float>(k);
+    const float t = term * term;
+    sum += t;
+    if (t < 1e-12f * sum) break;
+  }
+  return sum;
+}
+
+std::vector<float> kaiser_lowpass_taps(size_t num_taps, float cutoff_norm, float stopband_db) {
+  const size_t m = (num_taps < 3 ? size_t{3} : num_taps) | 1u;  // fir.rs:114
+  const float mid = static_cast<float>(m / 2);
+  const float fc = clamp_rs(cutoff_norm, 1e-4f, 0.4999f);
+  const float beta = kaiser_beta(stopband_db);
+  const float i0b = bessel_i0(beta);
+  std::vector<float> taps(m);
+  for (size_t n = 0; n < m; ++n) {
+    const float d = static_cast<float>(n) - mid;
+    const float ideal = (d == 0.0f) ? 2.0f * fc : std::sin(kTau * fc * d) / (kPi * d);
+    const float r = d / mid;
+    const float w = bessel_i0(beta * std::sqrt(fmax_rs(1.0f - r * r, 0.0f))) / i0b;
+    taps[n] = ideal * w;
+  }
+  float s = 0.0f;
+  for (float t : taps) s += t;
+  if (std::fabs(s) > FLT_EPSILON)
+    for (float& t : taps) t /= s;
+  return taps;
+}
+
+float kaiser_transition_norm(size_t num_taps, float stopband_db) {  // fir.rs:147-150
+  const float m = static_cast<float>((num_taps < 3 ? size_t{3} : num_taps) | 1u);
+  return (fmax_rs(stopband_db, 21.0f) - 8.0f) / (14.36f * m);
+}
+
+size_t kaiser_num_taps(float transition_norm, float stopband_db) {  // fir.rs:154-157
+  const float m = std::ceil((fmax_rs(stopband_db, 21.0f) - 8.0f) /
+                            (14.36f * fmax_rs(transition_norm, 1e-4f)));
+  return static_cast<size_t>(fmax_rs(m, 3.0f)) | 1u;
+}
+
+static BiquadCoeffs rbj_butterworth_lp(float fs, float fc) {  // iir.rs:51-67, 112-121
+  const float w0 = kTau * fc / fs;
+  const float sn = std::sin(w0), cs = std::cos(w0);
+  const float alpha = sn / (2.0f * std::sqrt(0.5f));
+  const float b0 = (1.0f - cs) * 0.5f;
+  const float b1 = 1.0f - cs;
+  const float b2 = (1.0f - cs) * 0.5f;
+  const float a0 = 1.0f + alpha;
+  const float a1 = -2.0f * cs;
+  const float a2 = 1.0f - alpha;
+  const float norm = 1.0f / a0;
+  return {b0 * norm, b1 * norm, b2 * norm, a1 * norm, a2 * norm};
+}
+
+BiquadCoeffs lp_cascade_design(float fs, float fc) { return rbj_butterworth_lp(fs, fc); }
+
+float dc_blocker_pole(float fs, float cut_hz) {  // dc.rs:17, iir.rs:122
+  return clamp_rs(1.0f - 2.0f * kPi * (fmax_rs(cut_hz, 0.1f) / fs), 0.0f, 0.9999f);
+}
+
+LpDcCoeffs lpdc_design(float fs, float lp_fc, float dc_cut_hz) {
+  return {rbj_butterworth_lp(fs, lp_fc), dc_blocker_pole(fs, dc_cut_hz)};
+}
+
+float cw_alpha(float fs, float env_bw_hz) {  // cw.rs:17-18
+  const float fc = fmax_rs(env_bw_hz, 1.0f);
+  return std::exp(-kTau * fc / fs);
+}
+
+Oscillator oscillator(float freq_hz, float fs) {  // rotator.rs:17-18
+  Oscillator o;
+  const float phi = kTau * freq_hz / fs;
+  o.w_re = std::cos(phi);
+  o.w_im = std::sin(phi);
+  o.theta = std::atan2(static_cast<double>(o.w_im), static_cast<double>(o.w_re));
+  // theta/2pi in [-0.5, 0.5] -> wrapping Q0.64. Split to keep 64 bits exact.
+  long double rev = static_cast<long double>(o.theta) / (2.0L * 3.14159265358979323846264338327950288L);
+  if (rev < 0) rev += 1.0L;
+  long double scaled = rev * 18446744073709551616.0L;  // 2^64
+  if (scaled >= 18446744073709551616.0L) scaled -= 18446744073709551616.0L;
+  o.step_q64 = static_cast<uint64_t>(scaled + 0.5L);
+  return o;
+}
+
+std::vector<float> phasor_table(double theta, size_t n) {
+  std::vector<float> t(2 * n);
+  for (size_t k = 0; k < n; ++k) {
+    const long double a = static_cast<long double>(theta) * static_cast<long double>(k);
+    t[2 * k] = static_cast<float>(std::cos(a));
+    t[2 * k + 1] = static_cast<float>(std::sin(a));
+  }
+  return t;
+}
+
+// ---- state-space extraction -------------------------------------------------
+// Run one exact-arithmetic (f64) step of the reference update with x = 0 on each
+// unit state to obtain the columns of A.
+template <class Step>
+static std::vector<double> extract_A(int S, Step step) {
+  std::vector<double> A(S * S);
+  for (int c = 0; c < S; ++c) {
+    std::vector<double> s(S, 0.0);
+    s[c] = 1.0;
+    step(s.data(), 0.0);
+    for (int r = 0; r < S; ++r) A[r * S + c] = s[r];
+  }
+  return A;
+}
+
+static double biquad_step(double* z, double x, const BiquadCoeffs& c) {  // iir.rs:34-40
+  const double y = x * c.b0 + z[0];
+  const double z1 = x * c.b1 + z[1] - c.a1 * y;
+  const double z2 = x * c.b2 - c.a2 * y;
+  z[0] = z1;
+  z[1] = z2;
+  return y;
+}
+
+StateSpace lp_cascade_ss(const BiquadCoeffs& c) {
+  StateSpace ss;
+  ss.S = 4;
+  ss.A = extract_A(4, [&](double* s, double x) {
+    const double y0 = biquad_step(s, x, c);
+    biquad_step(s + 2, y0, c);
+  });
+  ss.D = 0;
+  return ss;
+}
+
+StateSpace lpdc_ss(const LpDcCoeffs& c) {  // iir.rs:151-165, state (z0_1,z0_2,z1_1,z1_2,dc_x1,dc_y1)
+  StateSpace ss;
+  ss.S = 6;
+  ss.A = extract_A(6, [&](double* s, double x) {
+    const double y0 = biquad_step(s, x, c.bq);
+    const double y1 = biquad_step(s + 2, y0, c.bq);
+    const double y = y1 - s[4] + static_cast<double>(c.r) * s[5];
+    s[4] = y1;
+    s[5] = y;
+  });
+  ss.D = 0;
+  return ss;
+}
+
+StateSpace dc_ss(float r) {  // dc.rs:47-51, state (x1, y1)
+  StateSpace ss;
+  ss.S = 2;
+  ss.A = extract_A(2, [&](double* s, double x) {
+    const double y = x - s[0] + static_cast<double>(r) * s[1];
+    s[0] = x;
+    s[1] = y;
+  });
+  ss.D = 0;
+  return ss;
+}
+
+StateSpace onepole_ss(float a) {  // cw.rs:40, state y
+  StateSpace ss;
+  ss.S = 1;
+  ss.A = {static_cast<double>(a)};
+  ss.D = 0;
+  return ss;
+}
+
+std::vector<double> mat_mul(const std::vector<double>& X, const std::vector<double>& Y, int S) {
+  std::vector<double> Z(S * S, 0.0);
+  for (int i = 0; i < S; ++i)
+    for (int k = 0; k < S; ++k)
+      for (int j = 0; j < S; ++j) Z[i * S + j] += X[i * S + k] * Y[k * S + j];
+  return Z;
+}
+
+std::vector<double> mat_pow(const std::vector<double>& A, int S, uint64_t k) {
+  std::vector<double> R(S * S, 0.0);
+  for (int i = 0; i < S; ++i) R[i * S + i] = 1.0;
+  std::vector<double> P = A;
+  while (k) {
+    if (k & 1) R = mat_mul(R, P, S);
+    P = mat_mul(P, P, S);
+    k >>= 1;
+  }
+  return R;
+}
+
+}  // namespace orion

@@ -1,0 +1,94 @@
+// hip_common.hpp — shared device/host helpers for the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace orion {
+
+// cf32 as a packed pair: lane-level complex math maps onto v_pk_fma_f32 / v_pk_mul_f32.
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+struct HipError : std::runtime_error {
+  explicit HipError(const std::string& s) : std::runtime_error(s) {}
+};
+
+#define ORION_HIP(expr)                                                                    \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      throw ::orion::HipError(std::string(#expr) + ": " + hipGetErrorString(_e) + " @" +   \
+                              __FILE__ + ":" + std::to_string(__LINE__));                  \
+  } while (0)
+
+#define ORION_LAUNCH_CHECK() ORION_HIP(hipGetLastError())
+
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 splat2(float x) { return f2{x, x}; }
+
+// Complex multiply as the reference's Rotator::rotate_block writes it
+// (dsp/rotator.rs:80-83): re = fma(a, p.re, -(b*p.im)), im = fma(b, p.re, a*p.im).
+__device__ __forceinline__ f2 cmul_rot(f2 x, f2 p) {
+  return f2{__builtin_fmaf(x.x, p.x, -(x.y * p.y)), __builtin_fmaf(x.y, p.x, x.x * p.y)};
+}
+// Plain complex multiply (ours, not a reference op order).
+__device__ __forceinline__ f2 cmul(f2 a, f2 b) {
+  return f2{__builtin_fmaf(a.x, b.x, -(a.y * b.y)), __builtin_fmaf(a.x, b.y, a.y * b.x)};
+}
+
+// Exact oscillator phase: phasor for absolute step count k is e^{j*theta*k}
+// with theta/2pi = step_q64 / 2^64. (k*step) mod 2^64 is exact integer math;
+// the top 24 bits give an exactly representable f32 turn count for
+// sincospif, the remaining 40 bits a first-order correction (< 3.8e-7 rad, so
+// the neglected second-order term is < 1e-13).
+__device__ __forceinline__ f2 phasor_q64(uint64_t k, uint64_t step_q64) {
+  const uint64_t ph = k * step_q64;
+  const uint32_t hi24 = static_cast<uint32_t>(ph >> 40);
+  const uint64_t lo40 = ph & ((1ull << 40) - 1);
+  const float t2 = static_cast<float>(hi24) * (1.0f / 8388608.0f);  // 2*turns in [0,2)
+  float s, c;
+  sincospif(t2, &s, &c);
+  const float d = static_cast<float>(lo40) * (6.28318530717958647692f / 1099511627776.0f) *
+                  (1.0f / 16777216.0f);  // 2*pi * lo40 / 2^64
+  return f2{__builtin_fmaf(-s, d, c), __builtin_fmaf(c, d, s)};
+}
+
+// util.rs:305-322 atan2_approx, restated op for op (no contraction: this TU is
+// built with -ffp-contract=off, and the division is IEEE).
+__device__ __forceinline__ float atan2_approx(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const bool swap = ax < ay;
+  const float mn = swap ? ax : ay;
+  const float mx = swap ? ay : ax;
+  const float r = mn / (mx + 1.1920929e-7f);
+  const float r2 = r * r;
+  float phi = r * (0.7853981633974483f + r2 * (-0.2447f + r2 * 0.0663f));
+  if (swap) phi = 1.5707963267948966f - phi;
+  const float sgn = (y < 0.0f) ? -1.0f : 1.0f;
+  return (x < 0.0f) ? (3.14159265358979323846f - phi) * sgn : phi * sgn;
+}
+
+// FmQuadratureDemod discriminator input, demodulate/fm.rs:62-65 (non-FMA):
+// prod = (z.re*p.re + z.im*p.im, z.im*p.re - z.re*p.im).
+__device__ __forceinline__ float fm_disc(f2 z, f2 p, float k) {
+  const float pr = z.x * p.x + z.y * p.y;
+  const float pi = z.y * p.x - z.x * p.y;
+  return atan2_approx(pi, pr) * k;
+}
+
+// PmQuadratureDemod, demodulate/pm.rs:56-57: num-complex z * conj(prev),
+// re = a*c - b*d, im = a*d + b*c with (c, d) = (p.re, -p.im); then k*atan2.
+__device__ __forceinline__ float pm_disc(f2 z, f2 p, float k) {
+  const float c = p.x, d = -p.y;
+  const float wr = z.x * c - z.y * d;
+  const float wi = z.x * d + z.y * c;
+  return k * atan2_approx(wi, wr);
+}
+
+inline int div_up(long long a, long long b) { return static_cast<int>((a + b - 1) / b); }
+
+}  // namespace orion

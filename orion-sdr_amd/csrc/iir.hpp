@@ -1,0 +1,103 @@
+// iir.hpp — the reference's IIR recurrences (exact per-sample op order) and the
+// wave-level state-carry scan that parallelises them on gfx950.
+//
+// Every recurrence here is affine in its state: s' = A s + B x. A lane runs the
+// reference update over C consecutive samples from a zero state (its aggregate),
+// the 64 lanes of a wave combine aggregates with a Kogge-Stone scan using the
+// precomputed chunk-transition matrices (A^C)^(2^s), and each lane re-runs its
+// chunk from the exact incoming state. The re-run is the reference's own
+// update, so only the incoming state carries scan rounding (~1 ulp of the state).
+#pragma once
+#include "hip_common.hpp"
+
+namespace orion {
+
+// dsp/iir.rs:34-40 Biquad::process, TDF-II:
+//   y = fma(x,b0,z1); z1 = fma(x,b1,z2) - a1*y; z2 = x*b2 - a2*y.
+struct BiquadK {
+  float b0, b1, b2, a1, a2;
+  __device__ __forceinline__ float step(float& z1, float& z2, float x) const {
+    const float y = __builtin_fmaf(x, b0, z1);
+    z1 = __builtin_fmaf(x, b1, z2) - a1 * y;
+    z2 = x * b2 - a2 * y;
+    return y;
+  }
+};
+
+// dsp/iir.rs:79-83 LpCascade::process — two identical biquads. State order
+// (z0_1, z0_2, z1_1, z1_2) matches design.cpp lp_cascade_ss.
+struct RecLP4 {
+  static constexpr int S = 4;
+  BiquadK bq;
+  __device__ __forceinline__ float step(float (&s)[S], float x) const {
+    const float y0 = bq.step(s[0], s[1], x);
+    return bq.step(s[2], s[3], y0);
+  }
+};
+
+// dsp/iir.rs:151-165 LpDcCascade::process: LP4 then y = y1 - x1 + r*y1_prev.
+// State (z0_1, z0_2, z1_1, z1_2, dc_x1, dc_y1) = design.cpp lpdc_ss.
+struct RecLpDc {
+  static constexpr int S = 6;
+  BiquadK bq;
+  float r;
+  __device__ __forceinline__ float step(float (&s)[S], float x) const {
+    const float y0 = bq.step(s[0], s[1], x);
+    const float y1 = bq.step(s[2], s[3], y0);
+    const float y = y1 - s[4] + r * s[5];
+    s[4] = y1;
+    s[5] = y;
+    return y;
+  }
+};
+
+// dsp/dc.rs:47-51 DcBlocker: y = x - x1 + r*y1; state (x1, y1) = design.cpp dc_ss.
+struct RecDC {
+  static constexpr int S = 2;
+  float r;
+  __device__ __forceinline__ float step(float (&s)[S], float x) const {
+    const float y = x - s[0] + r * s[1];
+    s[0] = x;
+    s[1] = y;
+    return y;
+  }
+};
+
+// demodulate/cw.rs:40: y = a*y + (1-a)*mag.
+struct RecOnePole {
+  static constexpr int S = 1;
+  float a;
+  __device__ __forceinline__ float step(float (&s)[S], float x) const {
+    s[0] = a * s[0] + (1.0f - a) * x;
+    return s[0];
+  }
+};
+
+template <int S>
+__device__ __forceinline__ void matvec_acc(const float* __restrict__ Mx, const float (&v)[S],
+                                           float (&acc)[S]) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    float a = acc[i];
+#pragma unroll
+    for (int j = 0; j < S; ++j) a = __builtin_fmaf(Mx[i * S + j], v[j], a);
+    acc[i] = a;
+  }
+}
+
+// Inclusive Kogge-Stone over the 64 lanes of a wave:
+//   Q_L = agg_L + A^C * Q_{L-1}, using pw[s] = (A^C)^(2^s) (S*S floats each, uniform).
+template <int S>
+__device__ __forceinline__ void wave_scan_inclusive(float (&q)[S], const float* __restrict__ pw,
+                                                    int lane) {
+#pragma unroll 1
+  for (int s = 0; s < 6; ++s) {
+    const int d = 1 << s;
+    float o[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) o[i] = __shfl_up(q[i], d, 64);
+    if (lane >= d) matvec_acc<S>(pw + s * S * S, o, q);
+  }
+}
+
+}  // namespace orion

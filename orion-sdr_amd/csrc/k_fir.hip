@@ -1,0 +1,320 @@
+// k_fir.hip — standalone NCO and FIR-family kernels for gfx950.
+//   Rotator::rotate_block / mix_usb_block   dsp/rotator.rs:74-94
+//   FirDecimator::process                   dsp/decim.rs:44-76 (kept outputs only)
+//   FirLowpass::process                     dsp/fir.rs:47-66   (real)
+//   FirLowpassIq::process / filter_aligned  dsp/fir.rs:229-297 (complex, real taps)
+#include "kernels.hpp"
+#include "poly.hpp"
+
+namespace orion {
+namespace {
+
+constexpr int NT = 256;
+constexpr int kMaxGrid = 2048;  // memory-bound: cap and grid-stride (2048 = 8 WG per CU)
+
+// ------------------------------------------------------------------ NCO --
+template <bool A16, bool USB>
+__global__ __launch_bounds__(NT) void k_rotator(const f2* __restrict__ x, void* __restrict__ yv,
+                                                long long n, uint64_t k0, uint64_t step,
+                                                const f2* __restrict__ tab) {
+  constexpr int PER = kRotTile / (2 * NT);  // pairs per thread per tile (8)
+  const int t = threadIdx.x;
+  f2 tb[PER][2];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const f4 v = *reinterpret_cast<const f4*>(tab + 2 * t + 2 * NT * i);
+    tb[i][0] = f2{v.x, v.y};
+    tb[i][1] = f2{v.z, v.w};
+  }
+  for (long long base = static_cast<long long>(blockIdx.x) * kRotTile; base < n;
+       base += static_cast<long long>(gridDim.x) * kRotTile) {
+    const f2 S = phasor_q64(k0 + static_cast<uint64_t>(base) + 1, step);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const long long P = base + 2 * t + 2 * NT * i;
+      if (P >= n) break;
+      f2 v0, v1 = f2{0.0f, 0.0f};
+      const bool full = P + 1 < n;
+      if (A16 && full) {
+        const f4 v = *reinterpret_cast<const f4*>(x + P);
+        v0 = f2{v.x, v.y};
+        v1 = f2{v.z, v.w};
+      } else {
+        v0 = x[P];
+        if (full) v1 = x[P + 1];
+      }
+      const f2 p0 = cmul(S, tb[i][0]);
+      const f2 p1 = cmul(S, tb[i][1]);
+      if constexpr (USB) {
+        float* y = static_cast<float*>(yv);
+        y[P] = __builtin_fmaf(v0.x, p0.x, v0.y * p0.y);
+        if (full) y[P + 1] = __builtin_fmaf(v1.x, p1.x, v1.y * p1.y);
+      } else {
+        f2* y = static_cast<f2*>(yv);
+        const f2 o0 = cmul_rot(v0, p0), o1 = cmul_rot(v1, p1);
+        if (A16 && full) {
+          *reinterpret_cast<f4*>(y + P) = f4{o0.x, o0.y, o1.x, o1.y};
+        } else {
+          y[P] = o0;
+          if (full) y[P + 1] = o1;
+        }
+      }
+    }
+  }
+}
+
+// -------------------------------------------------- polyphase decimator --
+template <int Q, bool A16>
+__global__ __launch_bounds__(NT) void k_decim8(const f2* __restrict__ x, long long x_stride,
+                                               long long n, const f2* __restrict__ hist,
+                                               int hist_len, f2* __restrict__ out,
+                                               long long out_stride, long long n_out,
+                                               const Taps256 g) {
+  using P = Poly<8, Q, 512, NT>;
+  __shared__ __attribute__((aligned(16))) f2 U[P::LDS_F2];
+  const int t = threadIdx.x;
+  const int ch = blockIdx.y;
+  x += ch * x_stride;
+  hist += static_cast<long long>(ch) * hist_len;
+  out += ch * out_stride;
+  for (long long J = static_cast<long long>(blockIdx.x) * 512; J < n_out;
+       J += static_cast<long long>(gridDim.x) * 512) {
+    const long long porg = 8 * (J - Q);
+    for (int p = 2 * t; p < P::NS; p += 2 * NT) {
+      f2 v0, v1;
+      load_pair<A16>(x, n, hist, hist_len, porg + p, v0, v1);
+      U[P::slot(p)] = v0;
+      U[P::slot(p + 1)] = v1;
+    }
+    __syncthreads();
+    f2 acc[P::R];
+    P::compute(U, t, [&](int c, int q) { return g.g[c * Q + q]; }, acc);
+#pragma unroll
+    for (int r = 0; r < P::R; ++r) {
+      const long long j = J + P::R * t + r;
+      if (j < n_out) out[j] = acc[r];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_decim_generic(const f2* __restrict__ x, long long x_stride,
+                                                      long long n, const f2* __restrict__ hist,
+                                                      int hist_len, f2* __restrict__ out,
+                                                      long long out_stride, long long n_out, int M,
+                                                      int K, const float* __restrict__ g) {
+  const int ch = blockIdx.y;
+  x += ch * x_stride;
+  hist += static_cast<long long>(ch) * hist_len;
+  out += ch * out_stride;
+  for (long long j = static_cast<long long>(blockIdx.x) * NT + threadIdx.x; j < n_out;
+       j += static_cast<long long>(gridDim.x) * NT) {
+    f2 acc = f2{0.0f, 0.0f};
+    for (int k = 0; k < K; ++k)
+      acc = fma2(splat2(g[k]), load_hist(x, n, hist, hist_len, M * j - k), acc);
+    out[j] = acc;
+  }
+}
+
+// --------------------------------------------------------- real FIR -------
+// y[i] = sum_{k<KP} g[k] x[i-k], 512 outputs per sub-tile, 2 per lane.
+template <int KP>
+__global__ __launch_bounds__(NT) void k_fir_real(const float* __restrict__ x, long long n,
+                                                 const float* __restrict__ hist, int hist_len,
+                                                 float* __restrict__ y, const Taps256 g) {
+  constexpr int TT = 512;
+  static_assert(KP % 16 == 0, "taps padded to 16");
+  __shared__ __attribute__((aligned(16))) float L[TT + KP + 2];
+  const int t = threadIdx.x;
+  for (long long J = static_cast<long long>(blockIdx.x) * TT; J < n;
+       J += static_cast<long long>(gridDim.x) * TT) {
+    const long long org = J - KP;
+    for (int p = t; p < TT + KP + 2; p += NT) {
+      const long long P = org + p;
+      float v = 0.0f;
+      if (P >= 0) v = P < n ? x[P] : 0.0f;
+      else if (P >= -hist_len) v = hist[hist_len + P];
+      L[p] = v;
+    }
+    __syncthreads();
+    float acc0 = 0.0f, acc1 = 0.0f;
+    // element e <-> L[e - org]; outputs j = J + 2t (+1)
+    fir2_blocked<KP>(
+        [&](long long i, float& w0, float& w1) {
+          const f2 w = *reinterpret_cast<const f2*>(L + (i - org));
+          w0 = w.x;
+          w1 = w.y;
+        },
+        J + 2 * t, [&](int k) { return g.g[k]; }, acc0, acc1);
+    const long long j = J + 2 * t;
+    if (j < n) y[j] = acc0;
+    if (j + 1 < n) y[j + 1] = acc1;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_fir_real_generic(const float* __restrict__ x, long long n,
+                                                         const float* __restrict__ hist,
+                                                         int hist_len, float* __restrict__ y,
+                                                         int K, const float* __restrict__ g) {
+  for (long long i = static_cast<long long>(blockIdx.x) * NT + threadIdx.x; i < n;
+       i += static_cast<long long>(gridDim.x) * NT) {
+    float acc = 0.0f;
+    for (int k = 0; k < K; ++k) {
+      const long long P = i - k;
+      float v = 0.0f;
+      if (P >= 0) v = x[P];
+      else if (P >= -hist_len) v = hist[hist_len + P];
+      acc = __builtin_fmaf(g[k], v, acc);
+    }
+    y[i] = acc;
+  }
+}
+
+// ------------------------------------------------------ complex FIR -------
+template <int KP>
+__global__ __launch_bounds__(NT) void k_fir_iq(const f2* __restrict__ x, long long n,
+                                               const f2* __restrict__ hist, int hist_len,
+                                               f2* __restrict__ y, long long n_out, long long off,
+                                               const Taps256 g) {
+  constexpr int TT = 512;
+  __shared__ __attribute__((aligned(16))) f2 L[TT + KP + 2];
+  const int t = threadIdx.x;
+  for (long long J = static_cast<long long>(blockIdx.x) * TT; J < n_out;
+       J += static_cast<long long>(gridDim.x) * TT) {
+    const long long org = J + off - KP;
+    for (int p = t; p < TT + KP + 2; p += NT) L[p] = load_hist(x, n, hist, hist_len, org + p);
+    __syncthreads();
+    f2 acc0 = f2{0.0f, 0.0f}, acc1 = f2{0.0f, 0.0f};
+    // element e (= input index i + off) <-> L[e - org]
+    fir2_blocked<KP>(
+        [&](long long i, f2& w0, f2& w1) {
+          const f4 v = *reinterpret_cast<const f4*>(L + (i - org));
+          w0 = f2{v.x, v.y};
+          w1 = f2{v.z, v.w};
+        },
+        J + off + 2 * t, [&](int k) { return g.g[k]; }, acc0, acc1);
+    const long long j = J + 2 * t;
+    if (j < n_out) y[j] = acc0;
+    if (j + 1 < n_out) y[j + 1] = acc1;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_fir_iq_generic(const f2* __restrict__ x, long long n,
+                                                       const f2* __restrict__ hist, int hist_len,
+                                                       f2* __restrict__ y, long long n_out,
+                                                       long long off, int K,
+                                                       const float* __restrict__ g) {
+  for (long long i = static_cast<long long>(blockIdx.x) * NT + threadIdx.x; i < n_out;
+       i += static_cast<long long>(gridDim.x) * NT) {
+    f2 acc = f2{0.0f, 0.0f};
+    for (int k = 0; k < K; ++k) acc = fma2(splat2(g[k]), load_hist(x, n, hist, hist_len, i + off - k), acc);
+    y[i] = acc;
+  }
+}
+
+template <class V>
+__global__ void k_hist_update(const V* __restrict__ x, long long n, const V* __restrict__ old_h,
+                              V* __restrict__ new_h, int hist_len) {
+  for (int i = threadIdx.x; i < hist_len; i += blockDim.x) {
+    const long long P = n - hist_len + i;
+    new_h[i] = P >= 0 ? x[P] : old_h[hist_len + P];
+  }
+}
+
+inline int grid_for(long long work, int per_block) {
+  long long g = (work + per_block - 1) / per_block;
+  if (g > kMaxGrid) g = kMaxGrid;
+  return g < 1 ? 1 : static_cast<int>(g);
+}
+
+}  // namespace
+
+void launch_rotator(const f2* x, f2* y, long long n, uint64_t k0, uint64_t step, const f2* tab,
+                    hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = grid_for(n, kRotTile);
+  const bool a16 = reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(y) % 16 == 0;
+  if (a16) k_rotator<true, false><<<grid, NT, 0, s>>>(x, y, n, k0, step, tab);
+  else k_rotator<false, false><<<grid, NT, 0, s>>>(x, y, n, k0, step, tab);
+  ORION_LAUNCH_CHECK();
+}
+
+void launch_mix_usb(const f2* x, float* y, long long n, uint64_t k0, uint64_t step, const f2* tab,
+                    hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = grid_for(n, kRotTile);
+  if (reinterpret_cast<uintptr_t>(x) % 16 == 0) k_rotator<true, true><<<grid, NT, 0, s>>>(x, y, n, k0, step, tab);
+  else k_rotator<false, true><<<grid, NT, 0, s>>>(x, y, n, k0, step, tab);
+  ORION_LAUNCH_CHECK();
+}
+
+void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* hist, int hist_len,
+                        f2* out, long long out_stride, long long n_out, int nch, int M, int K,
+                        const Taps256& g, const float* g_dev, hipStream_t s) {
+  if (n_out <= 0 || nch <= 0) return;
+  const bool a16 = reinterpret_cast<uintptr_t>(x) % 16 == 0 && x_stride % 2 == 0;
+  // Fast polyphase path: M = 8 with K <= 128 / 256 taps; grid spread so that the
+  // whole launch has >= 2048 workgroups when channels allow.
+  if (M == 8 && K <= 256 && hist_len >= 8 * (K <= 128 ? 16 : 32)) {
+    const long long tiles = (n_out + 511) / 512;
+    long long gx = tiles;
+    const long long cap = (4 * kMaxGrid) / nch > 0 ? (4 * kMaxGrid) / nch : 1;
+    if (gx > cap) gx = cap;
+    const dim3 grid(static_cast<unsigned>(gx), nch);
+    if (K <= 128) {
+      if (a16) k_decim8<16, true><<<grid, NT, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g);
+      else k_decim8<16, false><<<grid, NT, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g);
+    } else {
+      if (a16) k_decim8<32, true><<<grid, NT, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g);
+      else k_decim8<32, false><<<grid, NT, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g);
+    }
+  } else {
+    const dim3 grid(grid_for(n_out, NT), nch);
+    k_decim_generic<<<grid, NT, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, M, K, g_dev);
+  }
+  ORION_LAUNCH_CHECK();
+}
+
+void launch_decim(const f2* x, long long n, const f2* hist, int hist_len, f2* out, long long n_out,
+                  int M, int K, const Taps256& g, const float* g_dev, hipStream_t s) {
+  launch_decim_batch(x, n, n, hist, hist_len, out, n_out, n_out, 1, M, K, g, g_dev, s);
+}
+
+void launch_fir_real(const float* x, long long n, const float* hist, int hist_len, float* y, int K,
+                     const Taps256& g, const float* g_dev, hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = grid_for(n, 512);
+  if (K <= 64 && hist_len >= 64) k_fir_real<64><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, g);
+  else if (K <= 128 && hist_len >= 128) k_fir_real<128><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, g);
+  else if (K <= 256 && hist_len >= 256) k_fir_real<256><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, g);
+  else k_fir_real_generic<<<grid_for(n, NT), NT, 0, s>>>(x, n, hist, hist_len, y, K, g_dev);
+  ORION_LAUNCH_CHECK();
+}
+
+void launch_fir_iq(const f2* x, long long n, const f2* hist, int hist_len, f2* y, long long n_out,
+                   long long off, int K, const Taps256& g, const float* g_dev, hipStream_t s) {
+  if (n_out <= 0) return;
+  const int grid = grid_for(n_out, 512);
+  if (K <= 64 && hist_len >= 64) k_fir_iq<64><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
+  else if (K <= 128 && hist_len >= 128) k_fir_iq<128><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
+  else if (K <= 256 && hist_len >= 256) k_fir_iq<256><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
+  else k_fir_iq_generic<<<grid_for(n_out, NT), NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, K, g_dev);
+  ORION_LAUNCH_CHECK();
+}
+
+void launch_hist_update_c(const f2* x, long long n, const f2* old_h, f2* new_h, int hist_len,
+                          hipStream_t s) {
+  if (hist_len <= 0) return;
+  k_hist_update<f2><<<1, NT, 0, s>>>(x, n, old_h, new_h, hist_len);
+  ORION_LAUNCH_CHECK();
+}
+void launch_hist_update_r(const float* x, long long n, const float* old_h, float* new_h,
+                          int hist_len, hipStream_t s) {
+  if (hist_len <= 0) return;
+  k_hist_update<float><<<1, NT, 0, s>>>(x, n, old_h, new_h, hist_len);
+  ORION_LAUNCH_CHECK();
+}
+
+}  // namespace orion

@@ -1,0 +1,82 @@
+// kernels.hpp — launch interfaces of the gfx950 kernels (host side).
+// Every pointer named *_dev is device memory; every launch is asynchronous on
+// the given stream and allocation-free (graph-capturable).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hip_common.hpp"
+
+namespace orion {
+
+// ---------------------------------------------------------------- NCO --
+// Rotator::rotate_block (dsp/rotator.rs:74-85) in closed form: output i uses the
+// phasor after k0+i+1 steps, e^{j theta (k0+i+1)}. tab_dev = e^{j theta p},
+// p < kRotTile.
+constexpr int kRotTile = 4096;
+void launch_rotator(const f2* x_dev, f2* y_dev, long long n, uint64_t k0, uint64_t step_q64,
+                    const f2* tab_dev, hipStream_t s);
+// SsbProductDemod front end helper / Rotator::mix_usb_block (rotator.rs:88-94):
+// y = fma(x.re, p.re, x.im*p.im).
+void launch_mix_usb(const f2* x_dev, float* y_dev, long long n, uint64_t k0, uint64_t step_q64,
+                    const f2* tab_dev, hipStream_t s);
+
+// ---------------------------------------------------------- FIR family --
+// Decimating FIR at the kept outputs only: out[j] = sum_k g[k] * x[M*j - k],
+// j < n_out, with x[P<0] from hist (hist_len samples ending at x[-1]).
+struct Taps256 { float g[256]; };
+void launch_decim(const f2* x_dev, long long n, const f2* hist_dev, int hist_len, f2* out_dev,
+                  long long n_out, int M, int K, const Taps256& g, const float* g_dev,
+                  hipStream_t s);
+// Batched over channels: x[ch*x_stride + i], out[ch*out_stride + j], shared taps.
+void launch_decim_batch(const f2* x_dev, long long x_stride, long long n, const f2* hist_dev,
+                        int hist_len, f2* out_dev, long long out_stride, long long n_out, int nch,
+                        int M, int K, const Taps256& g, const float* g_dev, hipStream_t s);
+// Real FIR y[i] = sum_k g[k] x[i-k] (x[P<0] from hist).
+void launch_fir_real(const float* x_dev, long long n, const float* hist_dev, int hist_len,
+                     float* y_dev, int K, const Taps256& g, const float* g_dev, hipStream_t s);
+// Complex-sample real-tap FIR y[i] = sum_k g[k] x[i + off - k], i < n_out
+// (x[P<0] from hist, x[P>=n] = 0). off = 0: streaming; off = (K-1)/2 with an
+// all-zero history: FirLowpassIq::filter_aligned.
+void launch_fir_iq(const f2* x_dev, long long n, const f2* hist_dev, int hist_len, f2* y_dev,
+                   long long n_out, long long off, int K, const Taps256& g, const float* g_dev,
+                   hipStream_t s);
+// Copy the last hist_len samples of [old_hist | x[0..n)] into new_hist.
+void launch_hist_update_c(const f2* x_dev, long long n, const f2* old_dev, f2* new_dev,
+                          int hist_len, hipStream_t s);
+void launch_hist_update_r(const float* x_dev, long long n, const float* old_dev, float* new_dev,
+                          int hist_len, hipStream_t s);
+
+// ----------------------------------------------------------- WBFM fused --
+// One pass: NCO mix -> polyphase decim x8 (<=128 taps) -> FM discriminator ->
+// LpCascade (wave scan, warm-up across workgroups) -> audio FIR (<=128 taps).
+constexpr int kWbfmM = 8;
+constexpr int kWbfmQ = 16;
+constexpr int kWbfmT = 512;                    // decimated outputs per sub-tile
+constexpr int kWbfmNS = kWbfmM * (kWbfmT + kWbfmQ);  // staged input samples per sub-tile
+constexpr int kWbfmHist = kWbfmM * kWbfmQ;     // raw input history (128)
+constexpr int kWbfmCarry = 8 + 128;            // iir[4], prev[2], pad[2], fhist[128]
+struct WbfmConst {
+  float g[128];      // decimator taps g[8q+c] stored phase-major at [c*16+q]; quirk-mapped
+                     // (g[0]=h[L-1], g[k]=h[k-1]), zero padded
+  float a[128];      // audio taps, quirk-mapped, zero padded
+  float b0, b1, b2, a1, a2;  // LpCascade biquad
+  float k;           // 1/dev (fm.rs:23)
+  float m8[16];      // A^8 (chunk transition, 8 samples per lane)
+  float pw[6 * 16];  // (A^8)^(2^s), s = 0..5
+};
+struct WbfmArgs {
+  const f2* x;  long long x_stride;  long long n;
+  float* y;     long long y_stride;  long long n_dec;
+  long long k0;                      // samples consumed by earlier calls
+  const uint64_t* step;              // [nch]
+  const f2* tab;                     // [nch][kWbfmNS] e^{j theta p}
+  const float* carry_in; float* carry_out;   // [nch][kWbfmCarry]
+  const f2* hist_in; f2* hist_out;           // [nch][kWbfmHist]
+  int A;                             // decimated outputs per workgroup
+  int wpre;                          // warm-up outputs before each workgroup's range
+};
+void launch_wbfm(const WbfmArgs& a, const WbfmConst& c, int nch, hipStream_t s);
+
+}  // namespace orion

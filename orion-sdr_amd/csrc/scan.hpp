@@ -1,0 +1,80 @@
+// scan.hpp — chunked state-carry scan for the reference's stateful recurrences.
+//
+// Blocks whose output depends on an IIR state (LpCascade, LpDcCascade,
+// DcBlocker, the CW one-pole, and the demodulators built on them) run as three
+// launches per call:
+//   agg   : every workgroup (CH = 4096 samples, 16 per lane) runs the reference
+//           update from a zero state and reduces its lanes' end states to one
+//           workgroup aggregate (wave Kogge-Stone + cross-wave combine);
+//   carry : one workgroup per channel scans the aggregates with the carried
+//           stream state -> the exact state entering every workgroup;
+//   apply : every workgroup recomputes its lane aggregates, derives each lane's
+//           exact entering state and re-runs the reference update to produce
+//           outputs; the workgroup holding the last sample stores the carried
+//           state for the next call.
+// Inputs are staged through LDS with coalesced loads; LDS rows are padded one
+// slot every 16 so the 16-samples-per-lane reads are bank-conflict free.
+#pragma once
+#include <cstdint>
+
+#include "hip_common.hpp"
+#include "iir.hpp"
+
+namespace orion {
+
+constexpr int kScanC = 16;                 // samples per lane
+constexpr int kScanNT = 256;               // lanes per workgroup
+constexpr int kScanCH = kScanC * kScanNT;  // samples per workgroup (4096)
+constexpr int kScanCarry = 8;              // carried floats per channel: state[<=6], prev[2]
+
+// Front ends (the per-sample map before the recurrence), one per reference block.
+enum class Pre : int {
+  Real = 0,    // f32 input (LpCascade / DcBlocker blocks)
+  Fm = 1,      // demodulate/fm.rs:60-68 (optionally translated, fm.rs:48-58)
+  Pm = 2,      // demodulate/pm.rs:54-58
+  Ssb = 3,     // demodulate/ssb.rs:33-38 (BFO rotator)
+  AmSqrt = 4,  // demodulate/am.rs:201-205, LP stage before the sqrt map
+  AmAbs = 5,   // demodulate/am.rs:232-239
+  Cw = 6,      // demodulate/cw.rs:38-39
+};
+enum class Post : int { Id = 0, Sqrt = 1, Gain = 2 };
+enum class RecK : int { LP4 = 0, LPDC = 1, DC = 2, ONEPOLE = 3 };
+
+// Matrices of the chunk transition, all S x S row-major f32, in one device buffer.
+struct ScanMatsLayout {
+  static constexpr int kPwc = 0;    // (A^C)^(2^s), s = 0..5
+  static constexpr int kM64 = 6;    // A^(64C)
+  static constexpr int kPch = 7;    // (A^CH)^(2^s), s = 0..7
+  static constexpr int kLane = 15;  // A^(C*L), L = 0..63
+  static constexpr int kCount = 79;
+};
+
+struct ScanCoef {
+  float b0, b1, b2, a1, a2;  // biquad (LP4 / LPDC)
+  float r;                   // DC pole (LPDC / DC)
+  float a;                   // one-pole (CW)
+  float k;                   // discriminator gain (FM: 1/dev, PM: k)
+  float k1, k2;              // AM AbsApprox
+  float gain;                // CW set_gain
+};
+
+struct ScanArgs {
+  const void* x;  long long x_stride;  // inputs: cf32 or f32, [ch][x_stride]
+  void* y;        long long y_stride;  // outputs: f32, [ch][y_stride]
+  long long n;                         // samples this call
+  long long k0;                        // samples consumed by earlier calls (oscillators)
+  int translate;                       // Pre::Fm: apply the fm.rs:48-58 translator
+  uint64_t step;                       // oscillator Q0.64 step (translator / BFO)
+  const f2* tab;                       // e^{j theta p}, p < kScanCH (oscillator table)
+  const float* mats;                   // ScanMatsLayout
+  float* aggs;                         // [ch][nblk][S]
+  float* sin;                          // [ch][nblk][S] state entering each workgroup
+  const float* carry_in;               // [ch][kScanCarry]
+  float* carry_out;                    // [ch][kScanCarry]
+  ScanCoef c;
+};
+
+void launch_scan(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, hipStream_t s);
+int scan_state_dim(RecK rec);
+
+}  // namespace orion

@@ -1,0 +1,292 @@
+// scan_blocks.cpp — stateful IIR / demodulator Blocks over the scan kernels.
+#include "scan_blocks.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+#include "scan.hpp"
+
+namespace orion {
+namespace {
+
+std::vector<float> to_f32(const std::vector<double>& m) {
+  std::vector<float> r(m.size());
+  for (size_t i = 0; i < m.size(); ++i) r[i] = static_cast<float>(m[i]);
+  return r;
+}
+
+// One recurrence stage: rec/pre/post choice, transition matrices, carried state.
+class ScanStage {
+ public:
+  ScanStage(RecK rec, Pre pre, Post post, const StateSpace& ss, const ScanCoef& c, int nch)
+      : rec_(rec), pre_(pre), post_(post), c_(c), nch_(nch), S_(ss.S) {
+    const int S = S_;
+    std::vector<float> mats(static_cast<size_t>(ScanMatsLayout::kCount) * S * S, 0.0f);
+    auto put = [&](int idx, const std::vector<double>& m) {
+      const auto f = to_f32(m);
+      std::copy(f.begin(), f.end(), mats.begin() + static_cast<size_t>(idx) * S * S);
+    };
+    const auto Mc = mat_pow(ss.A, S, kScanC);
+    auto p = Mc;
+    for (int s = 0; s < 6; ++s) {
+      put(ScanMatsLayout::kPwc + s, p);
+      p = mat_mul(p, p, S);
+    }
+    put(ScanMatsLayout::kM64, mat_pow(ss.A, S, 64ull * kScanC));
+    p = mat_pow(ss.A, S, kScanCH);
+    for (int s = 0; s < 8; ++s) {
+      put(ScanMatsLayout::kPch + s, p);
+      p = mat_mul(p, p, S);
+    }
+    for (int L = 0; L < 64; ++L) put(ScanMatsLayout::kLane + L, mat_pow(ss.A, S, static_cast<uint64_t>(kScanC) * L));
+    mats_.upload(mats.data(), mats.size() * sizeof(float));
+    for (auto& c0 : carry_) c0.resize(static_cast<size_t>(nch_) * kScanCarry * sizeof(float));
+  }
+  void set_osc(const Oscillator& o) {
+    step_ = o.step_q64;
+    const auto t = phasor_table(o.theta, kScanCH);
+    tab_.upload(t.data(), t.size() * sizeof(float));
+  }
+  void set_carry(const std::vector<float>& per_ch) {  // kScanCarry floats, same for every channel
+    std::vector<float> c(static_cast<size_t>(nch_) * kScanCarry);
+    for (int ch = 0; ch < nch_; ++ch) std::copy(per_ch.begin(), per_ch.end(), c.begin() + ch * kScanCarry);
+    for (auto& c0 : carry_) c0.upload(c.data(), c.size() * sizeof(float));
+    cur_ = 0;
+  }
+  ScanCoef& coef() { return c_; }
+  void set_translate(bool on) { translate_ = on; }
+  void run(const void* x, long long x_stride, long long n, void* y, long long y_stride, long long k0,
+           hipStream_t s) {
+    const long long nblk = (n + kScanCH - 1) / kScanCH;
+    ws_.resize(static_cast<size_t>(2 * nblk * nch_ * S_ + 16) * sizeof(float));
+    ScanArgs a{};
+    a.x = x;
+    a.x_stride = x_stride;
+    a.y = y;
+    a.y_stride = y_stride;
+    a.n = n;
+    a.k0 = k0;
+    a.translate = translate_ ? 1 : 0;
+    a.step = step_;
+    a.tab = tab_.size() ? tab_.as<f2>() : nullptr;
+    a.mats = mats_.as<float>();
+    a.aggs = ws_.as<float>();
+    a.sin = ws_.as<float>() + nblk * nch_ * S_;
+    a.carry_in = carry_[cur_].as<float>();
+    a.carry_out = carry_[cur_ ^ 1].as<float>();
+    a.c = c_;
+    launch_scan(rec_, pre_, post_, a, nch_, s);
+    cur_ ^= 1;
+  }
+
+ private:
+  RecK rec_;
+  Pre pre_;
+  Post post_;
+  ScanCoef c_;
+  int nch_, S_;
+  bool translate_ = false;
+  uint64_t step_ = 0;
+  DevBuf mats_, tab_, carry_[2], ws_;
+  int cur_ = 0;
+};
+
+ScanCoef coef_lp(const BiquadCoeffs& b) {
+  ScanCoef c{};
+  c.b0 = b.b0; c.b1 = b.b1; c.b2 = b.b2; c.a1 = b.a1; c.a2 = b.a2;
+  return c;
+}
+
+// Generic single-stage f32/cf32 -> f32 block.
+class ScanBlock : public Block {
+ public:
+  ScanBlock(const char* nm, Dt in, int nch) : nm_(nm), in_(in), nch_(nch) {}
+  const char* name() const override { return nm_; }
+  Dt in_type() const override { return in_; }
+  Dt out_type() const override { return Dt::F32; }
+  int channels() const override { return nch_; }
+  WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
+    const size_t n = std::min(n_in, out_cap);  // 1:1 blocks: min(in, out)
+    if (n == 0) return {0, 0};
+    run(in, n_in, n, out, out_cap, s);
+    k0_ += n;
+    return {n, n};
+  }
+  void reset() override {
+    k0_ = 0;
+    reset_state();
+    ORION_HIP(hipDeviceSynchronize());
+  }
+
+ protected:
+  virtual void run(const void* in, size_t stride, size_t n, void* out, size_t out_stride, hipStream_t s) = 0;
+  virtual void reset_state() = 0;
+  const char* nm_;
+  Dt in_;
+  int nch_;
+  uint64_t k0_ = 0;
+};
+
+class OneStageBlock : public ScanBlock {
+ public:
+  OneStageBlock(const char* nm, Dt in, int nch, std::unique_ptr<ScanStage> st, std::vector<float> carry0)
+      : ScanBlock(nm, in, nch), st_(std::move(st)), carry0_(std::move(carry0)) {
+    reset_state();
+  }
+  ScanStage& stage() { return *st_; }
+  std::vector<float> taps(int) const override { return coef_; }
+  std::vector<float> coef_;
+
+ protected:
+  void run(const void* in, size_t stride, size_t n, void* out, size_t out_stride, hipStream_t s) override {
+    st_->run(in, static_cast<long long>(stride), static_cast<long long>(n), out, static_cast<long long>(out_stride),
+             static_cast<long long>(k0_), s);
+  }
+  void reset_state() override { st_->set_carry(carry0_); }
+  std::unique_ptr<ScanStage> st_;
+  std::vector<float> carry0_;
+};
+
+std::vector<float> carry_zero() { return std::vector<float>(kScanCarry, 0.0f); }
+std::vector<float> carry_prev_one() {  // FM/PM: prev = 1 + 0j (fm.rs:29, pm.rs:31)
+  auto c = carry_zero();
+  c[6] = 1.0f;
+  return c;
+}
+
+// AM envelope: PowerSqrt = LP4 -> sqrt -> DC (two scans through a temp buffer);
+// AbsApprox = one LpDc scan.
+class AmBlock final : public ScanBlock {
+ public:
+  AmBlock(float fs, float bw) : ScanBlock("AmEnvelopeDemod", Dt::C32, 1) {
+    d_ = lpdc_design(fs, bw * 0.9f, 2.0f);  // am.rs:27
+    ScanCoef c = coef_lp(d_.bq);
+    c.r = d_.r;
+    lp_ = std::make_unique<ScanStage>(RecK::LP4, Pre::AmSqrt, Post::Sqrt, lp_cascade_ss(d_.bq), c, 1);
+    dc_ = std::make_unique<ScanStage>(RecK::DC, Pre::Real, Post::Id, dc_ss(d_.r), c, 1);
+    lpdc_ = std::make_unique<ScanStage>(RecK::LPDC, Pre::AmAbs, Post::Id, lpdc_ss(d_), c, 1);
+    reset_state();
+  }
+  void set_abs(float k1, float k2) {
+    abs_ = true;
+    lpdc_->coef().k1 = k1;
+    lpdc_->coef().k2 = k2;
+  }
+  std::vector<float> taps(int) const override {
+    return {d_.bq.b0, d_.bq.b1, d_.bq.b2, d_.bq.a1, d_.bq.a2, d_.r};
+  }
+
+ protected:
+  void run(const void* in, size_t stride, size_t n, void* out, size_t out_stride, hipStream_t s) override {
+    if (abs_) {
+      lpdc_->run(in, static_cast<long long>(stride), static_cast<long long>(n), out, static_cast<long long>(out_stride),
+                 static_cast<long long>(k0_), s);
+      return;
+    }
+    tmp_.resize(n * sizeof(float) + 16);
+    lp_->run(in, static_cast<long long>(stride), static_cast<long long>(n), tmp_.as<void>(), static_cast<long long>(n),
+             static_cast<long long>(k0_), s);
+    dc_->run(tmp_.as<void>(), static_cast<long long>(n), static_cast<long long>(n), out,
+             static_cast<long long>(out_stride), static_cast<long long>(k0_), s);
+  }
+  void reset_state() override {
+    lp_->set_carry(carry_zero());
+    dc_->set_carry(carry_zero());
+    lpdc_->set_carry(carry_zero());
+  }
+
+ private:
+  LpDcCoeffs d_;
+  bool abs_ = false;
+  std::unique_ptr<ScanStage> lp_, dc_, lpdc_;
+  DevBuf tmp_;
+};
+
+}  // namespace
+
+std::unique_ptr<Block> make_lp_cascade(float fs, float fc) {
+  const BiquadCoeffs b = lp_cascade_design(fs, fc);
+  auto st = std::make_unique<ScanStage>(RecK::LP4, Pre::Real, Post::Id, lp_cascade_ss(b), coef_lp(b), 1);
+  auto blk = std::make_unique<OneStageBlock>("LpCascade", Dt::F32, 1, std::move(st), carry_zero());
+  blk->coef_ = {b.b0, b.b1, b.b2, b.a1, b.a2};
+  return blk;
+}
+
+std::unique_ptr<Block> make_dc_blocker(float fs, float cut_hz) {
+  const float r = dc_blocker_pole(fs, cut_hz);
+  ScanCoef c{};
+  c.r = r;
+  auto st = std::make_unique<ScanStage>(RecK::DC, Pre::Real, Post::Id, dc_ss(r), c, 1);
+  auto blk = std::make_unique<OneStageBlock>("DcBlocker", Dt::F32, 1, std::move(st), carry_zero());
+  blk->coef_ = {r};
+  return blk;
+}
+
+std::unique_ptr<Block> make_fm_demod(float fs, float dev_hz, float audio_bw) {
+  const BiquadCoeffs b = lp_cascade_design(fs, audio_bw * 0.9f);  // fm.rs:24
+  ScanCoef c = coef_lp(b);
+  c.k = 1.0f / std::max(dev_hz, 1.0f);  // fm.rs:23
+  auto st = std::make_unique<ScanStage>(RecK::LP4, Pre::Fm, Post::Id, lp_cascade_ss(b), c, 1);
+  auto blk = std::make_unique<OneStageBlock>("FmQuadratureDemod", Dt::C32, 1, std::move(st), carry_prev_one());
+  blk->coef_ = {b.b0, b.b1, b.b2, b.a1, b.a2, c.k, fs};
+  return blk;
+}
+
+int fm_demod_with_translate(Block* b, float freq_hz) {
+  auto* o = dynamic_cast<OneStageBlock*>(b);
+  if (!o || std::strcmp(b->name(), "FmQuadratureDemod") != 0) return -4;
+  o->stage().set_osc(oscillator(freq_hz, o->coef_[6]));  // Rotator::new(freq_hz, fs), fm.rs:35
+  o->stage().set_translate(true);
+  return 0;
+}
+
+std::unique_ptr<Block> make_pm_demod(float fs, float k, float audio_bw) {
+  const BiquadCoeffs b = lp_cascade_design(fs, audio_bw * 0.9f);  // pm.rs:27
+  ScanCoef c = coef_lp(b);
+  c.k = k;
+  auto st = std::make_unique<ScanStage>(RecK::LP4, Pre::Pm, Post::Id, lp_cascade_ss(b), c, 1);
+  auto blk = std::make_unique<OneStageBlock>("PmQuadratureDemod", Dt::C32, 1, std::move(st), carry_prev_one());
+  blk->coef_ = {b.b0, b.b1, b.b2, b.a1, b.a2, k};
+  return blk;
+}
+
+std::unique_ptr<Block> make_ssb_demod(float fs, float bfo_hz, float audio_bw, int nch) {
+  const LpDcCoeffs d = lpdc_design(fs, audio_bw * 0.9f, 2.0f);  // ssb.rs:17
+  ScanCoef c = coef_lp(d.bq);
+  c.r = d.r;
+  auto st = std::make_unique<ScanStage>(RecK::LPDC, Pre::Ssb, Post::Id, lpdc_ss(d), c, nch);
+  st->set_osc(oscillator(bfo_hz, fs));  // ssb.rs:18 Rotator::new(bfo_hz, fs)
+  auto blk = std::make_unique<OneStageBlock>("SsbProductDemod", Dt::C32, nch, std::move(st), carry_zero());
+  blk->coef_ = {d.bq.b0, d.bq.b1, d.bq.b2, d.bq.a1, d.bq.a2, d.r};
+  return blk;
+}
+
+std::unique_ptr<Block> make_am_demod(float fs, float audio_bw) { return std::make_unique<AmBlock>(fs, audio_bw); }
+
+int am_demod_with_abs_approx(Block* b, float k1, float k2) {
+  auto* a = dynamic_cast<AmBlock*>(b);
+  if (!a) return -4;
+  a->set_abs(k1, k2);
+  return 0;
+}
+
+std::unique_ptr<Block> make_cw_demod(float fs, float tone_hz, float env_bw) {
+  (void)tone_hz;  // cw.rs:15: accepted for API symmetry, unused
+  const float a = cw_alpha(fs, env_bw);
+  ScanCoef c{};
+  c.a = a;
+  c.gain = 1.0f;
+  auto st = std::make_unique<ScanStage>(RecK::ONEPOLE, Pre::Cw, Post::Gain, onepole_ss(a), c, 1);
+  auto blk = std::make_unique<OneStageBlock>("CwEnvelopeDemod", Dt::C32, 1, std::move(st), carry_zero());
+  blk->coef_ = {a};
+  return blk;
+}
+
+int cw_demod_set_gain(Block* b, float g) {
+  auto* o = dynamic_cast<OneStageBlock*>(b);
+  if (!o || std::strcmp(b->name(), "CwEnvelopeDemod") != 0) return -4;
+  o->stage().coef().gain = g;
+  return 0;
+}
+
+}  // namespace orion

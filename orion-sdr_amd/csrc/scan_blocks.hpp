@@ -1,0 +1,20 @@
+// scan_blocks.hpp — Blocks built on the state-carry scan (scan.hpp).
+#pragma once
+#include <memory>
+
+#include "blocks.hpp"
+
+namespace orion {
+
+std::unique_ptr<Block> make_lp_cascade(float fs, float fc);                  // dsp/iir.rs:49-83
+std::unique_ptr<Block> make_dc_blocker(float fs, float cut_hz);              // dsp/dc.rs:8-59
+std::unique_ptr<Block> make_fm_demod(float fs, float dev_hz, float audio_bw);  // demodulate/fm.rs
+int fm_demod_with_translate(Block* b, float freq_hz);                        // fm.rs:34-37
+std::unique_ptr<Block> make_pm_demod(float fs, float k, float audio_bw);     // demodulate/pm.rs
+std::unique_ptr<Block> make_ssb_demod(float fs, float bfo_hz, float audio_bw, int nch);  // ssb.rs
+std::unique_ptr<Block> make_am_demod(float fs, float audio_bw);              // demodulate/am.rs
+int am_demod_with_abs_approx(Block* b, float k1, float k2);                  // am.rs:33-36
+std::unique_ptr<Block> make_cw_demod(float fs, float tone_hz, float env_bw);  // demodulate/cw.rs
+int cw_demod_set_gain(Block* b, float g);                                    // cw.rs:26-28
+
+}  // namespace orion

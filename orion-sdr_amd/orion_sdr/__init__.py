@@ -1,0 +1,392 @@
+"""orion_sdr (MI355X engine) — Python mirror of skynavga/orion-sdr's analog API.
+
+Same class names, constructor arguments and ``process(ndarray) -> ndarray``
+contract as the reference PyO3 module (``python/orion_sdr/__init__.pyi:18-79``,
+``src/python/demodulate.rs:9-148``): IQ arrays are ``numpy.complex64``, audio
+``numpy.float32``, inputs must be 1-D and C-contiguous (else ``ValueError`` /
+``TypeError``), every call returns a new array, and instances keep their
+streaming state between calls.
+
+Every class runs on the GPU through ``lib/liborion_sdr_amd.so`` (gfx950 HIP
+kernels behind the C ABI in ``include/orion_sdr_amd.h``). There is no CPU
+fallback: importing without the built library, or calling without a visible
+device, raises.
+
+``process`` also accepts torch CUDA tensors (device path, no host copies): the
+output is a new torch tensor on the same device, computed asynchronously on
+torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+__all__ = [
+    "Rotator", "FirDecimator", "FirLowpass", "FirLowpassIq", "LpCascade", "DcBlocker",
+    "FmQuadratureDemod", "PmQuadratureDemod", "SsbProductDemod", "AmEnvelopeDemod",
+    "CwEnvelopeDemod", "WbfmChain", "fir_lowpass_design", "kaiser_lowpass_taps",
+    "kaiser_transition_norm", "kaiser_num_taps", "lp_cascade_design", "lib_path", "OrionError",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(os.path.dirname(_HERE), "lib", "liborion_sdr_amd.so")
+
+
+def lib_path() -> str:
+    return _LIB
+
+
+class OrionError(RuntimeError):
+    """A failure reported by the C ABI (HIP error, bad argument, ...)."""
+
+
+class WorkReport(C.Structure):
+    _fields_ = [("in_read", C.c_size_t), ("out_written", C.c_size_t)]
+
+
+class WbfmParams(C.Structure):
+    _fields_ = [("fs", C.c_float), ("f_off", C.c_float), ("dec_cutoff", C.c_float),
+                ("dec_trans", C.c_float), ("dev_hz", C.c_float), ("audio_bw", C.c_float),
+                ("audio_pass", C.c_float), ("audio_trans", C.c_float), ("m", C.c_size_t)]
+
+
+def _load():
+    if not os.path.exists(_LIB):
+        raise ImportError(
+            f"orion_sdr: native library {_LIB} is missing — build it with "
+            "`make -C orion-sdr_amd` (hipcc, gfx950). There is no CPU fallback.")
+    L = C.CDLL(_LIB)
+    vp, sz, f, i = C.c_void_p, C.c_size_t, C.c_float, C.c_int
+    fp = C.POINTER(C.c_float)
+    sig = {
+        "orion_version": (C.c_char_p, []), "orion_last_error": (C.c_char_p, []),
+        "orion_device_count": (i, []), "orion_set_device": (i, [i]), "orion_synchronize": (i, [vp]),
+        "orion_rotator_new": (vp, [f, f]),
+        "orion_fir_decimator_new": (vp, [f, sz, f, f]),
+        "orion_fir_decimator_batch_new": (vp, [f, sz, f, f, sz]),
+        "orion_fir_lowpass_new": (vp, [f, f, f]),
+        "orion_fir_lowpass_iq_design": (vp, [sz, f, f]),
+        "orion_fir_lowpass_iq_from_taps": (vp, [fp, sz]),
+        "orion_fir_lowpass_iq_filter_aligned_device": (i, [vp, vp, sz, vp]),
+        "orion_fir_lowpass_iq_filter_aligned": (i, [vp, vp, sz]),
+        "orion_lp_cascade_new": (vp, [f, f]),
+        "orion_dc_blocker_new": (vp, [f, f]),
+        "orion_fm_quadrature_demod_new": (vp, [f, f, f]),
+        "orion_fm_quadrature_demod_with_translate": (i, [vp, f]),
+        "orion_pm_quadrature_demod_new": (vp, [f, f, f]),
+        "orion_ssb_product_demod_new": (vp, [f, f, f]),
+        "orion_ssb_product_demod_batch_new": (vp, [f, f, f, sz]),
+        "orion_am_envelope_demod_new": (vp, [f, f]),
+        "orion_am_envelope_demod_with_abs_approx": (i, [vp, f, f]),
+        "orion_cw_envelope_demod_new": (vp, [f, f, f]),
+        "orion_cw_envelope_demod_set_gain": (i, [vp, f]),
+        "orion_wbfm_chain_new": (vp, [C.POINTER(WbfmParams)]),
+        "orion_wbfm_chain_batch_new": (vp, [C.POINTER(WbfmParams), fp, sz]),
+        "orion_wbfm_chain_set_tiling": (i, [vp, i, i]),
+        "orion_block_process": (i, [vp, vp, sz, vp, sz, C.POINTER(WorkReport)]),
+        "orion_block_process_device": (i, [vp, vp, sz, vp, sz, vp, C.POINTER(WorkReport)]),
+        "orion_block_reset": (i, [vp]), "orion_block_free": (None, [vp]),
+        "orion_block_in_type": (i, [vp]), "orion_block_out_type": (i, [vp]),
+        "orion_block_out_len": (sz, [vp, sz]), "orion_block_channels": (sz, [vp]),
+        "orion_block_name": (C.c_char_p, [vp]),
+        "orion_block_taps": (i, [vp, i, fp, sz, C.POINTER(sz)]),
+        "orion_fir_lowpass_design": (sz, [f, f, f, fp, sz]),
+        "orion_kaiser_lowpass_taps": (sz, [sz, f, f, fp, sz]),
+        "orion_kaiser_transition_norm": (f, [sz, f]),
+        "orion_kaiser_num_taps": (sz, [f, f]),
+        "orion_lp_cascade_design": (None, [f, f, fp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
+_L = _load()
+
+
+def _err() -> str:
+    return (_L.orion_last_error() or b"").decode()
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise OrionError(f"orion_sdr: error {rc}: {_err()}")
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _taps_of(h, which: int) -> np.ndarray:
+    n = C.c_size_t(0)
+    _check(_L.orion_block_taps(h, which, None, 0, C.byref(n)))
+    out = np.zeros(n.value, np.float32)
+    _check(_L.orion_block_taps(h, which, _fptr(out), n.value, C.byref(n)))
+    return out
+
+
+_DT = {0: np.complex64, 1: np.float32}
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+class _Block:
+    """Shared Block contract (reference src/core.rs:12-22)."""
+
+    def __init__(self, handle):
+        if not handle:
+            raise OrionError(f"orion_sdr: construction failed: {_err()}")
+        self._h = handle
+        self._in = _DT[_L.orion_block_in_type(handle)]
+        self._out = _DT[_L.orion_block_out_type(handle)]
+        self._nch = _L.orion_block_channels(handle)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            _L.orion_block_free(h)
+            self._h = None
+
+    @property
+    def name(self) -> str:
+        return _L.orion_block_name(self._h).decode()
+
+    def out_len(self, n: int) -> int:
+        return _L.orion_block_out_len(self._h, n)
+
+    def reset(self):
+        _check(_L.orion_block_reset(self._h))
+
+    def _validate(self, x: np.ndarray) -> np.ndarray:
+        # python/tests/test_unit.py:86-127: wrong dtype / ndim / non-contiguous -> error
+        if not isinstance(x, np.ndarray):
+            raise TypeError(f"{type(self).__name__}.process expects a numpy array")
+        if x.dtype != self._in:
+            raise TypeError(f"{type(self).__name__}.process expects {np.dtype(self._in).name}, got {x.dtype}")
+        want_ndim = 1 if self._nch == 1 else 2
+        if x.ndim != want_ndim:
+            raise ValueError(f"{type(self).__name__}.process expects a {want_ndim}-D array, got {x.ndim}-D")
+        if not x.flags["C_CONTIGUOUS"]:
+            raise ValueError("array is not C-contiguous")
+        if self._nch > 1 and x.shape[0] != self._nch:
+            raise ValueError(f"expected {self._nch} channels, got {x.shape[0]}")
+        return x
+
+    def process_into(self, x: np.ndarray, out: np.ndarray) -> WorkReport:
+        """Preallocated path (core.rs:19-21 process_into): honours out capacity."""
+        x = self._validate(x)
+        n = x.shape[-1]
+        wr = WorkReport()
+        _check(_L.orion_block_process(self._h, x.ctypes.data, n, out.ctypes.data, out.shape[-1], C.byref(wr)))
+        return wr
+
+    def process(self, x):
+        if _is_torch(x):
+            return self.process_device(x)
+        x = self._validate(x)
+        n = x.shape[-1]
+        cap = self.out_len(n)
+        out = np.empty((cap,) if self._nch == 1 else (self._nch, cap), self._out)
+        wr = WorkReport()
+        _check(_L.orion_block_process(self._h, x.ctypes.data, n, out.ctypes.data, cap, C.byref(wr)))
+        if wr.out_written != cap:
+            out = out[..., : wr.out_written].copy()
+        return out
+
+    def process_device(self, x, out=None, stream=None):
+        """Device buffers (torch CUDA tensors). Asynchronous on `stream`
+        (default: torch's current stream). Returns (out, WorkReport)."""
+        import torch
+
+        if not x.is_cuda or not x.is_contiguous():
+            raise ValueError("process_device needs a contiguous CUDA tensor")
+        want = torch.complex64 if self._in is np.complex64 else torch.float32
+        if x.dtype != want:
+            raise TypeError(f"expected {want}, got {x.dtype}")
+        n = x.shape[-1]
+        cap = self.out_len(n)
+        odt = torch.complex64 if self._out is np.complex64 else torch.float32
+        if out is None:
+            out = torch.empty((cap,) if self._nch == 1 else (self._nch, cap), dtype=odt, device=x.device)
+        else:
+            cap = out.shape[-1]
+        s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+        wr = WorkReport()
+        _check(_L.orion_block_process_device(self._h, x.data_ptr(), n, out.data_ptr(), cap, s, C.byref(wr)))
+        return out if wr.out_written == cap else out[..., : wr.out_written]
+
+    def taps(self, which: int = 0) -> np.ndarray:
+        return _taps_of(self._h, which)
+
+
+# ---- DSP primitives (src/dsp) -------------------------------------------------
+class Rotator(_Block):
+    """dsp/rotator.rs:16 Rotator::new(freq_hz, fs); process = rotate_block."""
+
+    def __init__(self, freq_hz: float, fs: float):
+        super().__init__(_L.orion_rotator_new(freq_hz, fs))
+
+
+class FirDecimator(_Block):
+    """dsp/decim.rs:24 FirDecimator::new(fs, m, cutoff_hz, trans_hz). channels>1: batched
+    [nch, n] input (independent streams)."""
+
+    def __init__(self, fs: float, m: int, cutoff_hz: float, trans_hz: float, channels: int = 1):
+        h = (_L.orion_fir_decimator_new(fs, m, cutoff_hz, trans_hz) if channels == 1
+             else _L.orion_fir_decimator_batch_new(fs, m, cutoff_hz, trans_hz, channels))
+        super().__init__(h)
+
+
+class FirLowpass(_Block):
+    """dsp/fir.rs:16 FirLowpass::design(fs, pass_hz, trans_hz) (real f32 stream)."""
+
+    def __init__(self, fs: float, pass_hz: float, trans_hz: float):
+        super().__init__(_L.orion_fir_lowpass_new(fs, pass_hz, trans_hz))
+
+
+class FirLowpassIq(_Block):
+    """dsp/fir.rs:176-297. Use FirLowpassIq.design(...) or FirLowpassIq.from_taps(...)."""
+
+    def __init__(self, handle):
+        super().__init__(handle)
+
+    @classmethod
+    def design(cls, num_taps: int, cutoff_norm: float, stopband_db: float) -> "FirLowpassIq":
+        return cls(_L.orion_fir_lowpass_iq_design(num_taps, cutoff_norm, stopband_db))
+
+    @classmethod
+    def from_taps(cls, taps) -> "FirLowpassIq":
+        t = np.ascontiguousarray(taps, np.float32)
+        return cls(_L.orion_fir_lowpass_iq_from_taps(_fptr(t) if t.size else None, t.size))
+
+    def num_taps(self) -> int:
+        return len(self.taps())
+
+    def group_delay(self) -> int:
+        return (self.num_taps() - 1) // 2
+
+    def filter_aligned(self, io: np.ndarray) -> np.ndarray:
+        """fir.rs:260-276, returns the filtered copy (time-aligned, same length)."""
+        x = np.array(self._validate(io), copy=True)
+        _check(_L.orion_fir_lowpass_iq_filter_aligned(self._h, x.ctypes.data, x.size))
+        return x
+
+
+class LpCascade(_Block):
+    """dsp/iir.rs:49 LpCascade::design(fs, fc) as an f32 stream block."""
+
+    def __init__(self, fs: float, fc: float):
+        super().__init__(_L.orion_lp_cascade_new(fs, fc))
+
+
+class DcBlocker(_Block):
+    """dsp/dc.rs:15 DcBlocker::new(fs, cut_hz)."""
+
+    def __init__(self, fs: float, cut_hz: float):
+        super().__init__(_L.orion_dc_blocker_new(fs, cut_hz))
+
+
+# ---- demodulators (src/demodulate; PyO3 signatures src/python/demodulate.rs) ---
+class CwEnvelopeDemod(_Block):
+    def __init__(self, sample_rate: float, tone_hz: float, env_bw_hz: float):
+        super().__init__(_L.orion_cw_envelope_demod_new(sample_rate, tone_hz, env_bw_hz))
+
+    def set_gain(self, g: float):
+        _check(_L.orion_cw_envelope_demod_set_gain(self._h, g))
+
+
+class AmEnvelopeDemod(_Block):
+    """abs_approx=True uses k1=0.9482, k2=0.3920 (src/python/demodulate.rs:46-53)."""
+
+    def __init__(self, fs: float, audio_bw_hz: float, abs_approx: bool = False):
+        super().__init__(_L.orion_am_envelope_demod_new(fs, audio_bw_hz))
+        if abs_approx:
+            _check(_L.orion_am_envelope_demod_with_abs_approx(self._h, 0.9482, 0.3920))
+
+    def with_abs_approx(self, k1: float, k2: float) -> "AmEnvelopeDemod":
+        _check(_L.orion_am_envelope_demod_with_abs_approx(self._h, k1, k2))
+        return self
+
+
+class SsbProductDemod(_Block):
+    def __init__(self, fs: float, bfo_hz: float, audio_bw_hz: float, channels: int = 1):
+        h = (_L.orion_ssb_product_demod_new(fs, bfo_hz, audio_bw_hz) if channels == 1
+             else _L.orion_ssb_product_demod_batch_new(fs, bfo_hz, audio_bw_hz, channels))
+        super().__init__(h)
+
+
+class FmQuadratureDemod(_Block):
+    def __init__(self, fs: float, dev_hz: float, audio_bw_hz: float):
+        super().__init__(_L.orion_fm_quadrature_demod_new(fs, dev_hz, audio_bw_hz))
+
+    def with_translate(self, freq_hz: float) -> "FmQuadratureDemod":
+        _check(_L.orion_fm_quadrature_demod_with_translate(self._h, freq_hz))
+        return self
+
+
+class PmQuadratureDemod(_Block):
+    def __init__(self, fs: float, k: float, audio_bw_hz: float):
+        super().__init__(_L.orion_pm_quadrature_demod_new(fs, k, audio_bw_hz))
+
+
+class WbfmChain(_Block):
+    """The WBFM chain of docs/demodulate.md:128-133, fused on the GPU.
+    f_off: a float (one channel) or a sequence (one channel each; input [nch, n])."""
+
+    def __init__(self, fs=10e6, f_off=1.5e6, m=8, dec_cutoff=200e3, dec_trans=79e3, dev_hz=75e3,
+                 audio_bw=15e3, audio_pass=15e3, audio_trans=10e3):
+        offs = np.atleast_1d(np.asarray(f_off, np.float32))
+        p = WbfmParams(fs, float(offs[0]), dec_cutoff, dec_trans, dev_hz, audio_bw, audio_pass,
+                       audio_trans, m)
+        if np.ndim(f_off) == 0:
+            h = _L.orion_wbfm_chain_new(C.byref(p))
+        else:
+            offs = np.ascontiguousarray(offs)
+            h = _L.orion_wbfm_chain_batch_new(C.byref(p), _fptr(offs), offs.size)
+        super().__init__(h)
+
+    def set_tiling(self, outputs_per_wg: int, warmup: int):
+        _check(_L.orion_wbfm_chain_set_tiling(self._h, outputs_per_wg, warmup))
+
+
+# ---- designs (host) ----------------------------------------------------------
+def fir_lowpass_design(fs: float, pass_hz: float, trans_hz: float) -> np.ndarray:
+    n = _L.orion_fir_lowpass_design(fs, pass_hz, trans_hz, None, 0)
+    t = np.zeros(n, np.float32)
+    _L.orion_fir_lowpass_design(fs, pass_hz, trans_hz, _fptr(t), n)
+    return t
+
+
+def kaiser_lowpass_taps(num_taps: int, cutoff_norm: float, stopband_db: float) -> np.ndarray:
+    n = _L.orion_kaiser_lowpass_taps(num_taps, cutoff_norm, stopband_db, None, 0)
+    t = np.zeros(n, np.float32)
+    _L.orion_kaiser_lowpass_taps(num_taps, cutoff_norm, stopband_db, _fptr(t), n)
+    return t
+
+
+def kaiser_transition_norm(num_taps: int, stopband_db: float) -> float:
+    return _L.orion_kaiser_transition_norm(num_taps, stopband_db)
+
+
+def kaiser_num_taps(transition_norm: float, stopband_db: float) -> int:
+    return _L.orion_kaiser_num_taps(transition_norm, stopband_db)
+
+
+def lp_cascade_design(fs: float, fc: float) -> np.ndarray:
+    o = np.zeros(5, np.float32)
+    _L.orion_lp_cascade_design(fs, fc, _fptr(o))
+    return o
+
+
+def device_count() -> int:
+    return _L.orion_device_count()
+
+
+def version() -> str:
+    return _L.orion_version().decode()
