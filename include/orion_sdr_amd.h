@@ -106,8 +106,6 @@ typedef struct {
 orion_block* orion_wbfm_chain_new(const orion_wbfm_params* p);
 /* nch channels sharing the design, each with its own tuning offset f_off[ch]. */
 orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float* f_off, size_t nch);
-/* Tuning knob: decimated outputs per workgroup and IIR warm-up length. */
-int orion_wbfm_chain_set_tiling(orion_block* b, int outputs_per_wg, int warmup);
 
 /* ---- Block contract (core.rs:12-22) ------------------------------------ */
 /* Host buffers (synchronous). */

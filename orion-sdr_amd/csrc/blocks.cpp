@@ -289,22 +289,29 @@ class WbfmBlock final : public Block {
     h_aud_ = fir_lowpass_taps(fs2, p.audio_pass, p.audio_trans);
     if (h_dec_.size() > 128 || h_aud_.size() > 128)
       throw std::invalid_argument("fused WBFM chain supports <= 128 decimator and audio taps");
-    std::memset(&c_, 0, sizeof(c_));
+    std::memset(&cf_, 0, sizeof(cf_));
+    std::memset(&cb_, 0, sizeof(cb_));
     const auto g = fir_lowpass_as_standard(h_dec_);
-    for (size_t k = 0; k < g.size(); ++k) c_.g[(k % 8) * kWbfmQ + k / 8] = g[k];
+    for (size_t k = 0; k < g.size(); ++k) cf_.g[(k % 8) * kWbfmQ + k / 8] = g[k];
+    cf_.k = 1.0f / std::max(p.dev_hz, 1.0f);  // fm.rs:23
     const auto a = fir_lowpass_as_standard(h_aud_);
-    for (size_t k = 0; k < a.size(); ++k) c_.a[k] = a[k];
+    for (size_t k = 0; k < a.size(); ++k) cb_.a[k] = a[k];
     const BiquadCoeffs bq = lp_cascade_design(fs2, p.audio_bw * 0.9f);  // fm.rs:24
-    c_.b0 = bq.b0; c_.b1 = bq.b1; c_.b2 = bq.b2; c_.a1 = bq.a1; c_.a2 = bq.a2;
-    c_.k = 1.0f / std::max(p.dev_hz, 1.0f);  // fm.rs:23
+    cb_.b0 = bq.b0; cb_.b1 = bq.b1; cb_.b2 = bq.b2; cb_.a1 = bq.a1; cb_.a2 = bq.a2;
     const StateSpace ss = lp_cascade_ss(bq);
-    auto m8 = mat_pow(ss.A, 4, 8);
-    for (int i = 0; i < 16; ++i) c_.m8[i] = static_cast<float>(m8[i]);
-    auto pwm = m8;
+    auto pwm = mat_pow(ss.A, 4, kBackC);
     for (int s = 0; s < 6; ++s) {
-      for (int i = 0; i < 16; ++i) c_.pw[s * 16 + i] = static_cast<float>(pwm[i]);
+      for (int i = 0; i < 16; ++i) cb_.pw[s * 16 + i] = pwm[i];
       pwm = mat_mul(pwm, pwm, 4);
     }
+    const auto mw = mat_pow(ss.A, 4, 64ull * kBackC);
+    for (int i = 0; i < 16; ++i) cb_.mw[i] = mw[i];
+    std::vector<double> lm(64 * 16);
+    for (int L = 0; L < 64; ++L) {
+      const auto m = mat_pow(ss.A, 4, static_cast<uint64_t>(kBackC) * L);
+      std::copy(m.begin(), m.end(), lm.begin() + L * 16);
+    }
+    lanemats_.upload(lm.data(), lm.size() * sizeof(double));
     std::vector<uint64_t> steps(nch_);
     std::vector<float> tabs;
     tabs.reserve(static_cast<size_t>(nch_) * kWbfmNS * 2);
@@ -339,10 +346,13 @@ class WbfmBlock final : public Block {
       ORION_HIP(hipMemcpyAsync(carry_[nxt].as<void>(), carry_[cur_].as<void>(), carry_[cur_].size(),
                                hipMemcpyDeviceToDevice, s));
     } else {
+      phi_.resize(static_cast<size_t>(nch_) * n_dec * sizeof(float) + 64);
       WbfmArgs a{};
       a.x = static_cast<const f2*>(in);
       a.x_stride = static_cast<long long>(n);
       a.n = static_cast<long long>(n);
+      a.phi = phi_.as<float>();
+      a.phi_stride = static_cast<long long>(n_dec);
       a.y = static_cast<float*>(out);
       a.y_stride = static_cast<long long>(out_cap);
       a.n_dec = static_cast<long long>(n_dec);
@@ -353,9 +363,8 @@ class WbfmBlock final : public Block {
       a.carry_out = carry_[nxt].as<float>();
       a.hist_in = hist_[cur_].as<f2>();
       a.hist_out = hist_[nxt].as<f2>();
-      a.A = A_;
-      a.wpre = wpre_;
-      launch_wbfm(a, c_, nch_, s);
+      a.lanemats = lanemats_.as<double>();
+      launch_wbfm(a, cf_, cb_, nch_, s);
     }
     cur_ = nxt;
     k0_ += n;
@@ -373,22 +382,16 @@ class WbfmBlock final : public Block {
     k0_ = 0;
   }
   std::vector<float> taps(int which) const override { return which == 0 ? h_dec_ : h_aud_; }
-  void set_tiling(int A, int wpre) {
-    if (A < 1 || wpre < 0) throw std::invalid_argument("bad tiling");
-    A_ = A;
-    wpre_ = wpre;
-  }
 
  private:
   WbfmParams p_;
   int nch_;
   std::vector<float> h_dec_, h_aud_;
-  WbfmConst c_;
-  DevBuf step_, tab_, carry_[2], hist_[2];
+  WbfmFrontConst cf_;
+  WbfmBackConst cb_;
+  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_;
   int cur_ = 0;
   uint64_t k0_ = 0;
-  int A_ = 33 * kWbfmT - 640;  // 16256 outputs per workgroup: 33 full sub-tiles incl. warm-up
-  int wpre_ = 640;             // 512 IIR warm-up + 128 audio-FIR history
 };
 
 }  // namespace
@@ -411,11 +414,6 @@ int fir_lowpass_iq_filter_aligned(Block* b, void* io, size_t n, hipStream_t s) {
 }
 std::unique_ptr<Block> make_wbfm_chain(const WbfmParams& p, const std::vector<float>& f_off) {
   return std::make_unique<WbfmBlock>(p, f_off);
-}
-void wbfm_set_tiling(Block* b, int A, int wpre) {
-  auto* w = dynamic_cast<WbfmBlock*>(b);
-  if (!w) throw std::invalid_argument("not a WBFM chain");
-  w->set_tiling(A, wpre);
 }
 
 }  // namespace orion

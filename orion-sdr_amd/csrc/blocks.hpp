@@ -96,6 +96,5 @@ struct WbfmParams {
   size_t m;
 };
 std::unique_ptr<Block> make_wbfm_chain(const WbfmParams& p, const std::vector<float>& f_off);
-void wbfm_set_tiling(Block* b, int outputs_per_wg, int warmup);
 
 }  // namespace orion

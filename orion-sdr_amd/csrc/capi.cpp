@@ -152,13 +152,6 @@ orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float*
   if (!p || !f_off || nch == 0) { g_err = "null params / no channels"; return nullptr; }
   return make([&] { return orion::make_wbfm_chain(wbfm_params(p), std::vector<float>(f_off, f_off + nch)); });
 }
-int orion_wbfm_chain_set_tiling(orion_block* b, int A, int wpre) {
-  if (!b) return fail(ORION_E_NULL, "null handle");
-  return guarded([&] {
-    orion::wbfm_set_tiling(b->impl.get(), A, wpre);
-    return ORION_OK;
-  });
-}
 
 int orion_block_process(orion_block* b, const void* in, size_t n_in, void* out, size_t out_cap,
                         orion_work_report* wr) {

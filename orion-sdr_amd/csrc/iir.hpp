@@ -73,27 +73,32 @@ struct RecOnePole {
   }
 };
 
-template <int S>
-__device__ __forceinline__ void matvec_acc(const float* __restrict__ Mx, const float (&v)[S],
-                                           float (&acc)[S]) {
+// acc += Mx * v (S x S row-major). T = double for the scan combine: the chunk
+// transition matrices of these near-unit-circle filters have entries ~7 and
+// condition ~1e3, so f32 carries lose ~3 digits; f64 keeps the carried state
+// at the f32 rounding level of the reference's own update.
+__device__ __forceinline__ float fmaT(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fmaT(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+template <int S, class T, class MT>
+__device__ __forceinline__ void matvec_acc(const MT* __restrict__ Mx, const T (&v)[S], T (&acc)[S]) {
 #pragma unroll
   for (int i = 0; i < S; ++i) {
-    float a = acc[i];
+    T a = acc[i];
 #pragma unroll
-    for (int j = 0; j < S; ++j) a = __builtin_fmaf(Mx[i * S + j], v[j], a);
+    for (int j = 0; j < S; ++j) a = fmaT(static_cast<T>(Mx[i * S + j]), v[j], a);
     acc[i] = a;
   }
 }
 
 // Inclusive Kogge-Stone over the 64 lanes of a wave:
-//   Q_L = agg_L + A^C * Q_{L-1}, using pw[s] = (A^C)^(2^s) (S*S floats each, uniform).
-template <int S>
-__device__ __forceinline__ void wave_scan_inclusive(float (&q)[S], const float* __restrict__ pw,
-                                                    int lane) {
+//   Q_L = agg_L + A^C * Q_{L-1}, using pw[s] = (A^C)^(2^s) (S*S each, uniform).
+template <int S, class T, class MT>
+__device__ __forceinline__ void wave_scan_inclusive(T (&q)[S], const MT* __restrict__ pw, int lane) {
 #pragma unroll 1
   for (int s = 0; s < 6; ++s) {
     const int d = 1 << s;
-    float o[S];
+    T o[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) o[i] = __shfl_up(q[i], d, 64);
     if (lane >= d) matvec_acc<S>(pw + s * S * S, o, q);

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(NT) void k_scan_agg(const ScanArgs a) {
   using R = typename RecSel<RK>::T;
   constexpr int S = R::S;
   __shared__ float sb[PADN];
-  __shared__ float tot[4][S];
+  __shared__ double tot[4][S];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int ch = blockIdx.y;
   const long long base = static_cast<long long>(blockIdx.x) * CH;
@@ -115,17 +115,20 @@ __global__ __launch_bounds__(NT) void k_scan_agg(const ScanArgs a) {
     const int e = t * C + i;
     if (e < cnt) (void)rec.step(s, sb[pos(e)]);
   }
-  wave_scan_inclusive<S>(s, a.mats + ScanMatsLayout::kPwc * S * S, lane);
+  double q[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) q[i] = s[i];
+  wave_scan_inclusive<S>(q, a.mats + ScanMatsLayout::kPwc * S * S, lane);
   if (lane == 63)
 #pragma unroll
-    for (int i = 0; i < S; ++i) tot[wave][i] = s[i];
+    for (int i = 0; i < S; ++i) tot[wave][i] = q[i];
   __syncthreads();
   if (t == 0) {
-    float g[S];
+    double g[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) g[i] = tot[0][i];
     for (int w = 1; w < 4; ++w) {
-      float v[S];
+      double v[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) v[i] = tot[w][i];
       matvec_acc<S>(a.mats + ScanMatsLayout::kM64 * S * S, g, v);
@@ -133,7 +136,7 @@ __global__ __launch_bounds__(NT) void k_scan_agg(const ScanArgs a) {
       for (int i = 0; i < S; ++i) g[i] = v[i];
     }
     const long long nblk = gridDim.x;
-    float* out = a.aggs + (ch * nblk + blockIdx.x) * S;
+    double* out = a.aggs + (ch * nblk + blockIdx.x) * S;
 #pragma unroll
     for (int i = 0; i < S; ++i) out[i] = g[i];
   }
@@ -142,20 +145,20 @@ __global__ __launch_bounds__(NT) void k_scan_agg(const ScanArgs a) {
 template <RecK RK>
 __global__ __launch_bounds__(NT) void k_scan_carry(const ScanArgs a, int nblk) {
   constexpr int S = RecSel<RK>::T::S;
-  __shared__ float q[2][NT][S];
-  __shared__ float cs[S];
+  __shared__ double q[2][NT][S];
+  __shared__ double cs[S];
   const int t = threadIdx.x;
   const int ch = blockIdx.x;
   if (t < S) cs[t] = a.carry_in[ch * kScanCarry + t];
   __syncthreads();
-  const float* Mch = a.mats + ScanMatsLayout::kPch * S * S;
+  const double* Mch = a.mats + ScanMatsLayout::kPch * S * S;
   for (int c0 = 0; c0 < nblk; c0 += NT) {
     const int b = c0 + t;
-    float v[S], carry[S];
+    double v[S], carry[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) {
       carry[i] = cs[i];
-      v[i] = b < nblk ? a.aggs[(static_cast<long long>(ch) * nblk + b) * S + i] : 0.0f;
+      v[i] = b < nblk ? a.aggs[(static_cast<long long>(ch) * nblk + b) * S + i] : 0.0;
     }
     if (t == 0) matvec_acc<S>(Mch, carry, v);  // fold the incoming state into element 0
     int buf = 0;
@@ -165,7 +168,7 @@ __global__ __launch_bounds__(NT) void k_scan_carry(const ScanArgs a, int nblk) {
       for (int i = 0; i < S; ++i) q[buf][t][i] = v[i];
       __syncthreads();
       if (t >= d) {
-        float o[S];
+        double o[S];
 #pragma unroll
         for (int i = 0; i < S; ++i) o[i] = q[buf][t - d][i];
         matvec_acc<S>(Mch + s * S * S, o, v);
@@ -176,7 +179,7 @@ __global__ __launch_bounds__(NT) void k_scan_carry(const ScanArgs a, int nblk) {
     for (int i = 0; i < S; ++i) q[buf][t][i] = v[i];
     __syncthreads();
     if (b < nblk) {
-      float* out = a.sin + (static_cast<long long>(ch) * nblk + b) * S;
+      double* out = a.sin + (static_cast<long long>(ch) * nblk + b) * S;
 #pragma unroll
       for (int i = 0; i < S; ++i) out[i] = t == 0 ? carry[i] : q[buf][t - 1][i];
     }
@@ -191,7 +194,7 @@ __global__ __launch_bounds__(NT) void k_scan_apply(const ScanArgs a) {
   using R = typename RecSel<RK>::T;
   constexpr int S = R::S;
   __shared__ float sb[PADN];
-  __shared__ float tot[4][S];
+  __shared__ double tot[4][S];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int ch = blockIdx.y;
   const long long nblk = gridDim.x;
@@ -203,24 +206,27 @@ __global__ __launch_bounds__(NT) void k_scan_apply(const ScanArgs a) {
   float xs[C];
 #pragma unroll
   for (int i = 0; i < C; ++i) xs[i] = sb[pos(t * C + i)];
-  float q[S];
+  float s0[S];
 #pragma unroll
-  for (int i = 0; i < S; ++i) q[i] = 0.0f;
+  for (int i = 0; i < S; ++i) s0[i] = 0.0f;
 #pragma unroll
   for (int i = 0; i < C; ++i)
-    if (t * C + i < cnt) (void)rec.step(q, xs[i]);
+    if (t * C + i < cnt) (void)rec.step(s0, xs[i]);
+  double q[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) q[i] = s0[i];
   wave_scan_inclusive<S>(q, a.mats + ScanMatsLayout::kPwc * S * S, lane);
   if (lane == 63)
 #pragma unroll
     for (int i = 0; i < S; ++i) tot[wave][i] = q[i];
   __syncthreads();
   // state entering this wave
-  float cw[S];
-  const float* sin = a.sin + (ch * nblk + blockIdx.x) * S;
+  double cw[S];
+  const double* sin = a.sin + (ch * nblk + blockIdx.x) * S;
 #pragma unroll
   for (int i = 0; i < S; ++i) cw[i] = sin[i];
   for (int w = 0; w < wave; ++w) {
-    float v[S];
+    double v[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) v[i] = tot[w][i];
     matvec_acc<S>(a.mats + ScanMatsLayout::kM64 * S * S, cw, v);
@@ -228,25 +234,28 @@ __global__ __launch_bounds__(NT) void k_scan_apply(const ScanArgs a) {
     for (int i = 0; i < S; ++i) cw[i] = v[i];
   }
   // state entering this lane: Q_{L-1} + A^{C L} cw
-  float e[S];
+  double e[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) {
-    const float o = __shfl_up(q[i], 1, 64);
-    e[i] = lane == 0 ? 0.0f : o;
+    const double o = __shfl_up(q[i], 1, 64);
+    e[i] = lane == 0 ? 0.0 : o;
   }
   matvec_acc<S>(a.mats + (ScanMatsLayout::kLane + lane) * S * S, cw, e);
+  float ef[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) ef[i] = static_cast<float>(e[i]);
   // re-run with the reference update
 #pragma unroll
   for (int i = 0; i < C; ++i) {
     const int ei = t * C + i;
-    if (ei < cnt) sb[pos(ei)] = postmap<PO>(a, rec.step(e, xs[i]));
+    if (ei < cnt) sb[pos(ei)] = postmap<PO>(a, rec.step(ef, xs[i]));
   }
   const bool last_blk = base + cnt == a.n;
   if (last_blk && t * C <= cnt - 1 && cnt - 1 < t * C + C) {
     float* co = a.carry_out + ch * kScanCarry;
     const float* ci = a.carry_in + ch * kScanCarry;
 #pragma unroll
-    for (int i = 0; i < S; ++i) co[i] = e[i];
+    for (int i = 0; i < S; ++i) co[i] = ef[i];
     for (int i = S; i < 6; ++i) co[i] = 0.0f;
     if constexpr (PR == Pre::Fm || PR == Pre::Pm) {
       const f2* x = static_cast<const f2*>(a.x) + ch * a.x_stride;

@@ -48,35 +48,45 @@ void launch_hist_update_c(const f2* x_dev, long long n, const f2* old_dev, f2* n
 void launch_hist_update_r(const float* x_dev, long long n, const float* old_dev, float* new_dev,
                           int hist_len, hipStream_t s);
 
-// ----------------------------------------------------------- WBFM fused --
-// One pass: NCO mix -> polyphase decim x8 (<=128 taps) -> FM discriminator ->
-// LpCascade (wave scan, warm-up across workgroups) -> audio FIR (<=128 taps).
+// ------------------------------------------------------------ WBFM chain --
+// Two launches per call (k_wbfm.hip):
+//  front: NCO mix -> polyphase decim x8 (<= 128 taps) -> FM discriminator,
+//         writing phi (f32, 1/8 rate) — 8 B in, 0.5 B out per input sample;
+//  back : LpCascade (wave scan, f64 carries, warm-up across workgroups) ->
+//         audio FIR (<= 128 taps) — 0.59 B in, 0.5 B out per input sample.
 constexpr int kWbfmM = 8;
 constexpr int kWbfmQ = 16;
-constexpr int kWbfmT = 512;                    // decimated outputs per sub-tile
-constexpr int kWbfmNS = kWbfmM * (kWbfmT + kWbfmQ);  // staged input samples per sub-tile
-constexpr int kWbfmHist = kWbfmM * kWbfmQ;     // raw input history (128)
-constexpr int kWbfmCarry = 8 + 128;            // iir[4], prev[2], pad[2], fhist[128]
-struct WbfmConst {
-  float g[128];      // decimator taps g[8q+c] stored phase-major at [c*16+q]; quirk-mapped
-                     // (g[0]=h[L-1], g[k]=h[k-1]), zero padded
-  float a[128];      // audio taps, quirk-mapped, zero padded
-  float b0, b1, b2, a1, a2;  // LpCascade biquad
-  float k;           // 1/dev (fm.rs:23)
-  float m8[16];      // A^8 (chunk transition, 8 samples per lane)
-  float pw[6 * 16];  // (A^8)^(2^s), s = 0..5
+constexpr int kWbfmT = 512;                          // decimated outputs per front workgroup
+constexpr int kWbfmPhi = kWbfmT - 1;                 // discriminator outputs per front workgroup
+constexpr int kWbfmNS = kWbfmM * (kWbfmT + kWbfmQ);  // staged input samples per front workgroup
+constexpr int kWbfmHist = kWbfmM * kWbfmQ;           // raw input history (128)
+constexpr int kBackA = 4096;                         // audio outputs per back workgroup
+constexpr int kBackC = 19;                           // IIR samples per lane
+constexpr int kBackSpan = 256 * kBackC;              // 4864 = kBackA + 768 warm-up
+constexpr int kWbfmCarry = 8 + 128;                  // iir[4], prev[2], pad[2], fhist[128]
+struct WbfmFrontConst {
+  float g[128];  // decimator taps g[8q+c] phase-major at [c*16+q]; quirk-mapped
+                 // (g[0]=h[L-1], g[k]=h[k-1], dsp/fir.rs:57-66), zero padded
+  float k;       // 1/dev (fm.rs:23)
+};
+struct WbfmBackConst {
+  float a[128];               // audio taps, quirk-mapped, zero padded
+  float b0, b1, b2, a1, a2;   // LpCascade biquad (iir.rs:49-71)
+  double pw[6 * 16];          // (A^19)^(2^s), s = 0..5
+  double mw[16];              // A^(19*64): one wave's span
 };
 struct WbfmArgs {
   const f2* x;  long long x_stride;  long long n;
+  float* phi;   long long phi_stride;               // workspace [nch][>= n_dec]
   float* y;     long long y_stride;  long long n_dec;
-  long long k0;                      // samples consumed by earlier calls
-  const uint64_t* step;              // [nch]
-  const f2* tab;                     // [nch][kWbfmNS] e^{j theta p}
-  const float* carry_in; float* carry_out;   // [nch][kWbfmCarry]
-  const f2* hist_in; f2* hist_out;           // [nch][kWbfmHist]
-  int A;                             // decimated outputs per workgroup
-  int wpre;                          // warm-up outputs before each workgroup's range
+  long long k0;                                     // samples consumed by earlier calls
+  const uint64_t* step;                             // [nch] Q0.64 oscillator step
+  const f2* tab;                                    // [nch][kWbfmNS] e^{j theta p}
+  const float* carry_in; float* carry_out;          // [nch][kWbfmCarry]
+  const f2* hist_in; f2* hist_out;                  // [nch][kWbfmHist]
+  const double* lanemats;                           // A^(19 L), L = 0..63 (16 doubles each)
 };
-void launch_wbfm(const WbfmArgs& a, const WbfmConst& c, int nch, hipStream_t s);
+void launch_wbfm(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmBackConst& b, int nch,
+                 hipStream_t s);
 
 }  // namespace orion

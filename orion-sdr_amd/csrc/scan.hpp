@@ -66,9 +66,9 @@ struct ScanArgs {
   int translate;                       // Pre::Fm: apply the fm.rs:48-58 translator
   uint64_t step;                       // oscillator Q0.64 step (translator / BFO)
   const f2* tab;                       // e^{j theta p}, p < kScanCH (oscillator table)
-  const float* mats;                   // ScanMatsLayout
-  float* aggs;                         // [ch][nblk][S]
-  float* sin;                          // [ch][nblk][S] state entering each workgroup
+  const double* mats;                  // ScanMatsLayout (f64: see iir.hpp matvec_acc)
+  double* aggs;                        // [ch][nblk][S]
+  double* sin;                         // [ch][nblk][S] state entering each workgroup
   const float* carry_in;               // [ch][kScanCarry]
   float* carry_out;                    // [ch][kScanCarry]
   ScanCoef c;

@@ -21,10 +21,9 @@ class ScanStage {
   ScanStage(RecK rec, Pre pre, Post post, const StateSpace& ss, const ScanCoef& c, int nch)
       : rec_(rec), pre_(pre), post_(post), c_(c), nch_(nch), S_(ss.S) {
     const int S = S_;
-    std::vector<float> mats(static_cast<size_t>(ScanMatsLayout::kCount) * S * S, 0.0f);
+    std::vector<double> mats(static_cast<size_t>(ScanMatsLayout::kCount) * S * S, 0.0);
     auto put = [&](int idx, const std::vector<double>& m) {
-      const auto f = to_f32(m);
-      std::copy(f.begin(), f.end(), mats.begin() + static_cast<size_t>(idx) * S * S);
+      std::copy(m.begin(), m.end(), mats.begin() + static_cast<size_t>(idx) * S * S);
     };
     const auto Mc = mat_pow(ss.A, S, kScanC);
     auto p = Mc;
@@ -39,7 +38,7 @@ class ScanStage {
       p = mat_mul(p, p, S);
     }
     for (int L = 0; L < 64; ++L) put(ScanMatsLayout::kLane + L, mat_pow(ss.A, S, static_cast<uint64_t>(kScanC) * L));
-    mats_.upload(mats.data(), mats.size() * sizeof(float));
+    mats_.upload(mats.data(), mats.size() * sizeof(double));
     for (auto& c0 : carry_) c0.resize(static_cast<size_t>(nch_) * kScanCarry * sizeof(float));
   }
   void set_osc(const Oscillator& o) {
@@ -58,7 +57,7 @@ class ScanStage {
   void run(const void* x, long long x_stride, long long n, void* y, long long y_stride, long long k0,
            hipStream_t s) {
     const long long nblk = (n + kScanCH - 1) / kScanCH;
-    ws_.resize(static_cast<size_t>(2 * nblk * nch_ * S_ + 16) * sizeof(float));
+    ws_.resize(static_cast<size_t>(2 * nblk * nch_ * S_ + 16) * sizeof(double));
     ScanArgs a{};
     a.x = x;
     a.x_stride = x_stride;
@@ -69,9 +68,9 @@ class ScanStage {
     a.translate = translate_ ? 1 : 0;
     a.step = step_;
     a.tab = tab_.size() ? tab_.as<f2>() : nullptr;
-    a.mats = mats_.as<float>();
-    a.aggs = ws_.as<float>();
-    a.sin = ws_.as<float>() + nblk * nch_ * S_;
+    a.mats = mats_.as<double>();
+    a.aggs = ws_.as<double>();
+    a.sin = ws_.as<double>() + nblk * nch_ * S_;
     a.carry_in = carry_[cur_].as<float>();
     a.carry_out = carry_[cur_ ^ 1].as<float>();
     a.c = c_;

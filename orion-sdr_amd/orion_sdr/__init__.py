@@ -84,7 +84,6 @@ def _load():
         "orion_cw_envelope_demod_set_gain": (i, [vp, f]),
         "orion_wbfm_chain_new": (vp, [C.POINTER(WbfmParams)]),
         "orion_wbfm_chain_batch_new": (vp, [C.POINTER(WbfmParams), fp, sz]),
-        "orion_wbfm_chain_set_tiling": (i, [vp, i, i]),
         "orion_block_process": (i, [vp, vp, sz, vp, sz, C.POINTER(WorkReport)]),
         "orion_block_process_device": (i, [vp, vp, sz, vp, sz, vp, C.POINTER(WorkReport)]),
         "orion_block_reset": (i, [vp]), "orion_block_free": (None, [vp]),
@@ -350,9 +349,6 @@ class WbfmChain(_Block):
             offs = np.ascontiguousarray(offs)
             h = _L.orion_wbfm_chain_batch_new(C.byref(p), _fptr(offs), offs.size)
         super().__init__(h)
-
-    def set_tiling(self, outputs_per_wg: int, warmup: int):
-        _check(_L.orion_wbfm_chain_set_tiling(self._h, outputs_per_wg, warmup))
 
 
 # ---- designs (host) ----------------------------------------------------------
