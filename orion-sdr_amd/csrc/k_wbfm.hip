@@ -138,9 +138,13 @@ __global__ __launch_bounds__(NT) void k_wbfm_front(const WbfmArgs a, const WbfmF
   }
 }
 
+// Back-kernel LDS slot of local sample l (l = -128 .. kBackSpan-1): one pad slot
+// every 8 so the audio FIR's stride-8-per-lane reads are bank-conflict free.
+__device__ __forceinline__ int fpos(int l) { return (l + 128) + ((l + 128) >> 3); }
+
 __global__ __launch_bounds__(NT) void k_wbfm_back(const WbfmArgs a, const WbfmBackConst C) {
   constexpr int H = 128;  // f history slots in front of the span
-  __shared__ __attribute__((aligned(16))) float F[H + kBackSpan + 16];
+  __shared__ __attribute__((aligned(16))) float F[((H + kBackSpan + 32) * 9) / 8];
   __shared__ double tot[4][4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int ch = blockIdx.y;
@@ -154,14 +158,14 @@ __global__ __launch_bounds__(NT) void k_wbfm_back(const WbfmArgs a, const WbfmBa
   const float* __restrict__ ci = a.carry_in + ch * kWbfmCarry;
   const BiquadK bq{C.b0, C.b1, C.b2, C.a1, C.a2};
 
-  for (int i = t; i < cnt; i += NT) F[H + i] = phi[js + i];
-  if (first && t < H) F[t] = ci[8 + t];  // f[-128 .. -1] from the previous call
+  for (int i = t; i < cnt; i += NT) F[fpos(i)] = phi[js + i];
+  if (first && t < H) F[fpos(t - H)] = ci[8 + t];  // f[-128 .. -1] from the previous call
   __syncthreads();
 
   // ---- LpCascade: lane chunk [19 t, 19 t + 19) ----
   float xs[kBackC];
 #pragma unroll
-  for (int i = 0; i < kBackC; ++i) xs[i] = F[H + kBackC * t + i];
+  for (int i = 0; i < kBackC; ++i) xs[i] = F[fpos(kBackC * t + i)];
   float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int i = 0; i < kBackC; ++i)
@@ -195,7 +199,7 @@ __global__ __launch_bounds__(NT) void k_wbfm_back(const WbfmArgs a, const WbfmBa
 #pragma unroll
   for (int i = 0; i < kBackC; ++i) {
     const int li = kBackC * t + i;
-    if (li < cnt) F[H + li] = lp4_step(bq, ef, xs[i]);
+    if (li < cnt) F[fpos(li)] = lp4_step(bq, ef, xs[i]);
   }
   const bool last = a_end == a.n_dec;
   if (last && kBackC * t <= cnt - 1 && cnt - 1 < kBackC * t + kBackC) {
@@ -206,23 +210,40 @@ __global__ __launch_bounds__(NT) void k_wbfm_back(const WbfmArgs a, const WbfmBa
   __syncthreads();
 
   // ---- audio FIR (fir.rs:57-66, quirk-mapped taps) over [a0, a_end) ----
-  float* __restrict__ y = a.y + ch * a.y_stride;
+  // Lane t owns outputs a0 + 8t + i and a0 + 2048 + 8t + i (i < 8), accumulated as
+  // float2 pairs so one v_pk_fma_f32 applies a tap to both halves; the window
+  // pairs (f[j-k], f[j+2048-k]) come from two b32 LDS reads at stride 9 floats per
+  // lane (F is padded one slot every 8: conflict-free). Taps: one s_load_dwordx16
+  // per block of 16.
+  {
+    constexpr int R = 8, HALF = kBackA / 2, KA = 128;
+    const int o0 = static_cast<int>(a0 - js) + R * t;  // local index of the first output
+    f2 acc[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc[i] = f2{0.0f, 0.0f};
 #pragma unroll 1
-  for (int pass = 0; pass < kBackA / (2 * NT); ++pass) {
-    const long long jg = a0 + 2 * t + 2 * NT * pass;
-    if (jg >= a_end) break;
-    float acc0 = 0.0f, acc1 = 0.0f;
-    fir2_blocked<128>(
-        [&](long long e2, float& w0, float& w1) {
-          const f2 w = *reinterpret_cast<const f2*>(F + H + (e2 - js));
-          w0 = w.x;
-          w1 = w.y;
-        },
-        jg, [&](int k) { return C.a[k]; }, acc0, acc1);
-    y[jg] = acc0;
-    if (jg + 1 < a_end) y[jg + 1] = acc1;
+    for (int kb = 0; kb < KA / 16; ++kb) {
+      // output i, tap k = 16 kb + kk uses f[o0 + i - k]: window w = i + 15 - kk
+      const int wbase = o0 - 16 * kb - 15;
+      f2 w[R + 15];
+#pragma unroll
+      for (int m = 0; m < R + 15; ++m) w[m] = f2{F[fpos(wbase + m)], F[fpos(wbase + m + HALF)]};
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const f2 tap = splat2(C.a[16 * kb + kk]);
+#pragma unroll
+        for (int i = 0; i < R; ++i) acc[i] = fma2(tap, w[i + 15 - kk], acc[i]);
+      }
+    }
+    float* __restrict__ y = a.y + ch * a.y_stride;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const long long j = a0 + R * t + i;
+      if (j < a_end) y[j] = acc[i].x;
+      if (j + HALF < a_end) y[j + HALF] = acc[i].y;
+    }
   }
-  if (last && t < H) a.carry_out[ch * kWbfmCarry + 8 + t] = F[H + (a.n_dec - H + t - js)];
+  if (last && t < H) a.carry_out[ch * kWbfmCarry + 8 + t] = F[fpos(static_cast<int>(a.n_dec - H + t - js))];
 }
 
 }  // namespace

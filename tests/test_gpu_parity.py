@@ -30,8 +30,22 @@ def stream(blk, x, chunk):
 
 
 def report(name, v, tol):
-    print(f"[parity] {name}: {v:.3e} (tol {tol:.0e})")
-    assert v <= tol, f"{name}: {v:.3e} > {tol:.0e}"
+    print(f"[parity] {name}: {v:.3e} (tol {tol:.1e})")
+    assert v <= tol, f"{name}: {v:.3e} > {tol:.1e}"
+
+
+def ulp_floor(fn, x):
+    """The reference's own sensitivity: nrmse between fn(x) and fn(x*(1+2^-23))/(1+2^-23).
+    Narrow IIRs (poles near 1) and the FM discriminator amplify last-bit rounding;
+    no f32 implementation can be closer to the reference than this floor."""
+    s = np.float32(1.0 + 2.0 ** -23)
+    return nrmse(fn((x * s).astype(x.dtype)) / s, fn(x))
+
+
+def floor_tol(base, fn, x):
+    f = ulp_floor(fn, x)
+    print(f"[parity]   reference 1-ulp sensitivity floor {f:.3e}")
+    return max(base, 2.0 * f)
 
 
 # ---- Rotator (a1) -------------------------------------------------------------------
@@ -134,13 +148,17 @@ def test_fir_lowpass_iq(gpu_lib, oracle):
 # ---- IIR blocks (a6, a7) -------------------------------------------------------------------
 def test_lp_cascade_and_dc(gpu_lib, oracle):
     L = gpu_lib.LpCascade(1.25e6, 13.5e3)
-    report("lp_cascade golden nrmse", nrmse(L.process(GOLD["x_r"]), GOLD["lp_cascade_out"]), 1e-6)
+    xr = GOLD["x_r"]
+    report("lp_cascade golden nrmse", nrmse(L.process(xr), GOLD["lp_cascade_out"]),
+           floor_tol(1e-6, lambda v: oracle.lp_cascade(v, 1.25e6, 13.5e3), xr))
     x = RNG.standard_normal(300_000).astype(np.float32)
     got = stream(gpu_lib.LpCascade(48e3, 4500.0), x, 100_000)
-    report("lp_cascade 3e5 nrmse", nrmse(got, oracle.lp_cascade(x, 48e3, 4500.0)), 1e-6)
+    report("lp_cascade 3e5 nrmse", nrmse(got, oracle.lp_cascade(x, 48e3, 4500.0)),
+           floor_tol(1e-6, lambda v: oracle.lp_cascade(v, 48e3, 4500.0), x))
     xd = (x + 0.3).astype(np.float32)
     got = stream(gpu_lib.DcBlocker(48e3, 2.0), xd, 100_000)
-    report("dc_blocker 3e5 nrmse", nrmse(got, oracle.dc_blocker(xd, 48e3, 2.0)), 1e-5)
+    report("dc_blocker 3e5 nrmse", nrmse(got, oracle.dc_blocker(xd, 48e3, 2.0)),
+           floor_tol(1e-6, lambda v: oracle.dc_blocker(v, 48e3, 2.0), xd))
 
 
 # ---- demodulators (a9-a12) -------------------------------------------------------------------
