@@ -27,6 +27,15 @@ struct HipError : std::runtime_error {
 
 #define ORION_LAUNCH_CHECK() ORION_HIP(hipGetLastError())
 
+// Workgroup barrier for LDS hand-offs only. __syncthreads() on gfx950 also waits
+// vmcnt(0), which drains every outstanding global load — including a prefetch
+// meant to stay in flight across the barrier. This waits for this wave's LDS
+// operations (lgkmcnt) and then barriers; global loads keep flying and the
+// compiler still inserts its own vmcnt wait before their first use.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 splat2(float x) { return f2{x, x}; }
 

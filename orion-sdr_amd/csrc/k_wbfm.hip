@@ -45,36 +45,36 @@ __device__ __forceinline__ float lp4_step(const BiquadK& bq, float (&s)[4], floa
   return bq.step(s[2], s[3], y0);
 }
 
+// Prefetch of one tile's inputs: branch-free 16-B loads at clamped addresses, so
+// the loads stay in flight (a branchy prefetch makes the compiler merge register
+// copies behind an s_waitcnt vmcnt(0)). Tiles that reach before x[0] or past
+// x[n-1] are re-loaded exactly (history / zero padding) at staging time.
 template <bool A16>
 __device__ __forceinline__ void front_load(const WbfmArgs& a, int ch, long long porg, int t,
                                            f2 (&v)[KP][2]) {
-  const f2* __restrict__ x = a.x + ch * a.x_stride;
-  if (porg >= 0 && porg + PW::NS <= a.n) {  // interior tile: plain 16-B loads
+  const bool tiny = a.n < 2;  // nothing safe to clamp into: read the history buffer
+  const f2* __restrict__ x = tiny ? a.hist_in : a.x + ch * a.x_stride;
+  const long long hi = (tiny ? kWbfmHist : (a.n & ~1LL)) - 2;
 #pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      const int p = 2 * t + 2 * NT * k;
-      if (p < PW::NS) {
-        if constexpr (A16) {
-          const f4 w = *reinterpret_cast<const f4*>(x + porg + p);
-          v[k][0] = f2{w.x, w.y};
-          v[k][1] = f2{w.z, w.w};
-        } else {
-          v[k][0] = x[porg + p];
-          v[k][1] = x[porg + p + 1];
-        }
-      }
-    }
-  } else {  // first / last tile: history before 0, zeros past n
-    const f2* __restrict__ hist = a.hist_in + ch * kWbfmHist;
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      const int p = 2 * t + 2 * NT * k;
-      if (p < PW::NS) {
-        v[k][0] = load_hist(x, a.n, hist, kWbfmHist, porg + p);
-        v[k][1] = load_hist(x, a.n, hist, kWbfmHist, porg + p + 1);
+  for (int k = 0; k < KP; ++k) {
+    const int p = 2 * t + 2 * NT * k;
+    if (p < PW::NS) {
+      long long P = porg + p;
+      P = P < 0 ? 0 : (P > hi ? hi : P);
+      if constexpr (A16) {
+        const f4 w = *reinterpret_cast<const f4*>(x + P);
+        v[k][0] = f2{w.x, w.y};
+        v[k][1] = f2{w.z, w.w};
+      } else {
+        v[k][0] = x[P];
+        v[k][1] = x[P + 1];
       }
     }
   }
+}
+
+__device__ __forceinline__ bool front_boundary(const WbfmArgs& a, long long porg) {
+  return porg < 0 || porg + PW::NS > a.n;
 }
 
 template <bool A16>
@@ -97,6 +97,8 @@ __global__ __launch_bounds__(NT, 4) void k_wbfm_front(const WbfmArgs a, const Wb
   f2 v[KP][2];
   f2 tb0 = f2{1.0f, 0.0f}, tb1 = f2{1.0f, 0.0f};  // e^{j theta 2t}, e^{j theta (2t+1)}
   const f2* __restrict__ tabc = a.tab;
+  uint64_t step = 0;
+  f2 cprev = f2{1.0f, 0.0f};
   int cur_ch = -1;
   int u = lo + static_cast<int>(blockIdx.x >> 3);
   if (u < hi) {
@@ -110,22 +112,35 @@ __global__ __launch_bounds__(NT, 4) void k_wbfm_front(const WbfmArgs a, const Wb
     const long long J = static_cast<long long>(b) * kWbfmPhi;  // first phi of this tile
     const long long Jd = J - 1;                                 // first decimated output
     const long long porg = static_cast<long long>(M) * (Jd - Q);
-    if (ch != cur_ch) {  // this channel's phasor table (L2-resident)
+    if (ch != cur_ch) {  // per-channel constants, loaded before any prefetch is in flight
       tabc = a.tab + static_cast<long long>(ch) * PW::NS;
       const f4 tv = *reinterpret_cast<const f4*>(tabc + 2 * t);
       tb0 = f2{tv.x, tv.y};
       tb1 = f2{tv.z, tv.w};
+      step = a.step[ch];
+      const float* ci = a.carry_in + ch * kWbfmCarry;
+      cprev = f2{ci[4], ci[5]};  // d[-1]: the last decimated sample of the previous call
       cur_ch = ch;
     }
     // ---- stage: NCO mix, polyphase scatter ----
     // e^{j theta (2t + 512k)} = e^{j theta 2t} * e^{j theta 512k}; the second
-    // factor is uniform (scalar loads of tab[512k]).
+    // factor is uniform (scalar loads of tab[512k]). A boundary tile (before x[0]
+    // or past x[n-1]) replaces the clamped prefetch by the exact samples.
+    const bool bnd = front_boundary(a, porg);
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
-      if (2 * t + 2 * NT * k < PW::NS) {
+      const int p = 2 * t + 2 * NT * k;
+      if (p < PW::NS) {
+        f2 x0 = v[k][0], x1 = v[k][1];
+        if (bnd) {
+          const f2* __restrict__ xc = a.x + ch * a.x_stride;
+          const f2* __restrict__ hc = a.hist_in + ch * kWbfmHist;
+          x0 = load_hist(xc, a.n, hc, kWbfmHist, porg + p);
+          x1 = load_hist(xc, a.n, hc, kWbfmHist, porg + p + 1);
+        }
         const f2 ek = tabc[2 * NT * k];
-        U[s0 + 64 * k] = cmul_rot(v[k][0], cmul(tb0, ek));
-        U[s1 + 64 * k] = cmul_rot(v[k][1], cmul(tb1, ek));
+        U[s0 + 64 * k] = cmul_rot(x0, cmul(tb0, ek));
+        U[s1 + 64 * k] = cmul_rot(x1, cmul(tb1, ek));
       }
     }
     // ---- prefetch the next tile (lands during this tile's compute) ----
@@ -137,21 +152,18 @@ __global__ __launch_bounds__(NT, 4) void k_wbfm_front(const WbfmArgs a, const Wb
         front_load<A16>(a, chn, static_cast<long long>(M) * (Jdn - Q), t, v);
       }
     }
-    __syncthreads();
+    lds_barrier();  // LDS-only: the prefetch stays in flight
 
     // ---- polyphase FIR at the kept outputs; common phasor of the tile ----
     {
       f2 acc[PW::R];
       PW::compute(U, t, [&](int c, int q) { return C.g[c * Q + q]; }, acc);
-      const f2 S = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1), a.step[ch]);
+      const f2 S = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1), step);
       D[2 * t] = cmul(acc[0], S);
       D[2 * t + 1] = cmul(acc[1], S);
-      if (b == 0 && t == 0) {  // d[-1]: the last decimated sample of the previous call
-        const float* ci = a.carry_in + ch * kWbfmCarry;
-        D[0] = f2{ci[4], ci[5]};
-      }
+      if (b == 0 && t == 0) D[0] = cprev;
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---- FM discriminator (fm.rs:60-68) ----
     float* __restrict__ phi = a.phi + ch * a.phi_stride;
