@@ -44,6 +44,13 @@ __device__ __forceinline__ f2 splat2(float x) { return f2{x, x}; }
 __device__ __forceinline__ f2 cmul_rot(f2 x, f2 p) {
   return f2{__builtin_fmaf(x.x, p.x, -(x.y * p.y)), __builtin_fmaf(x.y, p.x, x.x * p.y)};
 }
+// cmul_rot with the same roundings, written as packed-f32 ops (v_pk_mul_f32 +
+// v_pk_fma_f32, the negation folded into a source modifier): t = (b*d, a*d)
+// rounded, then (fma(a, c, -t.x), fma(b, c, t.y)) for x = (a, b), p = (c, d).
+__device__ __forceinline__ f2 cmul_rot_pk(f2 x, f2 p) {
+  const f2 t = f2{x.y, x.x} * f2{p.y, p.y};
+  return __builtin_elementwise_fma(x, f2{p.x, p.x}, f2{-t.x, t.y});
+}
 // Plain complex multiply (ours, not a reference op order).
 __device__ __forceinline__ f2 cmul(f2 a, f2 b) {
   return f2{__builtin_fmaf(a.x, b.x, -(a.y * b.y)), __builtin_fmaf(a.x, b.y, a.y * b.x)};
@@ -87,6 +94,15 @@ __device__ __forceinline__ float fm_disc(f2 z, f2 p, float k) {
   const float pr = z.x * p.x + z.y * p.y;
   const float pi = z.y * p.x - z.x * p.y;
   return atan2_approx(pi, pr) * k;
+}
+
+// fm_disc with the same roundings as packed ops: (z.x p.x, z.y p.x) and
+// (z.y p.y, z.x p.y) rounded, then (sum, difference).
+__device__ __forceinline__ float fm_disc_pk(f2 z, f2 p, float k) {
+  const f2 a = z * f2{p.x, p.x};
+  const f2 b = f2{z.y, z.x} * f2{p.y, p.y};
+  const f2 s = a + f2{b.x, -b.y};
+  return atan2_approx(s.y, s.x) * k;
 }
 
 // PmQuadratureDemod, demodulate/pm.rs:56-57: num-complex z * conj(prev),

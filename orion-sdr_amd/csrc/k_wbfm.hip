@@ -24,6 +24,9 @@
 // The first tile / workgroup of each channel starts from the exact state carried
 // from the previous call (last decimated sample, 128 raw inputs, IIR state, last
 // 128 IIR outputs), so k calls equal one call on the concatenation.
+#include <algorithm>
+#include <cstdlib>
+
 #include "iir.hpp"
 #include "kernels.hpp"
 #include "poly.hpp"
@@ -40,10 +43,6 @@ static_assert(PW::NS == kWbfmNS, "staging size");
 constexpr int KP = (PW::NS + 2 * NT - 1) / (2 * NT);  // staged pairs per thread (9)
 static_assert(2 * NT * (KP - 1) + 2 * NT - 1 >= PW::NS - 1, "staging coverage");
 
-__device__ __forceinline__ float lp4_step(const BiquadK& bq, float (&s)[4], float x) {
-  const float y0 = bq.step(s[0], s[1], x);
-  return bq.step(s[2], s[3], y0);
-}
 
 // Prefetch of one tile's inputs: branch-free 16-B loads at clamped addresses, so
 // the loads stay in flight (a branchy prefetch makes the compiler merge register
@@ -77,7 +76,10 @@ __device__ __forceinline__ bool front_boundary(const WbfmArgs& a, long long porg
   return porg < 0 || porg + PW::NS > a.n;
 }
 
-template <bool A16>
+// ABL (timing ablations, never used by the product path; outputs are wrong):
+//   1 no global input loads, 2 no polyphase FIR, 4 no NCO mix, 8 no discriminator,
+//   16 no audio FIR, 32 no LpCascade scan, 64 skip the back kernel.
+template <bool A16, int ABL>
 __global__ __launch_bounds__(NT, 4) void k_wbfm_front(const WbfmArgs a, const WbfmFrontConst C,
                                                       int tiles_per_ch, int nch) {
   __shared__ __attribute__((aligned(16))) f2 U[PW::LDS_F2];
@@ -104,7 +106,12 @@ __global__ __launch_bounds__(NT, 4) void k_wbfm_front(const WbfmArgs a, const Wb
   if (u < hi) {
     const int ch = u / tiles_per_ch;
     const long long Jd = static_cast<long long>(u - ch * tiles_per_ch) * kWbfmPhi - 1;
-    front_load<A16>(a, ch, static_cast<long long>(M) * (Jd - Q), t, v);
+    if constexpr (ABL & 1) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) v[k][0] = v[k][1] = f2{static_cast<float>(t), 1.0f};
+    } else {
+      front_load<A16>(a, ch, static_cast<long long>(M) * (Jd - Q), t, v);
+    }
   }
   for (; u < hi; u += g8) {
     const int ch = u / tiles_per_ch;
@@ -138,9 +145,14 @@ __global__ __launch_bounds__(NT, 4) void k_wbfm_front(const WbfmArgs a, const Wb
           x0 = load_hist(xc, a.n, hc, kWbfmHist, porg + p);
           x1 = load_hist(xc, a.n, hc, kWbfmHist, porg + p + 1);
         }
-        const f2 ek = tabc[2 * NT * k];
-        U[s0 + 64 * k] = cmul_rot(x0, cmul(tb0, ek));
-        U[s1 + 64 * k] = cmul_rot(x1, cmul(tb1, ek));
+        if constexpr (ABL & 4) {
+          U[s0 + 64 * k] = x0;
+          U[s1 + 64 * k] = x1;
+        } else {
+          const f2 ek = tabc[2 * NT * k];
+          U[s0 + 64 * k] = cmul_rot(x0, cmul(tb0, ek));
+          U[s1 + 64 * k] = cmul_rot(x1, cmul(tb1, ek));
+        }
       }
     }
     // ---- prefetch the next tile (lands during this tile's compute) ----
@@ -149,7 +161,7 @@ __global__ __launch_bounds__(NT, 4) void k_wbfm_front(const WbfmArgs a, const Wb
       if (un < hi) {
         const int chn = un / tiles_per_ch;
         const long long Jdn = static_cast<long long>(un - chn * tiles_per_ch) * kWbfmPhi - 1;
-        front_load<A16>(a, chn, static_cast<long long>(M) * (Jdn - Q), t, v);
+        if constexpr (!(ABL & 1)) front_load<A16>(a, chn, static_cast<long long>(M) * (Jdn - Q), t, v);
       }
     }
     lds_barrier();  // LDS-only: the prefetch stays in flight
@@ -157,7 +169,12 @@ __global__ __launch_bounds__(NT, 4) void k_wbfm_front(const WbfmArgs a, const Wb
     // ---- polyphase FIR at the kept outputs; common phasor of the tile ----
     {
       f2 acc[PW::R];
-      PW::compute(U, t, [&](int c, int q) { return C.g[c * Q + q]; }, acc);
+      if constexpr (ABL & 2) {
+        acc[0] = U[PW::R * t];
+        acc[1] = U[PW::R * t + 1];
+      } else {
+        PW::compute(U, t, [&](int c, int q) { return C.g[c * Q + q]; }, acc);
+      }
       const f2 S = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1), step);
       D[2 * t] = cmul(acc[0], S);
       D[2 * t + 1] = cmul(acc[1], S);
@@ -171,7 +188,11 @@ __global__ __launch_bounds__(NT, 4) void k_wbfm_front(const WbfmArgs a, const Wb
     for (int r = 0; r < 2; ++r) {
       const int i = 2 * t + r;
       const long long j = J + i;
-      if (i < kWbfmPhi && j < a.n_dec) phi[j] = fm_disc(D[i + 1], D[i], C.k);
+      if constexpr (ABL & 8) {
+        if (i < kWbfmPhi && j < a.n_dec) phi[j] = D[i + 1].x + D[i].y;
+      } else {
+        if (i < kWbfmPhi && j < a.n_dec) phi[j] = fm_disc(D[i + 1], D[i], C.k);
+      }
     }
     // ---- carried state: last decimated sample and raw history ----
     if (J <= a.n_dec - 1 && a.n_dec - 1 < J + kWbfmPhi) {
@@ -190,152 +211,693 @@ __global__ __launch_bounds__(NT, 4) void k_wbfm_front(const WbfmArgs a, const Wb
   }
 }
 
-// ---- back kernel LDS images ---------------------------------------------------
-// F: phi staging, local sample l = 0 .. kBackSpan-1 (plain; read once by the IIR).
-// P: audio-FIR window pairs P[l] = (f[l], f[l + 2048]) for l = -128 .. 2815, one
-//    pad slot every 8 pairs (lane stride 8 -> 18 dwords: ds_read_b64 conflict-free).
-//    P aliases F: F is dead once every lane holds its IIR inputs in registers.
+// ---- front, wave-independent form ----------------------------------------------
+// One wave per workgroup and no s_barrier anywhere: every LDS hand-off is inside
+// one wave (DS operations of a wave complete in order; wave_lds_fence keeps the
+// compiler from reordering around them). Each wave owns a contiguous range of
+// decimated outputs [A, B) and walks it in tiles of TW = 64R outputs, one tile's
+// 8 TW new inputs prefetched into registers while the previous tile computes.
+// Consecutive tiles share 17 polyphase rows (the FIR's Q-row history): they are
+// copied inside LDS from the tail to the head of each row, times e^{-j theta NEW}
+// so that every tile is NCO-mixed relative to its own origin (the tile's common
+// phasor multiplies its outputs, as in the persistent form).
+// R = 6: lanes read 6-output windows at a 48-B stride (three 16-B bank slots, odd,
+// so the 16-lane ds_read_b128 groups are conflict-free); 11 b128 reads and 96
+// packed FMAs per lane and phase; 25.7 KB of LDS per wave (6 waves per CU).
+template <int R>
+struct Fw {
+  static constexpr int TW = 64 * R;      // decimated outputs per tile
+  static constexpr int NEW = M * TW;     // inputs entering per tile
+  static constexpr int KL = NEW / 128;   // 2-sample loads per lane per tile (4R)
+  static constexpr int LR = TW + Q + 2;  // row pitch: rows hold i = 0 .. TW+Q (+1 pad)
+  static constexpr int WIN = (R + Q) / 2;  // b128 window reads per lane and phase
+  static constexpr int LDS_F2 = M * LR;
+  static_assert(LR % 16 == 2, "row pitch = 2 mod 16 (phase-scattered b64 stores)");
+  static_assert((R % 2) == 0 && NEW <= kWbfmNS, "phasor table covers the tile");
+};
+
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Lane l receives lane l-1's value; lane 0 receives `first` (DPP wave_shr:1).
+__device__ __forceinline__ float wave_shr1(float v, float first) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(first), __float_as_int(v), 0x138,
+                                                    0xf, 0xf, false));
+}
+
+// Prefetch of a tile's new samples x[B + o], o = 2l + 128k, B = porg + 8Q.
+// Large inputs (CLAMP = false, n >= 2 NEW): the uniform base is clamped into
+// [0, n - NEW], so interior tiles load exactly and one offset register serves
+// every load; a boundary tile then loads shifted samples, all of which the
+// staging fixup rewrites. Small inputs (CLAMP = true): per-lane clamp of the
+// 32-bit offset to [0, n-2] (only the out-of-range samples are wrong).
+template <int R, bool A16, bool CLAMP>
+__device__ __forceinline__ void front2_load(const f2* __restrict__ x, long long n, long long porg,
+                                            int l, f2 (&v)[Fw<R>::KL][2]) {
+  const long long B = porg + 8 * Q;
+  const f2* __restrict__ xb;
+  int lo = 0, hi = 0;
+  if constexpr (CLAMP) {
+    constexpr long long kSat = 1LL << 30;
+    lo = static_cast<int>(max(-B, -kSat));                                   // even
+    hi = static_cast<int>(min(max((n - 2 - B) & ~1LL, -kSat), kSat));        // even, >= lo
+    xb = x + B;
+  } else {
+    xb = x + min(max(B, 0LL), (n - Fw<R>::NEW) & ~1LL);
+  }
+#pragma unroll
+  for (int k = 0; k < Fw<R>::KL; ++k) {
+    const int o = CLAMP ? min(max(2 * l + 128 * k, lo), hi) : 2 * l + 128 * k;
+    if constexpr (A16) {
+      // Nontemporal: the input is read once; streaming it past the caches keeps
+      // the phi / output lines resident (measured 6.9 vs 6.0 TB/s, membench).
+      const f4 w = __builtin_nontemporal_load(reinterpret_cast<const f4*>(xb + o));
+      v[k][0] = f2{w.x, w.y};
+      v[k][1] = f2{w.z, w.w};
+    } else {
+      v[k][0] = xb[o];
+      v[k][1] = xb[o + 1];
+    }
+  }
+}
+
+// One polyphase phase: window w (b128 pairs of U[c][R l ..]) against taps t.
+template <int R>
+__device__ __forceinline__ void front2_phase(const f4 (&w)[Fw<R>::WIN], const float (&t)[Q], f2 (&d)[R]) {
+#pragma unroll
+  for (int h = 0; h < Fw<R>::WIN; ++h) {
+    const f2 w0 = f2{w[h].x, w[h].y}, w1 = f2{w[h].z, w[h].w};
+    // window entry m -> output rho uses tap q = rho + Q - m
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int q0 = r + Q - 2 * h, q1 = r + Q - 2 * h - 1;
+      if (q0 >= 0 && q0 < Q) d[r] = fma2(splat2(t[q0]), w0, d[r]);
+      if (q1 >= 0 && q1 < Q) d[r] = fma2(splat2(t[q1]), w1, d[r]);
+    }
+  }
+}
+
+template <int R>
+__device__ __forceinline__ void front2_window(const f2* __restrict__ U, int l, int c, f4 (&w)[Fw<R>::WIN]) {
+  const f4* row = reinterpret_cast<const f4*>(U + c * Fw<R>::LR + R * l);
+#pragma unroll
+  for (int h = 0; h < Fw<R>::WIN; ++h) w[h] = row[h];
+}
+__device__ __forceinline__ void front2_taps(const float* __restrict__ g, int c, float (&t)[Q]) {
+#pragma unroll
+  for (int q = 0; q < Q; ++q) t[q] = g[c * Q + q];
+}
+
+// Polyphase FIR over the 8 phases (rolled: SGPR taps stay at 16 per phase).
+template <int R>
+__device__ __forceinline__ void front2_decim(const f2* __restrict__ U, int l, const float* __restrict__ g,
+                                             f2 (&d)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) d[r] = f2{0.0f, 0.0f};
+#pragma unroll 1
+  for (int c = 0; c < M; ++c) {
+    f4 w[Fw<R>::WIN];
+    float t[Q];
+    front2_window<R>(U, l, c, w);
+    front2_taps(g, c, t);
+    front2_phase<R>(w, t, d);
+  }
+}
+
+template <int R, bool A16, int ABL, bool CLAMP = false>
+__global__ __launch_bounds__(64, R <= 2 ? 3 : 2) void k_wbfm_front2(const WbfmArgs a, const WbfmFrontConst C,
+                                                    long long L, int wpc) {
+  using G = Fw<R>;
+  __shared__ __attribute__((aligned(16))) f2 U[G::LDS_F2];
+  const int l = threadIdx.x;
+  const int ch = blockIdx.x / wpc;
+  const long long A = static_cast<long long>(blockIdx.x - ch * wpc) * L;
+  const long long B = min(A + L, a.n_dec);
+  if (A >= B) return;
+  const int ntiles = static_cast<int>((B - A + G::TW) / G::TW);  // outputs A-1 .. B-1
+
+  const f2* __restrict__ tabc = a.tab + static_cast<long long>(ch) * kWbfmNS;
+  const bool tiny = a.n < 2;
+  const f2* __restrict__ xc = a.x + ch * a.x_stride;
+  const f2* __restrict__ xl = tiny ? a.hist_in + ch * kWbfmHist : xc;  // clamp target
+  const long long nl = tiny ? kWbfmHist : a.n;
+  const f2* __restrict__ hc = a.hist_in + ch * kWbfmHist;
+  const uint64_t step = a.step[ch];
+  const float* __restrict__ ci = a.carry_in + ch * kWbfmCarry;
+  const f2 cprev = f2{ci[4], ci[5]};
+  float* __restrict__ phi = a.phi + ch * a.phi_stride;
+
+  // Lane phasors: new samples p = 8Q + 2l + 128k (k < KL) -> e^{j theta p} =
+  // tb * tab[128k]; halo samples p = 2l, 2l+1 of the first tile -> tab[p].
+  const f4 tv = *reinterpret_cast<const f4*>(tabc + 8 * Q + 2 * l);
+  const f2 tb0 = f2{tv.x, tv.y}, tb1 = f2{tv.z, tv.w};
+  // Lane phasors e^{j theta p} of the new samples, p = 8Q + 2l + 128k (+1):
+  // the same for every tile (each tile is mixed relative to its own origin).
+  f2 ph[R <= 2 ? G::KL : 1][2];
+  if constexpr (R <= 2) {
+#pragma unroll
+    for (int k = 0; k < G::KL; ++k) {
+      const f2 ek = tabc[128 * k];
+      ph[k][0] = cmul(tb0, ek);
+      ph[k][1] = cmul(tb1, ek);
+    }
+  }
+  const f2 cn = tabc[G::NEW];
+  const f2 corr = f2{cn.x, -cn.y};  // e^{-j theta NEW}
+  const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
+  const int s0 = c0 * G::LR + (8 * Q + 2 * l + c0) / 8;
+  const int s1 = c1 * G::LR + (8 * Q + 2 * l + 1 + c1) / 8;
+
+  long long porg = 8LL * (A - 1 - Q);  // x index of staged sample p = 0
+  f2 v[G::KL][2];
+  if constexpr (ABL & 1) {
+#pragma unroll
+    for (int k = 0; k < G::KL; ++k) v[k][0] = v[k][1] = f2{static_cast<float>(l), 1.0f};
+  } else {
+    front2_load<R, A16, CLAMP>(xl, nl, porg, l, v);
+  }
+  {  // halo rows of the first tile (p = 2l, 2l+1), mixed with tab[p]
+    const f4 th = *reinterpret_cast<const f4*>(tabc + 2 * l);
+    const f2 x0 = load_hist(xc, a.n, hc, kWbfmHist, porg + 2 * l);
+    const f2 x1 = load_hist(xc, a.n, hc, kWbfmHist, porg + 2 * l + 1);
+    U[c0 * G::LR + (2 * l + c0) / 8] = cmul_rot(x0, f2{th.x, th.y});
+    U[c1 * G::LR + (2 * l + 1 + c1) / 8] = cmul_rot(x1, f2{th.z, th.w});
+  }
+
+  f2 Sv = f2{1.0f, 0.0f};  // lane m: common phasor of tile nb + m
+  int nb = 0;
+  f2 carry = f2{0.0f, 0.0f};
+  for (int n = 0; n < ntiles; ++n, porg += G::NEW) {
+    const long long jd0 = A - 1 + static_cast<long long>(n) * G::TW;
+    if (n == nb) {  // tile phasors for the next 64 tiles, one per lane
+      Sv = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1 + static_cast<long long>(l) * G::NEW), step);
+      nb += 64;
+    }
+    // ---- halo: the previous tile's last 17 rows -> rows 0..16 (x e^{-j theta NEW}) ----
+    if (n > 0 && !(ABL & 256)) {
+#pragma unroll
+      for (int r2 = 0; r2 < 2; ++r2) {
+        const int e = l + 64 * r2;
+        if (e < 72) {
+          const int c = e / 9, h = e - 9 * c;
+          const f4 w = *reinterpret_cast<const f4*>(U + c * G::LR + G::TW + 2 * h);
+          const f2 y0 = cmul(f2{w.x, w.y}, corr), y1 = cmul(f2{w.z, w.w}, corr);
+          *reinterpret_cast<f4*>(U + c * G::LR + 2 * h) = f4{y0.x, y0.y, y1.x, y1.y};
+        }
+      }
+      wave_lds_fence();
+    }
+    // ---- stage the new samples: NCO mix, polyphase scatter ----
+    const bool bnd = porg < 0 || porg + 8LL * (G::TW + Q) > a.n;
+    if constexpr (R <= 2) {  // lane phasors precomputed once per wave (2 KL registers pairs)
+#pragma unroll
+      for (int k = 0; k < G::KL; ++k) {
+        if constexpr (ABL & 4) {
+          U[s0 + 16 * k] = v[k][0];
+          U[s1 + 16 * k] = v[k][1];
+        } else {
+          U[s0 + 16 * k] = cmul_rot_pk(v[k][0], ph[k][0]);
+          U[s1 + 16 * k] = cmul_rot_pk(v[k][1], ph[k][1]);
+          if (k % 4 == 3) asm volatile("" ::: "memory");  // bound the live temporaries
+        }
+      }
+    } else {
+      // Opaque per tile: stops the compiler from hoisting all 2*KL lane phasors
+      // tb * tab[128k] out of the tile loop (96 live VGPRs for R = 6).
+      int opaque_zero;
+      asm volatile("s_mov_b32 %0, 0" : "=s"(opaque_zero));
+      const f2* tabk = tabc + opaque_zero;
+#pragma unroll
+      for (int k = 0; k < G::KL; ++k) {
+        const f2 x0 = v[k][0], x1 = v[k][1];
+        if constexpr (ABL & 4) {
+          U[s0 + 16 * k] = x0;
+          U[s1 + 16 * k] = x1;
+        } else {
+          const f2 ek = tabk[128 * k];
+          U[s0 + 16 * k] = cmul_rot_pk(x0, cmul(tb0, ek));
+          U[s1 + 16 * k] = cmul_rot_pk(x1, cmul(tb1, ek));
+        }
+      }
+    }
+    // ---- prefetch the next tile (lands during this tile's FIR) ----
+    // The compiler fence keeps the new loads below the staging stores, so the
+    // current and the next tile's registers are never live together.
+    asm volatile("" ::: "memory");
+    if constexpr (!(ABL & 1))
+      if (n + 1 < ntiles) front2_load<R, A16, CLAMP>(xl, nl, porg + G::NEW, l, v);
+    if (bnd) {
+      // Tile reaching before x[0] or past x[n-1]: the clamped prefetch staged
+      // wrong samples there; rewrite exactly those slots (history / zeros).
+      wave_lds_fence();
+#pragma unroll 1
+      for (int p = 8 * Q + l; p < 8 * (G::TW + Q); p += 64) {
+        const long long P = porg + p;
+        if (!CLAMP || P < 0 || P >= a.n) {  // unclamped loads may be shifted: rewrite all
+          const int c = (-p) & 7;
+          U[c * G::LR + (p + c) / 8] = cmul_rot(load_hist(xc, a.n, hc, kWbfmHist, P), tabc[p]);
+        }
+      }
+    }
+    wave_lds_fence();
+
+    // ---- polyphase FIR: outputs jd0 + R l + rho ----
+    f2 d[R];
+    if constexpr (ABL & 2) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) d[r] = U[R * l + r];
+    } else {
+      front2_decim<R>(U, l, C.g, d);
+    }
+    if constexpr (!(ABL & 1024)) {
+      const int sl = n - (nb - 64);
+      const f2 S = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.x), sl)),
+                      __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.y), sl))};
+#pragma unroll
+      for (int r = 0; r < R; ++r) d[r] = cmul(d[r], S);
+    }
+    if (n == 0 && A == 0 && l == 0) d[0] = cprev;  // d[-1]: carried from the previous call
+
+    // ---- FM discriminator (fm.rs:60-68) ----
+    const f2 pv = (ABL & 1024) ? d[0] : f2{wave_shr1(d[R - 1].x, carry.x), wave_shr1(d[R - 1].y, carry.y)};
+    // Emitted outputs: tile-relative index e = R l + r in [elo, ehi) (32-bit).
+    const int elo = static_cast<int>(max(A - jd0, 0LL));
+    const int ehi = static_cast<int>(min(B - jd0, static_cast<long long>(G::TW)));
+    float* __restrict__ phit = phi + jd0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int e = R * l + r;
+      const f2 pr = r == 0 ? pv : d[r - 1];
+      if constexpr (ABL & 128) {  // timing only: coalesced lane order, wrong data
+        const int ec = l + 64 * r;
+        if (ec >= elo && ec < ehi) phit[ec] = (ABL & 8) ? d[r].x + pr.y : fm_disc_pk(d[r], pr, C.k);
+      } else if constexpr (ABL & 512) {  // timing only: no stores (kept alive)
+        const float o = (ABL & 8) ? d[r].x + pr.y : fm_disc_pk(d[r], pr, C.k);
+        if (o == 1234.5f) phit[e] = o;
+      } else if (e >= elo && e < ehi) {
+        if constexpr (ABL & 8) phit[e] = d[r].x + pr.y;
+        else phit[e] = fm_disc_pk(d[r], pr, C.k);
+      }
+    }
+    carry = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[R - 1].x), 63)),
+               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[R - 1].y), 63))};
+    // ---- carried state: last decimated sample and raw history ----
+    if (jd0 <= a.n_dec - 1 && a.n_dec - 1 < jd0 + G::TW) {
+      const int rl = static_cast<int>(a.n_dec - 1 - jd0);
+      float* co = a.carry_out + ch * kWbfmCarry;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (R * l + r == rl) {
+          co[4] = d[r].x;
+          co[5] = d[r].y;
+          co[6] = 0.0f;
+          co[7] = 0.0f;
+        }
+#pragma unroll
+      for (int t2 = 0; t2 < kWbfmHist / 64; ++t2) {
+        const int t = l + 64 * t2;
+        a.hist_out[ch * kWbfmHist + t] = load_hist(xc, a.n, hc, kWbfmHist, a.n - kWbfmHist + t);
+      }
+    }
+  }
+}
+
+// ---- back kernel ------------------------------------------------------------
+// One workgroup (256 lanes) per block of kBackA = 4096 audio outputs [a0, a0+4096),
+// split into two halves 2048 apart. Each half runs LpCascade over its 2048 phi
+// plus kBackW = 510 samples of zero-state warm-up (double pole, r = 0.953: the
+// transient is < 2e-8 of the state after 510 samples); lane l owns chunk l
+// (kBackC = 10 samples) of both halves and runs them as one packed float2
+// recurrence (v_pk_* ops: the reference's f32 TDF-II roundings, two chunks at
+// once). Chunk states come from an f64 Kogge-Stone scan per half.
+// Local index j = i - a0. Half A covers j in [-510, 2050), half B j + 2048.
+// Block 0 has no warm-up data: its half-A lanes 0..50 see zero input and lane
+// 50's aggregate is replaced by the IIR state carried from the previous call,
+// which then enters lane 51 (j = 0) exactly.
+// LDS: F (phi, j in [-510, 4098), zero outside [0, n_dec)) for pass 1, aliased
+// by P[j] = (f[j], f[j + 2048]) for j in [-124, 2048), the audio FIR's pair image
+// (one v_pk_fma_f32 applies a tap to both halves), one pad slot per 8 pairs
+// (lane stride 9 pairs = 18 dwords: conflict-free ds_read_b64).
 constexpr int kHalf = kBackA / 2;
-constexpr int kPairs = kBackSpan - kBackA + kHalf + 128;  // 2944
-__device__ __forceinline__ int ppos(int l) { return (l + 128) + ((l + 128) >> 3); }
-constexpr int kPSlots = kPairs + kPairs / 8 + 8;
-constexpr int kBackLdsBytes = (kPSlots * 8 > kBackSpan * 4 ? kPSlots * 8 : kBackSpan * 4);
+constexpr int kFSpan = kBackSpan + kHalf;                 // 4608 staged phi
+constexpr int kPairs = kHalf + 124;                       // j in [-124, 2048)
+__host__ __device__ constexpr int ppos(int e) { return e + (e >> 3); }  // e = j + 124
+constexpr int kPDummy = ppos(kPairs) + 1;                 // sink for unneeded warm-up pairs
+constexpr int kPSlots = kPDummy + 1;
+constexpr int kBackLdsBytes = (kPSlots * 8 > kFSpan * 4 ? kPSlots * 8 : kFSpan * 4);
+static_assert(kBackW % kBackC == 0 && 2 * kBackSpan >= kBackA + 2 * kBackW, "back geometry");
 
-__device__ __forceinline__ void put_f(f2* P, int l, float f) {
-  if (l < kPairs - 128) P[ppos(l)].x = f;
-  if (l >= kHalf - 128) P[ppos(l - kHalf)].y = f;
-}
-__device__ __forceinline__ float get_f(const f2* P, int l) {
-  return l < kPairs - 128 ? P[ppos(l)].x : P[ppos(l - kHalf)].y;
-}
+// BiquadK::step on two independent streams: identical roundings, packed ops.
+struct Biquad2 {
+  f2 b0, b1, b2, a1, a2;
+  __device__ __forceinline__ f2 step(f2& z1, f2& z2, f2 x) const {
+    const f2 y = __builtin_elementwise_fma(x, b0, z1);
+    z1 = __builtin_elementwise_fma(x, b1, z2) - a1 * y;
+    z2 = x * b2 - a2 * y;
+    return y;
+  }
+  __device__ __forceinline__ f2 lp4(f2 (&s)[4], f2 x) const {
+    const f2 y0 = step(s[0], s[1], x);
+    return step(s[2], s[3], y0);
+  }
+};
 
-__global__ __launch_bounds__(NT) void k_wbfm_back(const WbfmArgs a, const WbfmBackConst C) {
+template <int ABL>
+__global__ __launch_bounds__(NT, 4) void k_wbfm_back(const WbfmArgs a, const WbfmBackConst C) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[kBackLdsBytes];
-  __shared__ double tot[4][4];
+  __shared__ double tot[4][2][4];
   float* F = reinterpret_cast<float*>(lds);
   f2* P = reinterpret_cast<f2*>(lds);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int ch = blockIdx.y;
   const long long a0 = static_cast<long long>(blockIdx.x) * kBackA;
   const long long a_end = min(a0 + kBackA, a.n_dec);
-  long long js = a0 - (kBackSpan - kBackA);
-  const bool first = js <= 0;
-  if (first) js = 0;
-  const int cnt = static_cast<int>(a_end - js);
+  const bool first = blockIdx.x == 0;
+  const bool last = a_end == a.n_dec;
   const float* __restrict__ phi = a.phi + ch * a.phi_stride;
   const float* __restrict__ ci = a.carry_in + ch * kWbfmCarry;
-  const BiquadK bq{C.b0, C.b1, C.b2, C.a1, C.a2};
+  const Biquad2 bq{splat2(C.b0), splat2(C.b1), splat2(C.b2), splat2(C.a1), splat2(C.a2)};
 
-  for (int i = t; i < cnt; i += NT) F[i] = phi[js + i];
+  // ---- stage phi (zero outside [0, n_dec)) ----
+  for (int e = t; e < kFSpan; e += NT) {
+    const long long i = a0 - kBackW + e;
+    F[e] = (i >= 0 && i < a.n_dec) ? phi[i] : 0.0f;
+  }
   __syncthreads();
+  f2 xs[kBackC];  // (half A, half B) inputs of this lane's chunks
+#pragma unroll
+  for (int i = 0; i < kBackC; i += 2) {  // b64 pairs, 40-B lane stride: conflict-free
+    const f2 u = *reinterpret_cast<const f2*>(F + kBackC * t + i);
+    const f2 w = *reinterpret_cast<const f2*>(F + kBackC * t + i + kHalf);
+    xs[i] = f2{u.x, w.x};
+    xs[i + 1] = f2{u.y, w.y};
+  }
 
-  // ---- LpCascade: lane chunk [19 t, 19 t + 19) ----
-  float xs[kBackC];
+  // ---- pass 1: zero-state chunk aggregates, f64 scan per half ----
+  f2 s[4] = {f2{0, 0}, f2{0, 0}, f2{0, 0}, f2{0, 0}};
+  if constexpr (!(ABL & 32)) {
 #pragma unroll
-  for (int i = 0; i < kBackC; ++i) xs[i] = F[kBackC * t + i];  // stride 19: conflict-free
-  float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int i = 0; i < kBackC; ++i) (void)bq.lp4(s, xs[i]);
+  }
+  double q[2][4];
 #pragma unroll
-  for (int i = 0; i < kBackC; ++i)
-    if (kBackC * t + i < cnt) (void)lp4_step(bq, s, xs[i]);
-  double q[4] = {s[0], s[1], s[2], s[3]};
-  wave_scan_inclusive<4>(q, C.pw, lane);
+  for (int k = 0; k < 4; ++k) {
+    q[0][k] = s[k].x;
+    q[1][k] = s[k].y;
+  }
+  if (first && t == kBackW / kBackC - 1)  // state at j = 0 (previous call) enters lane 51
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[0][k] = ci[k];
+  if constexpr (!(ABL & 32)) {
+#pragma unroll 1
+    for (int st = 0; st < 6; ++st) {
+      const int d = 1 << st;
+      double o[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[h][k] = __shfl_up(q[h][k], d, 64);
+      if (lane >= d) {
+        matvec_acc<4>(C.pw + st * 16, o[0], q[0]);
+        matvec_acc<4>(C.pw + st * 16, o[1], q[1]);
+      }
+    }
+  }
   if (lane == 63)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) tot[wave][i] = q[i];
-  __syncthreads();  // also: every lane has read its xs (F is dead, P may overwrite it)
-  double cw[4];
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) cw[i] = first ? static_cast<double>(ci[i]) : 0.0;
-  for (int w = 0; w < wave; ++w) {
-    double vv[4];
+      for (int k = 0; k < 4; ++k) tot[wave][h][k] = q[h][k];
+  __syncthreads();  // also: every lane holds its inputs (F is dead, P may overwrite it)
+
+  // entering state of this lane's chunks: lanemats[lane] * (state entering the
+  // wave) + the exclusive in-wave prefix
+  f2 ef[4];
+  {
+    double cw[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    for (int w = 0; w < wave; ++w) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) vv[i] = tot[w][i];
-    matvec_acc<4>(C.mw, cw, vv);
+      for (int h = 0; h < 2; ++h) {
+        double vv[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) cw[i] = vv[i];
+        for (int k = 0; k < 4; ++k) vv[k] = tot[w][h][k];
+        matvec_acc<4>(C.mw, cw[h], vv);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cw[h][k] = vv[k];
+      }
+    }
+    double e[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double o = __shfl_up(q[h][k], 1, 64);
+        e[h][k] = lane == 0 ? 0.0 : o;
+      }
+    matvec_acc<4>(a.lanemats + lane * 16, cw[0], e[0]);
+    matvec_acc<4>(a.lanemats + lane * 16, cw[1], e[1]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ef[k] = f2{static_cast<float>(e[0][k]), static_cast<float>(e[1][k])};
   }
-  double e[4];
+  if constexpr (ABL & 32) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const double o = __shfl_up(q[i], 1, 64);
-    e[i] = lane == 0 ? 0.0 : o;
+    for (int k = 0; k < 4; ++k) ef[k] = f2{0, 0};
   }
-  matvec_acc<4>(a.lanemats + lane * 16, cw, e);
-  float ef[4] = {static_cast<float>(e[0]), static_cast<float>(e[1]), static_cast<float>(e[2]),
-                 static_cast<float>(e[3])};
-  if (first && t < 128) put_f(P, t - 128, ci[8 + t]);  // f[-128 .. -1] from the previous call
+
+  // ---- pass 2: the reference's f32 recurrence from the entering state ----
+  // Pairs j < -124 (warm-up not needed by the FIR) and, in block 0, j < 0 (the
+  // previous call's f values are written below) go to a dummy slot.
+  const int jlo = first ? 0 : -124;
+  const int j0 = kBackC * t - kBackW;
+  if (!last) {
 #pragma unroll
-  for (int i = 0; i < kBackC; ++i) {
-    const int li = kBackC * t + i;
-    if (li < cnt) put_f(P, li, lp4_step(bq, ef, xs[i]));
+    for (int i = 0; i < kBackC; ++i) {
+      const int j = j0 + i;
+      const f2 f = (ABL & 32) ? xs[i] * ef[0] : bq.lp4(ef, xs[i]);
+      P[j >= jlo ? ppos(j + 124) : kPDummy] = f;
+    }
+  } else {
+    // last block: also capture the IIR state after sample n_dec - 1
+    const int jl = static_cast<int>(a.n_dec - 1 - a0);  // local index of the last sample
+    float cap[4] = {0, 0, 0, 0};
+    bool have = false;
+#pragma unroll
+    for (int i = 0; i < kBackC; ++i) {
+      const int j = j0 + i;
+      const f2 f = (ABL & 32) ? xs[i] * ef[0] : bq.lp4(ef, xs[i]);
+      P[j >= jlo ? ppos(j + 124) : kPDummy] = f;
+      if (j == jl && jl < kHalf) {  // half A owns j < 2048 (its tail past 2048 is B's)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cap[k] = ef[k].x;
+        have = true;
+      }
+      if (j + kHalf == jl && j >= 0) {  // half B owns j >= 2048 (its warm-up is A's)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cap[k] = ef[k].y;
+        have = true;
+      }
+    }
+    if (have) {
+      float* co = a.carry_out + ch * kWbfmCarry;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) co[k] = cap[k];
+    }
   }
-  const bool last = a_end == a.n_dec;
-  if (last && kBackC * t <= cnt - 1 && cnt - 1 < kBackC * t + kBackC) {
-    float* co = a.carry_out + ch * kWbfmCarry;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) co[i] = ef[i];
+  // Pairs j in [-124, 0): .y = f[j + 2048] came from half B's warm-up; the exact
+  // value is half A's (converged) f at 1924 .. 2047. Block 0: .x = f[-124 .. -1]
+  // of the previous call.
+  __syncthreads();
+  if (t < 124) {
+    P[ppos(t)].y = P[ppos(t + kHalf)].x;
+    if (first) P[ppos(t)].x = ci[8 + 4 + t];
   }
   __syncthreads();
 
-  // ---- audio FIR (fir.rs:57-66, quirk-mapped taps) over [a0, a_end) ----
-  // Lane t owns outputs a0 + 8t + i and a0 + 2048 + 8t + i (i < 8) as float2
-  // pairs: one ds_read_b64 fetches (f[l], f[l+2048]), one v_pk_fma_f32 applies a
-  // tap to both. Taps: one s_load_dwordx16 per block of 16.
+  // ---- audio FIR (fir.rs:57-66, quirk-mapped taps) ----
+  // Lane t owns outputs j = 8t + i and j + 2048 (i < 8) as float2 pairs. Output
+  // j, tap k = 16 kb + kk reads f[j - k]: window index m = i + 15 - kk of the
+  // 23 pairs starting at e = 8t - 16kb - 15 + 124 = 8(t - 2kb) + 109; with
+  // ppos, slot = 9(t - 2kb) + 109 + m + ((109 + m) >> 3): a per-lane base plus
+  // compile-time offsets.
   {
     constexpr int R = 8, KA = 128;
-    const int o0 = static_cast<int>(a0 - js) + R * t;  // local index of the first output
     f2 acc[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) acc[i] = f2{0.0f, 0.0f};
+    if constexpr (ABL & 16) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) acc[i] = P[ppos(8 * t + i + 124)];
+    } else {
 #pragma unroll 1
-    for (int kb = 0; kb < KA / 16; ++kb) {
-      // output i, tap k = 16 kb + kk uses f[o0 + i - k]: window index m = i + 15 - kk
-      const int wbase = o0 - 16 * kb - 15;
-      f2 w[R + 15];
+      for (int kb = 0; kb < KA / 16; ++kb) {
+        const f2* __restrict__ Pl = P + 9 * (t - 2 * kb) + 109;
+        f2 w[R + 15];
 #pragma unroll
-      for (int m = 0; m < R + 15; ++m) w[m] = P[ppos(wbase + m)];
+        for (int m = 0; m < R + 15; ++m) w[m] = Pl[m + ((109 + m) >> 3)];
 #pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const f2 tap = splat2(C.a[16 * kb + kk]);
+        for (int kk = 0; kk < 16; ++kk) {
+          const f2 tap = splat2(C.a[16 * kb + kk]);
 #pragma unroll
-        for (int i = 0; i < R; ++i) acc[i] = fma2(tap, w[i + 15 - kk], acc[i]);
+          for (int i = 0; i < R; ++i) acc[i] = fma2(tap, w[i + 15 - kk], acc[i]);
+        }
       }
     }
-    float* __restrict__ y = a.y + ch * a.y_stride;
+    float* __restrict__ y = a.y + ch * a.y_stride + a0;
+    const int nv = static_cast<int>(a_end - a0);
+    if (nv == kBackA) {
+      float4* ya = reinterpret_cast<float4*>(y + R * t);
+      float4* yb = reinterpret_cast<float4*>(y + kHalf + R * t);
+      if ((reinterpret_cast<uintptr_t>(y) & 15) == 0) {
+        ya[0] = float4{acc[0].x, acc[1].x, acc[2].x, acc[3].x};
+        ya[1] = float4{acc[4].x, acc[5].x, acc[6].x, acc[7].x};
+        yb[0] = float4{acc[0].y, acc[1].y, acc[2].y, acc[3].y};
+        yb[1] = float4{acc[4].y, acc[5].y, acc[6].y, acc[7].y};
+      } else {
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const long long j = a0 + R * t + i;
-      if (j < a_end) y[j] = acc[i].x;
-      if (j + kHalf < a_end) y[j + kHalf] = acc[i].y;
+        for (int i = 0; i < R; ++i) {
+          y[R * t + i] = acc[i].x;
+          y[kHalf + R * t + i] = acc[i].y;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int j = R * t + i;
+        if (j < nv) y[j] = acc[i].x;
+        if (j + kHalf < nv) y[j + kHalf] = acc[i].y;
+      }
     }
   }
-  if (last && t < 128) a.carry_out[ch * kWbfmCarry + 8 + t] = get_f(P, static_cast<int>(a.n_dec - 128 + t - js));
+  if (last && t < 128) {  // last 128 f values (fhist of the next call)
+    const int j = static_cast<int>(a.n_dec - 128 + t - a0);
+    float f;
+    if (j >= 0) f = j < kHalf ? P[ppos(j + 124)].x : P[ppos(j - kHalf + 124)].y;
+    else f = j >= -124 ? P[ppos(j + 124)].x : ci[8 + 128 + j];  // reaches into the carried history
+    a.carry_out[ch * kWbfmCarry + 8 + t] = f;
+  }
 }
 
 }  // namespace
 
-int wbfm_front_grid() {
+namespace {
+
+constexpr int kFrontR = 2;
+
+// Wave ranges for the wave-independent front: as many resident waves as LDS and
+// registers allow, rounded down to a multiple of 4 per CU (one per SIMD each, so
+// no SIMD carries more waves than another), one round; each wave owns N tiles =
+// N*TW - 1 phi outputs.
+struct Front2Plan {
+  int grid, wpc;
+  long long L;
+};
+template <int R>
+Front2Plan front2_plan(long long n_dec, int nch, int ncu) {
+  using G = Fw<R>;
+  int per_cu = std::min<int>((160 * 1024) / static_cast<int>(G::LDS_F2 * sizeof(f2)), R <= 2 ? 12 : 8);
+  if (const char* e = std::getenv("ORION_WBFM_WPCU")) per_cu = std::atoi(e);  // experiments
+  per_cu = std::max(4, per_cu & ~3);
+  const long long slots = static_cast<long long>(per_cu) * ncu;
+  const long long tiles = static_cast<long long>(nch) * ((n_dec + G::TW) / G::TW);
+  long long N = std::max<long long>(1, (tiles + slots - 1) / slots);
+  if (const char* e = std::getenv("ORION_WBFM_TILES")) N = std::max(1, std::atoi(e));  // experiments
+  Front2Plan p;
+  p.L = N * G::TW - 1;
+  p.wpc = static_cast<int>((n_dec + p.L - 1) / p.L);
+  p.grid = p.wpc * nch;
+  return p;
+}
+
+template <int R>
+void launch_front2(bool a16, long long n_dec, int nch, int ncu, const WbfmArgs& a,
+                   const WbfmFrontConst& f, hipStream_t s) {
+  const Front2Plan fp = front2_plan<R>(n_dec, nch, ncu);
+  if (a.n < 2LL * Fw<R>::NEW) {  // small input: per-lane clamped loads
+    if (a16) k_wbfm_front2<R, true, 0, true><<<fp.grid, 64, 0, s>>>(a, f, fp.L, fp.wpc);
+    else k_wbfm_front2<R, false, 0, true><<<fp.grid, 64, 0, s>>>(a, f, fp.L, fp.wpc);
+  } else {
+    if (a16) k_wbfm_front2<R, true, 0><<<fp.grid, 64, 0, s>>>(a, f, fp.L, fp.wpc);
+    else k_wbfm_front2<R, false, 0><<<fp.grid, 64, 0, s>>>(a, f, fp.L, fp.wpc);
+  }
+}
+
+template <int ABL>
+void launch_abl(const Front2Plan& fp, dim3 gb, const WbfmArgs& a, const WbfmFrontConst& f,
+                const WbfmBackConst& b, hipStream_t s) {
+  k_wbfm_front2<kFrontR, true, ABL & ~(16 | 32 | 64)><<<fp.grid, 64, 0, s>>>(a, f, fp.L, fp.wpc);
+  if constexpr (!(ABL & 64)) k_wbfm_back<ABL & 48><<<gb, NT, 0, s>>>(a, b);
+}
+
+void launch_wbfm_ablation(int abl, bool a16, const Front2Plan& fp, dim3 gb, const WbfmArgs& a,
+                          const WbfmFrontConst& f, const WbfmBackConst& b, hipStream_t s) {
+  if (!a16) throw HipError("ablation runs need 16-B aligned input");
+  switch (abl) {
+    case 1: launch_abl<1>(fp, gb, a, f, b, s); break;
+    case 2: launch_abl<2>(fp, gb, a, f, b, s); break;
+    case 4: launch_abl<4>(fp, gb, a, f, b, s); break;
+    case 8: launch_abl<8>(fp, gb, a, f, b, s); break;
+    case 3: launch_abl<3>(fp, gb, a, f, b, s); break;
+    case 14: launch_abl<14>(fp, gb, a, f, b, s); break;
+    case 15: launch_abl<15>(fp, gb, a, f, b, s); break;
+    case 16: launch_abl<16>(fp, gb, a, f, b, s); break;
+    case 32: launch_abl<32>(fp, gb, a, f, b, s); break;
+    case 48: launch_abl<48>(fp, gb, a, f, b, s); break;
+    case 128: launch_abl<128>(fp, gb, a, f, b, s); break;
+    case 143: launch_abl<143>(fp, gb, a, f, b, s); break;
+    case 142: launch_abl<142>(fp, gb, a, f, b, s); break;
+    case 128 | 1: launch_abl<128 | 1>(fp, gb, a, f, b, s); break;
+    case 512 | 1: launch_abl<512 | 1>(fp, gb, a, f, b, s); break;
+    case 512: launch_abl<512>(fp, gb, a, f, b, s); break;
+    case 14 | 256: launch_abl<14 | 256>(fp, gb, a, f, b, s); break;
+    case 14 | 512: launch_abl<14 | 512>(fp, gb, a, f, b, s); break;
+    case 14 | 1024: launch_abl<14 | 1024>(fp, gb, a, f, b, s); break;
+    case 14 | 256 | 512 | 1024: launch_abl<14 | 256 | 512 | 1024>(fp, gb, a, f, b, s); break;
+    case 15 | 256 | 512 | 1024: launch_abl<15 | 256 | 512 | 1024>(fp, gb, a, f, b, s); break;
+    default: throw HipError("unknown ORION_WBFM_ABL value " + std::to_string(abl));
+  }
+}
+
+int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
+}  // namespace
+
+int device_cus() {
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) ncu = p.multiProcessorCount;
   }
-  return ((4 * ncu) + 7) / 8 * 8;  // 4 resident workgroups per CU, a multiple of 8 (XCDs)
+  return ncu;
 }
 
 void launch_wbfm(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmBackConst& b, int nch,
                  hipStream_t s) {
   if (a.n_dec <= 0 || nch <= 0) return;
-  static const int G = wbfm_front_grid();
+  static const int ncu = device_cus();
+  static const int abl = env_int("ORION_WBFM_ABL", 0);      // timing ablations only
+  static const int variant = env_int("ORION_WBFM_FRONT", 2);  // 1: persistent barrier form
   const bool a16 = (reinterpret_cast<uintptr_t>(a.x) % 16 == 0) && (a.x_stride % 2 == 0);
-  const int tiles = div_up(a.n_dec, kWbfmPhi);
-  const long long total = static_cast<long long>(tiles) * nch;
-  int grid = G;
-  if (total < grid) grid = static_cast<int>((total + 7) / 8 * 8);
-  if (a16) k_wbfm_front<true><<<grid, NT, 0, s>>>(a, f, tiles, nch);
-  else k_wbfm_front<false><<<grid, NT, 0, s>>>(a, f, tiles, nch);
   const dim3 gb(div_up(a.n_dec, kBackA), nch);
-  k_wbfm_back<<<gb, NT, 0, s>>>(a, b);
+  static const int rsel = env_int("ORION_WBFM_R", kFrontR);  // experiments: 2, 4, 6
+  const Front2Plan fp = front2_plan<kFrontR>(a.n_dec, nch, ncu);
+  if (abl != 0) {
+    launch_wbfm_ablation(abl, a16, fp, gb, a, f, b, s);
+  } else if (variant == 1) {
+    const int G = ((4 * ncu) + 7) / 8 * 8;  // 4 resident workgroups per CU, a multiple of 8 (XCDs)
+    const int tiles = div_up(a.n_dec, kWbfmPhi);
+    const long long total = static_cast<long long>(tiles) * nch;
+    const int grid = total < G ? static_cast<int>((total + 7) / 8 * 8) : G;
+    if (a16) k_wbfm_front<true, 0><<<grid, NT, 0, s>>>(a, f, tiles, nch);
+    else k_wbfm_front<false, 0><<<grid, NT, 0, s>>>(a, f, tiles, nch);
+    k_wbfm_back<0><<<gb, NT, 0, s>>>(a, b);
+  } else {
+    if (rsel == 2) launch_front2<2>(a16, a.n_dec, nch, ncu, a, f, s);
+    else if (rsel == 4) launch_front2<4>(a16, a.n_dec, nch, ncu, a, f, s);
+    else launch_front2<6>(a16, a.n_dec, nch, ncu, a, f, s);
+    k_wbfm_back<0><<<gb, NT, 0, s>>>(a, b);
+  }
   ORION_LAUNCH_CHECK();
 }
 

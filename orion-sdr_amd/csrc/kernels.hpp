@@ -61,8 +61,9 @@ constexpr int kWbfmPhi = kWbfmT - 1;                 // discriminator outputs pe
 constexpr int kWbfmNS = kWbfmM * (kWbfmT + kWbfmQ);  // staged input samples per front workgroup
 constexpr int kWbfmHist = kWbfmM * kWbfmQ;           // raw input history (128)
 constexpr int kBackA = 4096;                         // audio outputs per back workgroup
-constexpr int kBackC = 19;                           // IIR samples per lane
-constexpr int kBackSpan = 256 * kBackC;              // 4864 = kBackA + 768 warm-up
+constexpr int kBackC = 10;                           // IIR samples per lane and half
+constexpr int kBackW = 510;                          // zero-state warm-up per half (51 chunks)
+constexpr int kBackSpan = 256 * kBackC;              // 2560 = kBackA / 2 + warm-up (+2)
 constexpr int kWbfmCarry = 8 + 128;                  // iir[4], prev[2], pad[2], fhist[128]
 struct WbfmFrontConst {
   float g[128];  // decimator taps g[8q+c] phase-major at [c*16+q]; quirk-mapped
@@ -72,8 +73,8 @@ struct WbfmFrontConst {
 struct WbfmBackConst {
   float a[128];               // audio taps, quirk-mapped, zero padded
   float b0, b1, b2, a1, a2;   // LpCascade biquad (iir.rs:49-71)
-  double pw[6 * 16];          // (A^19)^(2^s), s = 0..5
-  double mw[16];              // A^(19*64): one wave's span
+  double pw[6 * 16];          // (A^C)^(2^s), s = 0..5 (C = kBackC)
+  double mw[16];              // A^(64 C): one wave's span
 };
 struct WbfmArgs {
   const f2* x;  long long x_stride;  long long n;
@@ -84,7 +85,7 @@ struct WbfmArgs {
   const f2* tab;                                    // [nch][kWbfmNS] e^{j theta p}
   const float* carry_in; float* carry_out;          // [nch][kWbfmCarry]
   const f2* hist_in; f2* hist_out;                  // [nch][kWbfmHist]
-  const double* lanemats;                           // A^(19 L), L = 0..63 (16 doubles each)
+  const double* lanemats;                           // A^(C L), L = 0..63 (16 doubles each)
 };
 void launch_wbfm(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmBackConst& b, int nch,
                  hipStream_t s);

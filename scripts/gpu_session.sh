@@ -32,6 +32,10 @@ for s in ${STEPS:-tests smoke bench prof}; do
              step pmc$i 600 rocprofv3 --pmc $set -d "$OUT/pmc$i" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ${BARGS:-} || exit $?
            done ;;
     list)  step list 120 rocprofv3 -L || exit $? ;;
+    abl)   for v in ${ABLS:-0 1 2 4 8 3 14 15 16 32 48}; do  # timing ablations (k_wbfm.hip ABL)
+             ORION_WBFM_ABL=$v step abl$v 300 rocprofv3 --kernel-trace --stats -d "$OUT/abl$v" -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu ${BARGS:-} || exit $?
+             python3 scripts/prof_summary.py "$OUT/abl$v" | sed "s/^/ABL=$v /" | grep avg; rm -rf "$OUT/abl$v"
+           done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
