@@ -98,7 +98,8 @@ int orion_cw_envelope_demod_set_gain(orion_block* b, float g);
 /* The WBFM chain composed per docs/demodulate.md:128-133 (no single reference
  * type): Rotator(-f_off, fs) -> FirDecimator(fs, m, dec_cutoff, dec_trans) ->
  * FmQuadratureDemod(fs/m, dev_hz, audio_bw) -> FirLowpass(fs/m, audio_pass,
- * audio_trans). cf32 -> f32, fused into one gfx950 kernel (m must be 8). */
+ * audio_trans). cf32 -> f32 in two gfx950 kernels per call (m must be 8):
+ * front = NCO + polyphase decimation + discriminator, back = LpCascade + audio FIR. */
 typedef struct {
   float fs, f_off, dec_cutoff, dec_trans, dev_hz, audio_bw, audio_pass, audio_trans;
   size_t m;

@@ -144,9 +144,8 @@ class DecimBlock final : public Block {
                        hist_len_, static_cast<f2*>(out), static_cast<long long>(out_cap),
                        static_cast<long long>(n_write), nch_, static_cast<int>(m_), K_, fast_,
                        g_dev_.as<float>(), s);
-    for (int ch = 0; ch < nch_; ++ch)
-      launch_hist_update_c(x + ch * n, static_cast<long long>(n), hist_[cur_].as<f2>() + ch * hist_len_,
-                           hist_[cur_ ^ 1].as<f2>() + ch * hist_len_, hist_len_, s);
+    launch_hist_update_c(x, static_cast<long long>(n), hist_[cur_].as<f2>(), hist_[cur_ ^ 1].as<f2>(),
+                         hist_len_, s, nch_, static_cast<long long>(n));
     cur_ ^= 1;
     return {n, n_write};  // all input consumed, decim.rs:72-75
   }
@@ -340,9 +339,8 @@ class WbfmBlock final : public Block {
     const int nxt = cur_ ^ 1;
     if (n_dec == 0) {  // decimator consumed input, demod saw nothing (core.rs chain semantics)
       const f2* x = static_cast<const f2*>(in);
-      for (int ch = 0; ch < nch_; ++ch)
-        launch_hist_update_c(x + ch * n, static_cast<long long>(n), hist_[cur_].as<f2>() + ch * kWbfmHist,
-                             hist_[nxt].as<f2>() + ch * kWbfmHist, kWbfmHist, s);
+      launch_hist_update_c(x, static_cast<long long>(n), hist_[cur_].as<f2>(), hist_[nxt].as<f2>(),
+                           kWbfmHist, s, nch_, static_cast<long long>(n));
       ORION_HIP(hipMemcpyAsync(carry_[nxt].as<void>(), carry_[cur_].as<void>(), carry_[cur_].size(),
                                hipMemcpyDeviceToDevice, s));
     } else {

@@ -215,8 +215,14 @@ __global__ __launch_bounds__(NT) void k_fir_iq_generic(const f2* __restrict__ x,
 }
 
 template <class V>
-__global__ void k_hist_update(const V* __restrict__ x, long long n, const V* __restrict__ old_h,
-                              V* __restrict__ new_h, int hist_len) {
+__global__ void k_hist_update(const V* __restrict__ x, long long n, long long x_stride,
+                              const V* __restrict__ old_h, V* __restrict__ new_h, int hist_len) {
+  // one workgroup per channel (blockIdx.x): the last hist_len samples of the
+  // stream that is this call's input appended to the previous history
+  const int ch = blockIdx.x;
+  x += ch * x_stride;
+  old_h += static_cast<long long>(ch) * hist_len;
+  new_h += static_cast<long long>(ch) * hist_len;
   for (int i = threadIdx.x; i < hist_len; i += blockDim.x) {
     const long long P = n - hist_len + i;
     new_h[i] = P >= 0 ? x[P] : old_h[hist_len + P];
@@ -305,15 +311,15 @@ void launch_fir_iq(const f2* x, long long n, const f2* hist, int hist_len, f2* y
 }
 
 void launch_hist_update_c(const f2* x, long long n, const f2* old_h, f2* new_h, int hist_len,
-                          hipStream_t s) {
-  if (hist_len <= 0) return;
-  k_hist_update<f2><<<1, NT, 0, s>>>(x, n, old_h, new_h, hist_len);
+                          hipStream_t s, int nch, long long x_stride) {
+  if (hist_len <= 0 || nch <= 0) return;
+  k_hist_update<f2><<<nch, NT, 0, s>>>(x, n, x_stride, old_h, new_h, hist_len);
   ORION_LAUNCH_CHECK();
 }
 void launch_hist_update_r(const float* x, long long n, const float* old_h, float* new_h,
                           int hist_len, hipStream_t s) {
   if (hist_len <= 0) return;
-  k_hist_update<float><<<1, NT, 0, s>>>(x, n, old_h, new_h, hist_len);
+  k_hist_update<float><<<1, NT, 0, s>>>(x, n, n, old_h, new_h, hist_len);
   ORION_LAUNCH_CHECK();
 }
 

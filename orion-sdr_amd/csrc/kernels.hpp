@@ -44,7 +44,7 @@ void launch_fir_iq(const f2* x_dev, long long n, const f2* hist_dev, int hist_le
                    hipStream_t s);
 // Copy the last hist_len samples of [old_hist | x[0..n)] into new_hist.
 void launch_hist_update_c(const f2* x_dev, long long n, const f2* old_dev, f2* new_dev,
-                          int hist_len, hipStream_t s);
+                          int hist_len, hipStream_t s, int nch = 1, long long x_stride = 0);
 void launch_hist_update_r(const float* x_dev, long long n, const float* old_dev, float* new_dev,
                           int hist_len, hipStream_t s);
 

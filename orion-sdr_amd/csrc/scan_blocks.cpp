@@ -9,12 +9,6 @@
 namespace orion {
 namespace {
 
-std::vector<float> to_f32(const std::vector<double>& m) {
-  std::vector<float> r(m.size());
-  for (size_t i = 0; i < m.size(); ++i) r[i] = static_cast<float>(m[i]);
-  return r;
-}
-
 // One recurrence stage: rec/pre/post choice, transition matrices, carried state.
 class ScanStage {
  public:

@@ -24,7 +24,13 @@ for s in ${STEPS:-tests smoke bench prof}; do
            [ $rc -le 1 ] || exit $rc ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) step bench 600 python bench.py --steps ${BSTEPS:-10} --warmup 3 ${BARGS:-} || exit $? ;;
-    prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu ${BARGS:-} || exit $? ;;
+    cfgs)  for c in c3 c4 c5; do  # the other BASELINE configs
+             step bench_$c 600 python bench.py --steps 10 --warmup 3 --no-cpu --config $c || exit $?
+             step prof_$c 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$c" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --config $c || exit $?
+             find "$OUT/prof_$c" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_$c.csv" \;
+           done ;;
+    prof)  step prof 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu ${BARGS:-} || exit $?
+           find "$OUT/prof" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \; ;;
     pmc)   i=0
            IFS=';' read -ra SETS <<< "${PMC_SETS:-$DEFAULT_PMC}"
            for set in "${SETS[@]}"; do
