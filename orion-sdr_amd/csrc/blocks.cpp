@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace orion {
@@ -53,6 +54,7 @@ WorkReport Block::process_host(const void* in, size_t n_in, void* out, size_t ou
                                w.out_written * ob, nch, hipMemcpyDeviceToHost, s));
   }
   ORION_HIP(hipStreamSynchronize(s));
+  check_device_errors();
   return w;
 }
 
@@ -311,6 +313,36 @@ class WbfmBlock final : public Block {
       std::copy(m.begin(), m.end(), lm.begin() + L * 16);
     }
     lanemats_.upload(lm.data(), lm.size() * sizeof(double));
+    // fused chain constants: chunks of kFuC per lane, halves of kFuL/2
+    std::memset(&cu_, 0, sizeof(cu_));
+    for (size_t k = 0; k < a.size(); ++k) cu_.a[k] = a[k];
+    cu_.b0 = bq.b0; cu_.b1 = bq.b1; cu_.b2 = bq.b2; cu_.a1 = bq.a1; cu_.a2 = bq.a2;
+    auto pf = mat_pow(ss.A, 4, kFuC);
+    for (int s = 0; s < 6; ++s) {
+      for (int i = 0; i < 16; ++i) cu_.pw[s * 16 + i] = pf[i];
+      pf = mat_mul(pf, pf, 4);
+    }
+    const auto mh = mat_pow(ss.A, 4, kFuL / 2);
+    for (int i = 0; i < 16; ++i) cu_.mh[i] = mh[i];
+    std::vector<double> lf(64 * 16);
+    for (int L = 0; L < 64; ++L) {
+      const auto m = mat_pow(ss.A, 4, static_cast<uint64_t>(kFuC) * L);
+      std::copy(m.begin(), m.end(), lf.begin() + L * 16);
+    }
+    lanemats_fu_.upload(lf.data(), lf.size() * sizeof(double));
+    // The fused chain hands each range only its predecessor's zero-state IIR
+    // aggregate, exact when A^kFuL (the state carried across one whole range)
+    // is below f32 resolution relative to A^0 = I; the 4th-order Butterworth at
+    // fc/fs2 = 0.0108 (the WBFM defaults) has ||A^1024|| ~ 1e-19. Otherwise the
+    // two-kernel path (510-sample warm-up per 2048) is used; see DESIGN.md.
+    {
+      const auto m = mat_pow(ss.A, 4, kFuL);
+      double fro = 0.0;
+      for (double v : m) fro += v * v;
+      fused_ok_ = std::sqrt(fro) < 1e-12;
+    }
+    err_.resize(sizeof(int));
+    err_.zero();
     std::vector<uint64_t> steps(nch_);
     std::vector<float> tabs;
     tabs.reserve(static_cast<size_t>(nch_) * kWbfmNS * 2);
@@ -362,7 +394,28 @@ class WbfmBlock final : public Block {
       a.hist_in = hist_[cur_].as<f2>();
       a.hist_out = hist_[nxt].as<f2>();
       a.lanemats = lanemats_.as<double>();
-      launch_wbfm(a, cf_, cb_, nch_, s);
+      static const char* path = std::getenv("ORION_WBFM_PATH");  // "split": force the two-kernel path
+      const bool fused = fused_ok_ && !(path && std::strcmp(path, "split") == 0);
+      if (fused) {
+        const long long slots = wbfm_fused_slots(static_cast<long long>(n_dec), nch_);
+        if (static_cast<size_t>(slots) * kFuSlot * 4 > hand_.size()) {
+          hand_.resize(static_cast<size_t>(slots) * kFuSlot * 4);
+          flags_.resize(static_cast<size_t>(slots) * 3 * 4);
+          flags_.zero(s);  // epochs start at 1: a zeroed flag never matches
+        }
+        a.lanemats_fu = lanemats_fu_.as<double>();
+        a.hand = hand_.as<uint32_t>();
+        a.flags = flags_.as<uint32_t>();
+        a.err = err_.as<int>();
+        a.epoch = ++epoch_;
+        if (epoch_ == 0xFFFFFFFFu) {  // never reuse a tag that may sit in a flag
+          flags_.zero(s);
+          epoch_ = 0;
+        }
+        launch_wbfm_fused(a, cf_, cu_, nch_, s);
+      } else {
+        launch_wbfm(a, cf_, cb_, nch_, s);
+      }
     }
     cur_ = nxt;
     k0_ += n;
@@ -380,6 +433,14 @@ class WbfmBlock final : public Block {
     k0_ = 0;
   }
   std::vector<float> taps(int which) const override { return which == 0 ? h_dec_ : h_aud_; }
+  void check_device_errors() override {
+    int e = 0;
+    ORION_HIP(hipMemcpy(&e, err_.as<void>(), sizeof(int), hipMemcpyDeviceToHost));
+    if (e) {
+      err_.zero();
+      throw HipError("WBFM fused chain: a range hand-off wait timed out");
+    }
+  }
 
  private:
   WbfmParams p_;
@@ -387,7 +448,10 @@ class WbfmBlock final : public Block {
   std::vector<float> h_dec_, h_aud_;
   WbfmFrontConst cf_;
   WbfmBackConst cb_;
-  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_;
+  WbfmFusedConst cu_;
+  bool fused_ok_ = false;
+  uint32_t epoch_ = 0;
+  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, lanemats_fu_, hand_, flags_, err_;
   int cur_ = 0;
   uint64_t k0_ = 0;
 };

@@ -61,6 +61,8 @@ class Block {
                                     hipStream_t s) = 0;
   // Host buffers: stage through device memory, synchronous.
   WorkReport process_host(const void* in, size_t n_in, void* out, size_t out_cap);
+  // Errors a kernel could only flag in device memory (read after a sync).
+  virtual void check_device_errors() {}
   virtual void reset() = 0;
   virtual int channels() const { return 1; }
   // Designed coefficients (for tests): which = 0 primary taps, 1 secondary.

@@ -776,6 +776,450 @@ __global__ __launch_bounds__(NT, 4) void k_wbfm_back(const WbfmArgs a, const Wbf
   }
 }
 
+// ---- fused chain -------------------------------------------------------------
+// k_wbfm_fused<N>: the whole chain in one kernel, no phi round trip through HBM.
+// One wave per range of L = 128 N decimated outputs [A, A+L) of a channel
+// (waves of one channel are consecutive blockIdx). Per wave:
+//   1. front (as k_wbfm_front2, tiles aligned at A; input prefetched two tiles
+//      ahead): N tiles -> phi in LDS. phi[A] needs d[A-1], the previous range's
+//      last decimated sample;
+//   2. hand-off 1: publish d[A+L-1], wait for the predecessor's, finish phi[A];
+//   3. LpCascade zero-state pass over the range (two halves of L/2 as one packed
+//      float2 recurrence, f64 Kogge-Stone per half) -> the range's zero-state
+//      aggregate a_w;
+//   4. hand-off 2: publish a_w, wait for a_{w-1}. The state entering the range
+//      is sum_k A^{L(k-1)} a_{w-k} = a_{w-1}: the host only selects this kernel
+//      when ||A^L|| is negligible (f32 cannot see the remainder);
+//   5. the reference's f32 recurrence from the entering states -> the audio
+//      FIR's pair image P[j] = (f[j], f[j+L/2]) (as in k_wbfm_back);
+//   6. hand-off 3: publish f[A+L-128 .. A+L), wait for the predecessor's last
+//      128 -> the FIR history; 7. audio FIR -> y.
+// Each hand-off publishes before it waits and only needs the predecessor's
+// previous stage, so no wait chain is longer than three ranges; waves are
+// dispatched in blockIdx order per XCD, so the predecessor is resident or done.
+// Waits are bounded (the kernel never hangs; a timeout sets *err). Hand-off data
+// use agent-scope relaxed atomics (coherent across the XCDs' L2s), ordered by an
+// s_waitcnt vmcnt(0) before the flag store.
+namespace fu {
+using G = Fw<2>;
+constexpr int PB = kFuTail;  // FIR history pairs (j >= -128)
+
+template <int N>
+struct Geo {
+  static constexpr int L = 128 * N;           // outputs per range
+  static constexpr int NH = L / 2;            // per IIR half
+  static constexpr int CH = NH / 64;          // IIR chunk per lane per half = FIR outputs per lane per half
+  static_assert((CH & (CH - 1)) == 0 && CH >= 8, "chunk a power of two");
+  // FIR pair slots: one pad per CH pairs -> lane stride CH+1 pairs (2(CH+1) dwords:
+  // 2 x odd, so the ds_read_b64 of 32 lanes hit distinct bank pairs)
+  __host__ __device__ static constexpr int pslot(int e) { return e + e / CH; }
+  static constexpr int PSlots = pslot(NH + PB) + 1;
+  static constexpr int UPhiBytes = G::LDS_F2 * 8 + L * 4;   // front image + phi
+  static constexpr int LdsBytes = (PSlots * 8 > UPhiBytes ? PSlots * 8 : UPhiBytes);
+  static constexpr int WavesPerSimd = N <= 8 ? 3 : 2;
+};
+
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// This wave's stores have completed (reached the agent coherence point).
+__device__ __forceinline__ void stores_done() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+__device__ __forceinline__ void publish(uint32_t* flag, uint32_t epoch, int l) {
+  stores_done();
+  if (l == 0) st_agent(flag, epoch);
+}
+__device__ __forceinline__ void wait_for(const uint32_t* flag, uint32_t epoch, int* err) {
+  for (int it = 0; it < (1 << 21); ++it) {
+    if (ld_agent(flag) == epoch) {
+      asm volatile("" ::: "memory");
+      return;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double u2d(uint32_t lo, uint32_t hi) {
+  return __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+}
+}  // namespace fu
+
+// One front tile of the fused kernel (tiles aligned at the range start).
+struct FuTile {
+  const WbfmArgs& a;
+  const WbfmFrontConst& C;
+  f2* U;
+  float* Phi;
+  const f2* xc;
+  const f2* hc;
+  const f2* tabc;
+  int ch, l, s0, s1;
+  f2 corr;
+};
+
+template <bool A16, bool CLAMP>
+__device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, long long jd0, const f2 (&ph)[8][2],
+                                        f2 (&v)[8][2], bool next, const f2* xl, long long nl, f2 Sv, f2& carry,
+                                        f2& dA) {
+  using G = fu::G;
+  constexpr int R = 2;
+  f2* __restrict__ U = T.U;
+  const int l = T.l;
+  if (n > 0) {
+#pragma unroll
+    for (int r2 = 0; r2 < 2; ++r2) {
+      const int e = l + 64 * r2;
+      if (e < 72) {
+        const int c = e / 9, h = e - 9 * c;
+        const f4 w = *reinterpret_cast<const f4*>(U + c * G::LR + G::TW + 2 * h);
+        const f2 y0 = cmul(f2{w.x, w.y}, T.corr), y1 = cmul(f2{w.z, w.w}, T.corr);
+        *reinterpret_cast<f4*>(U + c * G::LR + 2 * h) = f4{y0.x, y0.y, y1.x, y1.y};
+      }
+    }
+    wave_lds_fence();
+  }
+  const bool bnd = porg < 0 || porg + 8LL * (G::TW + Q) > T.a.n;
+#pragma unroll
+  for (int k = 0; k < G::KL; ++k) {
+    U[T.s0 + 16 * k] = cmul_rot_pk(v[k][0], ph[k][0]);
+    U[T.s1 + 16 * k] = cmul_rot_pk(v[k][1], ph[k][1]);
+    if (k % 4 == 3) asm volatile("" ::: "memory");
+  }
+  asm volatile("" ::: "memory");
+  // two-deep prefetch: these registers now load the tile after next
+  if (next) front2_load<R, A16, CLAMP>(xl, nl, porg + 2 * G::NEW, l, v);
+  if (bnd) {
+    wave_lds_fence();
+#pragma unroll 1
+    for (int p = 8 * Q + l; p < 8 * (G::TW + Q); p += 64) {
+      const long long Pp = porg + p;
+      if (!CLAMP || Pp < 0 || Pp >= T.a.n) {
+        const int c = (-p) & 7;
+        U[c * G::LR + (p + c) / 8] = cmul_rot(load_hist(T.xc, T.a.n, T.hc, kWbfmHist, Pp), T.tabc[p]);
+      }
+    }
+  }
+  wave_lds_fence();
+  f2 d[R];
+  front2_decim<R>(U, l, T.C.g, d);
+  {
+    const f2 S = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.x), n)),
+                    __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.y), n))};
+#pragma unroll
+    for (int r = 0; r < R; ++r) d[r] = cmul(d[r], S);
+  }
+  const f2 pv = f2{wave_shr1(d[R - 1].x, carry.x), wave_shr1(d[R - 1].y, carry.y)};
+  T.Phi[G::TW * n + 2 * l] = fm_disc_pk(d[0], pv, T.C.k);  // lane 0 of tile 0: redone after hand-off 1
+  T.Phi[G::TW * n + 2 * l + 1] = fm_disc_pk(d[1], d[0], T.C.k);
+  if (n == 0) dA = d[0];
+  carry = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[R - 1].x), 63)),
+             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[R - 1].y), 63))};
+  const WbfmArgs& a = T.a;
+  if (jd0 <= a.n_dec - 1 && a.n_dec - 1 < jd0 + G::TW) {  // carried state of the next call
+    const int rl = static_cast<int>(a.n_dec - 1 - jd0);
+    float* co = a.carry_out + T.ch * kWbfmCarry;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (R * l + r == rl) {
+        co[4] = d[r].x;
+        co[5] = d[r].y;
+        co[6] = 0.0f;
+        co[7] = 0.0f;
+      }
+#pragma unroll
+    for (int t2 = 0; t2 < kWbfmHist / 64; ++t2) {
+      const int t = l + 64 * t2;
+      a.hist_out[T.ch * kWbfmHist + t] = load_hist(T.xc, a.n, T.hc, kWbfmHist, a.n - kWbfmHist + t);
+    }
+  }
+}
+
+template <int N, bool A16, bool CLAMP>
+__global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(const WbfmArgs a,
+                                                                             const WbfmFrontConst C,
+                                                                             const WbfmFusedConst Bc, int wpc) {
+  using G = fu::G;
+  using Y = fu::Geo<N>;
+  constexpr int L = Y::L, NH = Y::NH, CH = Y::CH;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[Y::LdsBytes];
+  f2* U = reinterpret_cast<f2*>(lds);                        // front image ...
+  float* Phi = reinterpret_cast<float*>(lds + G::LDS_F2 * 8);  // ... and phi, then
+  f2* P = reinterpret_cast<f2*>(lds);                        // the FIR pairs over both
+  const int l = threadIdx.x;
+  const int ch = blockIdx.x / wpc;
+  const int wl = blockIdx.x - ch * wpc;
+  const long long A = static_cast<long long>(wl) * L;
+  const long long B = min(A + L, a.n_dec);
+  const int Lr = static_cast<int>(B - A);  // outputs of this range (1 .. L)
+  const bool first = wl == 0, last = B == a.n_dec;
+  uint32_t* slot = a.hand + static_cast<long long>(blockIdx.x) * kFuSlot;
+  const uint32_t* pslot_ = a.hand + static_cast<long long>(blockIdx.x - 1) * kFuSlot;
+  uint32_t* flag = a.flags + 3LL * blockIdx.x;
+  const uint32_t* pflag = a.flags + 3LL * (blockIdx.x - 1);
+
+  const f2* __restrict__ tabc = a.tab + static_cast<long long>(ch) * kWbfmNS;
+  const bool tiny = a.n < 2;
+  const f2* __restrict__ xc = a.x + ch * a.x_stride;
+  const f2* __restrict__ xl = tiny ? a.hist_in + ch * kWbfmHist : xc;
+  const long long nl = tiny ? kWbfmHist : a.n;
+  const f2* __restrict__ hc = a.hist_in + ch * kWbfmHist;
+  const uint64_t step = a.step[ch];
+  const float* __restrict__ ci = a.carry_in + ch * kWbfmCarry;
+
+  // ==== 1. front ====
+  const f4 tv = *reinterpret_cast<const f4*>(tabc + 8 * Q + 2 * l);
+  const f2 tb0 = f2{tv.x, tv.y}, tb1 = f2{tv.z, tv.w};
+  f2 ph[G::KL][2];
+#pragma unroll
+  for (int k = 0; k < G::KL; ++k) {
+    const f2 ek = tabc[128 * k];
+    ph[k][0] = cmul(tb0, ek);
+    ph[k][1] = cmul(tb1, ek);
+  }
+  const f2 cn = tabc[G::NEW];
+  const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
+  const FuTile T{a, C, U, Phi, xc, hc, tabc, ch, l, c0 * G::LR + (8 * Q + 2 * l + c0) / 8,
+                 c1 * G::LR + (8 * Q + 2 * l + 1 + c1) / 8, f2{cn.x, -cn.y}};
+
+  long long porg = 8LL * (A - Q);  // tile n computes d[A + 128 n + (0..127)]
+  f2 va[G::KL][2], vb[G::KL][2];
+  front2_load<2, A16, CLAMP>(xl, nl, porg, l, va);
+  front2_load<2, A16, CLAMP>(xl, nl, porg + G::NEW, l, vb);
+  {
+    const f4 th = *reinterpret_cast<const f4*>(tabc + 2 * l);
+    const f2 x0 = load_hist(xc, a.n, hc, kWbfmHist, porg + 2 * l);
+    const f2 x1 = load_hist(xc, a.n, hc, kWbfmHist, porg + 2 * l + 1);
+    U[c0 * G::LR + (2 * l + c0) / 8] = cmul_rot(x0, f2{th.x, th.y});
+    U[c1 * G::LR + (2 * l + 1 + c1) / 8] = cmul_rot(x1, f2{th.z, th.w});
+  }
+  const f2 Sv = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1 + static_cast<long long>(l) * G::NEW), step);
+  f2 carry = f2{0.0f, 0.0f};
+  f2 dA = f2{0.0f, 0.0f};  // d[A] (lane 0), waiting for d[A-1]
+#pragma unroll 1
+  for (int n = 0; n < N; n += 2, porg += 2 * G::NEW) {
+    const long long jd0 = A + static_cast<long long>(n) * G::TW;
+    fu_tile<A16, CLAMP>(T, n, porg, jd0, ph, va, n + 2 < N, xl, nl, Sv, carry, dA);
+    fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + G::TW, ph, vb, n + 3 < N, xl, nl, Sv, carry, dA);
+  }
+
+  // ==== 2. hand-off 1: last decimated sample ====
+  if (!last) {
+    if (l == 0) {
+      fu::st_agent(slot + 0, __float_as_uint(carry.x));
+      fu::st_agent(slot + 1, __float_as_uint(carry.y));
+    }
+    fu::publish(flag + 0, a.epoch, l);
+  }
+  f2 dprev;
+  if (first) {
+    dprev = f2{ci[4], ci[5]};
+  } else {
+    fu::wait_for(pflag + 0, a.epoch, a.err);
+    dprev = f2{__uint_as_float(fu::ld_agent(pslot_ + 0)), __uint_as_float(fu::ld_agent(pslot_ + 1))};
+  }
+  if (l == 0) Phi[0] = fm_disc_pk(dA, dprev, C.k);
+  wave_lds_fence();
+
+  // ==== 3. LpCascade zero-state pass, f64 scan per half ====
+  const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
+  f2 xs[CH];
+#pragma unroll
+  for (int i = 0; i < CH; i += 4) {
+    const f4 u = *reinterpret_cast<const f4*>(Phi + CH * l + i);
+    const f4 w = *reinterpret_cast<const f4*>(Phi + NH + CH * l + i);
+    xs[i] = f2{u.x, w.x};
+    xs[i + 1] = f2{u.y, w.y};
+    xs[i + 2] = f2{u.z, w.z};
+    xs[i + 3] = f2{u.w, w.w};
+  }
+  f2 s[4] = {f2{0, 0}, f2{0, 0}, f2{0, 0}, f2{0, 0}};
+#pragma unroll
+  for (int i = 0; i < CH; ++i) (void)bq.lp4(s, xs[i]);
+  double q[2][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    q[0][k] = s[k].x;
+    q[1][k] = s[k].y;
+  }
+#pragma unroll 1
+  for (int st = 0; st < 6; ++st) {
+    const int dd = 1 << st;
+    double o[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[h][k] = __shfl_up(q[h][k], dd, 64);
+    if (l >= dd) {
+      matvec_acc<4>(Bc.pw + st * 16, o[0], q[0]);
+      matvec_acc<4>(Bc.pw + st * 16, o[1], q[1]);
+    }
+  }
+  double aggA[4], agg[4];  // zero-state state after half A; after the whole range
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    aggA[k] = __shfl(q[0][k], 63, 64);
+    agg[k] = __shfl(q[1][k], 63, 64);
+  }
+  matvec_acc<4>(Bc.mh, aggA, agg);
+
+  // ==== 4. hand-off 2: zero-state aggregate -> entering state ====
+  if (!last) {
+    if (l < 8) {
+      const int kk = l >> 1;
+      const double v8 = kk == 0 ? agg[0] : kk == 1 ? agg[1] : kk == 2 ? agg[2] : agg[3];
+      const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v8));
+      fu::st_agent(slot + 2 + l, (l & 1) ? static_cast<uint32_t>(b >> 32) : static_cast<uint32_t>(b));
+    }
+    fu::publish(flag + 1, a.epoch, l);
+  }
+  double sw[4];
+  if (first) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sw[k] = ci[k];
+  } else {
+    fu::wait_for(pflag + 1, a.epoch, a.err);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sw[k] = fu::u2d(fu::ld_agent(pslot_ + 2 + 2 * k), fu::ld_agent(pslot_ + 3 + 2 * k));
+  }
+  // entering states: half A lane l: A^{CH l} sw + exclusive prefix A; half B lane
+  // l: A^{CH l} (A^NH sw + aggA) + exclusive prefix B
+  f2 ef[4];
+  {
+    double sB[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sB[k] = aggA[k];
+    matvec_acc<4>(Bc.mh, sw, sB);
+    double e[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double o = __shfl_up(q[h][k], 1, 64);
+        e[h][k] = l == 0 ? 0.0 : o;
+      }
+    matvec_acc<4>(a.lanemats_fu + l * 16, sw, e[0]);
+    matvec_acc<4>(a.lanemats_fu + l * 16, sB, e[1]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ef[k] = f2{static_cast<float>(e[0][k]), static_cast<float>(e[1][k])};
+  }
+  wave_lds_fence();  // every lane holds its phi (the pair image overwrites Phi)
+
+  // ==== 5. pass 2 (reference recurrence) -> P[j] = (f[j], f[j+NH]) ====
+  {
+    const int jl = Lr - 1;  // local index of the channel's last sample (last range)
+    float cap[4] = {0, 0, 0, 0};
+    bool have = false;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int j = CH * l + i;
+      const f2 f = bq.lp4(ef, xs[i]);
+      P[Y::pslot(j + fu::PB)] = f;
+      if (last) {
+        if (j == jl) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) cap[k] = ef[k].x;
+          have = true;
+        }
+        if (j + NH == jl) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) cap[k] = ef[k].y;
+          have = true;
+        }
+      }
+    }
+    if (have) {
+      float* co = a.carry_out + ch * kWbfmCarry;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) co[k] = cap[k];
+    }
+  }
+  wave_lds_fence();
+  // pairs j in [-128, 0): .y = f[j + NH] (this range's own f at NH-128 .. NH-1)
+#pragma unroll
+  for (int r2 = 0; r2 < 2; ++r2) {
+    const int t = l + 64 * r2;  // j = t - 128
+    P[Y::pslot(t)].y = P[Y::pslot(t + NH)].x;
+  }
+
+  // ==== 6. hand-off 3: last 128 IIR outputs -> FIR history ====
+  if (!last) {
+#pragma unroll
+    for (int r2 = 0; r2 < 2; ++r2) {
+      const int t = l + 64 * r2;  // f[L - 128 + t] = P[NH - 128 + t].y
+      fu::st_agent(slot + 16 + t, __float_as_uint(P[Y::pslot(NH - 128 + t + fu::PB)].y));
+    }
+    fu::publish(flag + 2, a.epoch, l);
+  }
+  if (first) {
+#pragma unroll
+    for (int r2 = 0; r2 < 2; ++r2) {
+      const int t = l + 64 * r2;
+      P[Y::pslot(t)].x = ci[8 + t];  // f[t - 128] of the previous call
+    }
+  } else {
+    fu::wait_for(pflag + 2, a.epoch, a.err);
+#pragma unroll
+    for (int r2 = 0; r2 < 2; ++r2) {
+      const int t = l + 64 * r2;
+      P[Y::pslot(t)].x = __uint_as_float(fu::ld_agent(pslot_ + 16 + t));
+    }
+  }
+  wave_lds_fence();
+
+  // ==== 7. audio FIR (fir.rs:57-66) over [A, B) ====
+  // lane l: outputs j = CH l + i and j + NH (i < CH); tap k = 16 kb + kk of
+  // output i reads f[j - k]: window m = i + 15 - kk of the CH+15 pairs from
+  // e = CH l - 16 kb - 15 + 128 = CH (l - 16kb/CH) + 113; slot = (CH+1)(l -
+  // 16kb/CH) + 113 + m + (113 + m)/CH: a per-lane base and compile-time offsets.
+  {
+    constexpr int KA = 128;
+    f2 acc[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) acc[i] = f2{0.0f, 0.0f};
+#pragma unroll 1
+    for (int kb = 0; kb < KA / 16; ++kb) {
+      const f2* __restrict__ Pl = P + (CH + 1) * (l - 16 * kb / CH) + 113;
+      f2 w[CH + 15];
+#pragma unroll
+      for (int m = 0; m < CH + 15; ++m) w[m] = Pl[m + (113 + m) / CH];
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const f2 tap = splat2(Bc.a[16 * kb + kk]);
+#pragma unroll
+        for (int i = 0; i < CH; ++i) acc[i] = fma2(tap, w[i + 15 - kk], acc[i]);
+      }
+    }
+    float* __restrict__ y = a.y + ch * a.y_stride + A;
+    if (Lr == L && (reinterpret_cast<uintptr_t>(y) & 15) == 0) {
+      float4* ya = reinterpret_cast<float4*>(y + CH * l);
+      float4* yb = reinterpret_cast<float4*>(y + NH + CH * l);
+#pragma unroll
+      for (int i = 0; i < CH; i += 4) {
+        ya[i / 4] = float4{acc[i].x, acc[i + 1].x, acc[i + 2].x, acc[i + 3].x};
+        yb[i / 4] = float4{acc[i].y, acc[i + 1].y, acc[i + 2].y, acc[i + 3].y};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int j = CH * l + i;
+        if (j < Lr) y[j] = acc[i].x;
+        if (j + NH < Lr) y[j + NH] = acc[i].y;
+      }
+    }
+  }
+  if (last) {  // the next call's FIR history: f[n_dec - 128 .. n_dec)
+#pragma unroll
+    for (int r2 = 0; r2 < 2; ++r2) {
+      const int t = l + 64 * r2;
+      const int j = Lr - 128 + t;  // >= -128
+      const float f = j < NH ? P[Y::pslot(j + fu::PB)].x : P[Y::pslot(j - NH + fu::PB)].y;
+      a.carry_out[ch * kWbfmCarry + 8 + t] = f;
+    }
+  }
+}
+
 }  // namespace
 
 namespace {
@@ -855,6 +1299,30 @@ void launch_wbfm_ablation(int abl, bool a16, const Front2Plan& fp, dim3 gb, cons
     default: throw HipError("unknown ORION_WBFM_ABL value " + std::to_string(abl));
   }
 }
+
+}  // namespace
+
+long long wbfm_fused_slots(long long n_dec, int nch) {
+  return static_cast<long long>(nch) * ((n_dec + kFuL - 1) / kFuL) + 1;
+}
+
+void launch_wbfm_fused(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
+                       hipStream_t s) {
+  if (a.n_dec <= 0 || nch <= 0) return;
+  const bool a16 = (reinterpret_cast<uintptr_t>(a.x) % 16 == 0) && (a.x_stride % 2 == 0);
+  const int wpc = static_cast<int>((a.n_dec + kFuL - 1) / kFuL);
+  const int grid = wpc * nch;
+  if (a.n < 2LL * Fw<2>::NEW) {
+    if (a16) k_wbfm_fused<kFuN, true, true><<<grid, 64, 0, s>>>(a, f, b, wpc);
+    else k_wbfm_fused<kFuN, false, true><<<grid, 64, 0, s>>>(a, f, b, wpc);
+  } else {
+    if (a16) k_wbfm_fused<kFuN, true, false><<<grid, 64, 0, s>>>(a, f, b, wpc);
+    else k_wbfm_fused<kFuN, false, false><<<grid, 64, 0, s>>>(a, f, b, wpc);
+  }
+  ORION_LAUNCH_CHECK();
+}
+
+namespace {
 
 int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);

@@ -76,6 +76,20 @@ struct WbfmBackConst {
   double pw[6 * 16];          // (A^C)^(2^s), s = 0..5 (C = kBackC)
   double mw[16];              // A^(64 C): one wave's span
 };
+// Fused single-kernel chain (k_wbfm_fused): one wave per range of kFuL outputs.
+constexpr int kFuN = 16;                             // front tiles (128 outputs) per range
+constexpr int kFuL = kFuN * 128;                     // 2048 outputs per wave range
+constexpr int kFuC = kFuL / 128;                     // IIR samples per lane and half (16)
+constexpr int kFuTail = 128;                         // IIR outputs handed to the next range
+constexpr int kFuSlot = 144;                         // u32 words per hand-off slot
+// slot layout (u32 words): [0,2) last decimated sample, [2,10) zero-state IIR
+// aggregate (4 f64), [16,144) last 128 IIR outputs. Flags: 3 u32 per slot.
+struct WbfmFusedConst {
+  float a[128];               // audio taps, quirk-mapped, zero padded
+  float b0, b1, b2, a1, a2;   // LpCascade biquad (iir.rs:49-71)
+  double pw[6 * 16];          // (A^kFuC)^(2^s)
+  double mh[16];              // A^(kFuL/2): one half range
+};
 struct WbfmArgs {
   const f2* x;  long long x_stride;  long long n;
   float* phi;   long long phi_stride;               // workspace [nch][>= n_dec]
@@ -86,8 +100,19 @@ struct WbfmArgs {
   const float* carry_in; float* carry_out;          // [nch][kWbfmCarry]
   const f2* hist_in; f2* hist_out;                  // [nch][kWbfmHist]
   const double* lanemats;                           // A^(C L), L = 0..63 (16 doubles each)
+  // fused chain only
+  const double* lanemats_fu;                        // A^(kFuC L), L = 0..63
+  uint32_t* hand;                                   // [slots][kFuSlot] hand-off data
+  uint32_t* flags;                                  // [slots][3] epoch of the last publish
+  int* err;                                         // set if a hand-off wait timed out
+  uint32_t epoch;                                   // this launch's tag (never 0)
 };
 void launch_wbfm(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmBackConst& b, int nch,
                  hipStream_t s);
+// Fused chain: requires ||A^kFuL|| negligible (the block checks it); returns the
+// number of hand-off slots it needs for (n_dec, nch).
+long long wbfm_fused_slots(long long n_dec, int nch);
+void launch_wbfm_fused(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
+                       hipStream_t s);
 
 }  // namespace orion
