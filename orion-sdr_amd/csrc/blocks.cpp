@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -408,11 +409,31 @@ class WbfmBlock final : public Block {
         a.flags = flags_.as<uint32_t>();
         a.err = err_.as<int>();
         a.epoch = ++epoch_;
+        static const int fu_abl = [] {
+          const char* e = std::getenv("ORION_WBFM_FUABL");  // timing ablations only
+          return e ? std::atoi(e) : 0;
+        }();
+        a.fu_abl = fu_abl;
+        static const char* trace_path = std::getenv("ORION_WBFM_TRACE");  // debug: phase timestamps
+        if (trace_path) {
+          trace_.resize(static_cast<size_t>(slots) * kFuTracePoints * 8);
+          trace_.zero(s);
+          a.trace = trace_.as<long long>();
+        }
         if (epoch_ == 0xFFFFFFFFu) {  // never reuse a tag that may sit in a flag
           flags_.zero(s);
           epoch_ = 0;
         }
         launch_wbfm_fused(a, cf_, cu_, nch_, s);
+        if (trace_path) {  // debug: dump this launch's timestamps (overwrites: last launch wins)
+          std::vector<long long> h(static_cast<size_t>(slots) * kFuTracePoints);
+          ORION_HIP(hipMemcpyAsync(h.data(), trace_.as<void>(), h.size() * 8, hipMemcpyDeviceToHost, s));
+          ORION_HIP(hipStreamSynchronize(s));
+          if (FILE* f = std::fopen(trace_path, "wb")) {
+            std::fwrite(h.data(), 8, h.size(), f);
+            std::fclose(f);
+          }
+        }
       } else {
         launch_wbfm(a, cf_, cb_, nch_, s);
       }
@@ -451,7 +472,7 @@ class WbfmBlock final : public Block {
   WbfmFusedConst cu_;
   bool fused_ok_ = false;
   uint32_t epoch_ = 0;
-  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, lanemats_fu_, hand_, flags_, err_;
+  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, lanemats_fu_, hand_, flags_, err_, trace_;
   int cur_ = 0;
   uint64_t k0_ = 0;
 };

@@ -323,6 +323,33 @@ __device__ __forceinline__ void front2_decim(const f2* __restrict__ U, int l, co
   }
 }
 
+// Same FIR with the taps in LDS (phase-major, 16 floats per phase = 4 broadcast
+// ds_read_b128): every operand wait is then an LDS wait the compiler can count
+// (scalar tap loads share lgkmcnt and force a full drain per phase), so with the
+// 8 phases unrolled the next phase's reads overlap this phase's FMAs.
+template <int R>
+__device__ __forceinline__ void front2_decim_lds(const f2* __restrict__ U, int l, const float* __restrict__ Gt,
+                                                 f2 (&d)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) d[r] = f2{0.0f, 0.0f};
+#pragma unroll
+  for (int c = 0; c < M; ++c) {
+    f4 w[Fw<R>::WIN];
+    front2_window<R>(U, l, c, w);
+    const f4* tq = reinterpret_cast<const f4*>(Gt + c * Q);
+    float t[Q];
+#pragma unroll
+    for (int i = 0; i < Q / 4; ++i) {
+      const f4 v = tq[i];
+      t[4 * i] = v.x;
+      t[4 * i + 1] = v.y;
+      t[4 * i + 2] = v.z;
+      t[4 * i + 3] = v.w;
+    }
+    front2_phase<R>(w, t, d);
+  }
+}
+
 template <int R, bool A16, int ABL, bool CLAMP = false>
 __global__ __launch_bounds__(64, R <= 2 ? 3 : 2) void k_wbfm_front2(const WbfmArgs a, const WbfmFrontConst C,
                                                     long long L, int wpc) {
@@ -802,6 +829,12 @@ __global__ __launch_bounds__(NT, 4) void k_wbfm_back(const WbfmArgs a, const Wbf
 // s_waitcnt vmcnt(0) before the flag store.
 namespace fu {
 using G = Fw<2>;
+// debug timing: lane 0 records s_memrealtime (100 MHz) at phase boundaries
+__device__ __forceinline__ void trace(const WbfmArgs& a, int r, int point) {
+  if (a.trace && (threadIdx.x & 63) == 0)
+    a.trace[static_cast<long long>(r) * kFuTracePoints + point] =
+        static_cast<long long>(__builtin_amdgcn_s_memrealtime());
+}
 constexpr int PB = kFuTail;  // FIR history pairs (j >= -128)
 
 template <int N>
@@ -846,23 +879,31 @@ __device__ __forceinline__ double u2d(uint32_t lo, uint32_t hi) {
 }
 }  // namespace fu
 
-// One front tile of the fused kernel (tiles aligned at the range start).
+// One front tile (tiles aligned at the range start). The registers v hold this
+// tile's prefetched inputs on entry; on exit they hold the loads issued for the
+// tile two ahead (pf), possibly in the next range, possibly another channel.
 struct FuTile {
   const WbfmArgs& a;
   const WbfmFrontConst& C;
   f2* U;
   float* Phi;
+  const float* Gt;  // decimator taps in LDS (phase-major)
   const f2* xc;
   const f2* hc;
   const f2* tabc;
   int ch, l, s0, s1;
   f2 corr;
+  bool first;  // the channel's first range: d[A-1] is the carried sample
+};
+struct FuPrefetch {  // where the tile two ahead starts
+  const f2* xl;
+  long long nl, porg;
+  bool on;
 };
 
 template <bool A16, bool CLAMP>
 __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, long long jd0, const f2 (&ph)[8][2],
-                                        f2 (&v)[8][2], bool next, const f2* xl, long long nl, f2 Sv, f2& carry,
-                                        f2& dA) {
+                                        f2 (&v)[8][2], const FuPrefetch& pf, f2 Sv, f2& carry, f2& dA) {
   using G = fu::G;
   constexpr int R = 2;
   f2* __restrict__ U = T.U;
@@ -888,14 +929,17 @@ __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, 
     if (k % 4 == 3) asm volatile("" ::: "memory");
   }
   asm volatile("" ::: "memory");
-  // two-deep prefetch: these registers now load the tile after next
-  if (next) front2_load<R, A16, CLAMP>(xl, nl, porg + 2 * G::NEW, l, v);
+  // unconditional: a conditional prefetch makes the compiler's wait counting
+  // assume the other buffer's loads may be absent and drain them (vmcnt(0))
+  front2_load<R, A16, CLAMP>(pf.xl, pf.nl, pf.porg, l, v);
   if (bnd) {
+    // Tile reaching before x[0] or past x[n-1]: rewrite the new samples (and, in
+    // a range's first tile, the halo rows) exactly from the history / zeros.
     wave_lds_fence();
 #pragma unroll 1
-    for (int p = 8 * Q + l; p < 8 * (G::TW + Q); p += 64) {
+    for (int p = (n == 0 ? 0 : 8 * Q) + l; p < 8 * (G::TW + Q); p += 64) {
       const long long Pp = porg + p;
-      if (!CLAMP || Pp < 0 || Pp >= T.a.n) {
+      if (!CLAMP || Pp < 0 || Pp >= T.a.n || p < 8 * Q) {
         const int c = (-p) & 7;
         U[c * G::LR + (p + c) / 8] = cmul_rot(load_hist(T.xc, T.a.n, T.hc, kWbfmHist, Pp), T.tabc[p]);
       }
@@ -904,14 +948,27 @@ __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, 
   wave_lds_fence();
   f2 d[R];
   front2_decim<R>(U, l, T.C.g, d);
-  {
-    const f2 S = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.x), n)),
-                    __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.y), n))};
+  const f2 S = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.x), n)),
+                  __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.y), n))};
 #pragma unroll
-    for (int r = 0; r < R; ++r) d[r] = cmul(d[r], S);
+  for (int r = 0; r < R; ++r) d[r] = cmul(d[r], S);
+  if (n == 0 && !T.first) {
+    // d[A-1], the previous range's last output, from this tile's image (rows
+    // i = 0..15; the range setup staged U[c][0], c >= 1): taps 2l, 2l+1 per
+    // lane, summed over the wave.
+    f2 acc = f2{0.0f, 0.0f};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int k = 2 * l + t, c = k & 7, q = k >> 3;
+      acc = fma2(splat2(T.Gt[c * Q + q]), U[c * G::LR + 15 - q], acc);  // LDS taps: no vmcnt drain
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+      acc += f2{__shfl_xor(acc.x, off, 64), __shfl_xor(acc.y, off, 64)};
+    carry = cmul(acc, S);
   }
   const f2 pv = f2{wave_shr1(d[R - 1].x, carry.x), wave_shr1(d[R - 1].y, carry.y)};
-  T.Phi[G::TW * n + 2 * l] = fm_disc_pk(d[0], pv, T.C.k);  // lane 0 of tile 0: redone after hand-off 1
+  T.Phi[G::TW * n + 2 * l] = fm_disc_pk(d[0], pv, T.C.k);
   T.Phi[G::TW * n + 2 * l + 1] = fm_disc_pk(d[1], d[0], T.C.k);
   if (n == 0) dA = d[0];
   carry = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[R - 1].x), 63)),
@@ -936,39 +993,51 @@ __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, 
   }
 }
 
-template <int N, bool A16, bool CLAMP>
-__global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(const WbfmArgs a,
-                                                                             const WbfmFrontConst C,
-                                                                             const WbfmFusedConst Bc, int wpc) {
-  using G = fu::G;
-  using Y = fu::Geo<N>;
-  constexpr int L = Y::L, NH = Y::NH, CH = Y::CH;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[Y::LdsBytes];
-  f2* U = reinterpret_cast<f2*>(lds);                        // front image ...
-  float* Phi = reinterpret_cast<float*>(lds + G::LDS_F2 * 8);  // ... and phi, then
-  f2* P = reinterpret_cast<f2*>(lds);                        // the FIR pairs over both
-  const int l = threadIdx.x;
-  const int ch = blockIdx.x / wpc;
-  const int wl = blockIdx.x - ch * wpc;
-  const long long A = static_cast<long long>(wl) * L;
-  const long long B = min(A + L, a.n_dec);
-  const int Lr = static_cast<int>(B - A);  // outputs of this range (1 .. L)
-  const bool first = wl == 0, last = B == a.n_dec;
-  uint32_t* slot = a.hand + static_cast<long long>(blockIdx.x) * kFuSlot;
-  const uint32_t* pslot_ = a.hand + static_cast<long long>(blockIdx.x - 1) * kFuSlot;
-  uint32_t* flag = a.flags + 3LL * blockIdx.x;
-  const uint32_t* pflag = a.flags + 3LL * (blockIdx.x - 1);
+// Range geometry shared by the front and the back of one range.
+struct FuRange {
+  int r, ch, wl;
+  long long A, B;
+  int Lr;
+  bool first, last;
+};
+template <int N>
+__device__ __forceinline__ FuRange fu_range(const WbfmArgs& a, int r, int wpc) {
+  FuRange g;
+  g.r = r;
+  g.ch = r / wpc;
+  g.wl = r - g.ch * wpc;
+  g.A = static_cast<long long>(g.wl) * fu::Geo<N>::L;
+  g.B = min(g.A + fu::Geo<N>::L, a.n_dec);
+  g.Lr = static_cast<int>(g.B - g.A);
+  g.first = g.wl == 0;
+  g.last = g.B == a.n_dec;
+  return g;
+}
 
-  const f2* __restrict__ tabc = a.tab + static_cast<long long>(ch) * kWbfmNS;
+// Where range g's first tile starts (its first two tiles are prefetched into va/vb).
+__device__ __forceinline__ FuPrefetch fu_origin(const WbfmArgs& a, const FuRange& g) {
   const bool tiny = a.n < 2;
-  const f2* __restrict__ xc = a.x + ch * a.x_stride;
-  const f2* __restrict__ xl = tiny ? a.hist_in + ch * kWbfmHist : xc;
-  const long long nl = tiny ? kWbfmHist : a.n;
-  const f2* __restrict__ hc = a.hist_in + ch * kWbfmHist;
-  const uint64_t step = a.step[ch];
-  const float* __restrict__ ci = a.carry_in + ch * kWbfmCarry;
+  FuPrefetch p;
+  p.xl = tiny ? a.hist_in + g.ch * kWbfmHist : a.x + g.ch * a.x_stride;
+  p.nl = tiny ? kWbfmHist : a.n;
+  p.porg = 8LL * (g.A - Q);
+  p.on = true;
+  return p;
+}
 
-  // ==== 1. front ====
+// The front of one range: N tiles -> Phi[0 .. L); dA = d[A] (for phi[A]) and
+// dlast = d[A+L-1] (for the next range). On entry va/vb hold the range's first
+// two tiles; on exit, when nx.on, the next range's first two (nx = its origin).
+template <int N, bool A16, bool CLAMP>
+__device__ __forceinline__ void fu_front_range(const WbfmArgs& a, const WbfmFrontConst& C, const FuRange& g,
+                                               f2* U, float* Phi, const float* Gt, f2 (&va)[8][2], f2 (&vb)[8][2],
+                                               const FuPrefetch& nx, f2& dA, f2& dlast) {
+  using G = fu::G;
+  const int l = threadIdx.x & 63;
+  const f2* __restrict__ tabc = a.tab + static_cast<long long>(g.ch) * kWbfmNS;
+  const f2* __restrict__ xc = a.x + g.ch * a.x_stride;
+  const f2* __restrict__ hc = a.hist_in + g.ch * kWbfmHist;
+  const FuPrefetch org = fu_origin(a, g);
   const f4 tv = *reinterpret_cast<const f4*>(tabc + 8 * Q + 2 * l);
   const f2 tb0 = f2{tv.x, tv.y}, tb1 = f2{tv.z, tv.w};
   f2 ph[G::KL][2];
@@ -980,49 +1049,76 @@ __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(con
   }
   const f2 cn = tabc[G::NEW];
   const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
-  const FuTile T{a, C, U, Phi, xc, hc, tabc, ch, l, c0 * G::LR + (8 * Q + 2 * l + c0) / 8,
-                 c1 * G::LR + (8 * Q + 2 * l + 1 + c1) / 8, f2{cn.x, -cn.y}};
-
-  long long porg = 8LL * (A - Q);  // tile n computes d[A + 128 n + (0..127)]
-  f2 va[G::KL][2], vb[G::KL][2];
-  front2_load<2, A16, CLAMP>(xl, nl, porg, l, va);
-  front2_load<2, A16, CLAMP>(xl, nl, porg + G::NEW, l, vb);
-  {
+  const FuTile T{a, C, U, Phi, Gt, xc, hc, tabc, g.ch, l, c0 * G::LR + (8 * Q + 2 * l + c0) / 8,
+                 c1 * G::LR + (8 * Q + 2 * l + 1 + c1) / 8, f2{cn.x, -cn.y}, g.first};
+  long long porg = org.porg;  // tile n computes d[A + 128 n + (0..127)]
+  {  // halo rows of the first tile (p = 2l, 2l+1): clamped here, exact via the boundary fixup
+    const long long P0 = porg + 2 * l;
+    const long long hi = (org.nl & ~1LL) - 2;
+    const long long Pc = P0 < 0 ? 0 : (P0 > hi ? hi : P0);
+    const f2 x0 = org.xl[Pc], x1 = org.xl[Pc + 1];
     const f4 th = *reinterpret_cast<const f4*>(tabc + 2 * l);
-    const f2 x0 = load_hist(xc, a.n, hc, kWbfmHist, porg + 2 * l);
-    const f2 x1 = load_hist(xc, a.n, hc, kWbfmHist, porg + 2 * l + 1);
     U[c0 * G::LR + (2 * l + c0) / 8] = cmul_rot(x0, f2{th.x, th.y});
     U[c1 * G::LR + (2 * l + 1 + c1) / 8] = cmul_rot(x1, f2{th.z, th.w});
   }
-  const f2 Sv = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1 + static_cast<long long>(l) * G::NEW), step);
+  {  // p = -l (row c = l, i = 0), l = 1..7: used only by d[A-1]. Not the first
+     // range, so porg - l >= 0: a plain load (a branchy one would drain the prefetch)
+    const long long Pm = max(porg - (l & 7), 0LL);
+    const f2 xm = xc[Pm];
+    const f2 tc = tabc[l & 7];
+    if (!g.first && l >= 1 && l < 8) U[l * G::LR] = cmul_rot(xm, f2{tc.x, -tc.y});
+  }
+  const f2 Sv = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1 + static_cast<long long>(l) * G::NEW),
+                           a.step[g.ch]);
   f2 carry = f2{0.0f, 0.0f};
-  f2 dA = f2{0.0f, 0.0f};  // d[A] (lane 0), waiting for d[A-1]
+  if (g.first) {  // d[-1]: the last decimated sample of the previous call (fm.rs:29 on reset)
+    const float* ci = a.carry_in + g.ch * kWbfmCarry;
+    carry = f2{ci[4], ci[5]};
+  }
 #pragma unroll 1
   for (int n = 0; n < N; n += 2, porg += 2 * G::NEW) {
-    const long long jd0 = A + static_cast<long long>(n) * G::TW;
-    fu_tile<A16, CLAMP>(T, n, porg, jd0, ph, va, n + 2 < N, xl, nl, Sv, carry, dA);
-    fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + G::TW, ph, vb, n + 3 < N, xl, nl, Sv, carry, dA);
+    const long long jd0 = g.A + static_cast<long long>(n) * G::TW;
+    FuPrefetch p0{org.xl, org.nl, porg + 2 * G::NEW, true}, p1{org.xl, org.nl, porg + 3 * G::NEW, true};
+    // past the range: the next range's first tiles, or (none) a harmless re-read
+    if (n + 2 >= N) p0 = nx.on ? FuPrefetch{nx.xl, nx.nl, nx.porg, true} : FuPrefetch{org.xl, org.nl, porg, true};
+    if (n + 3 >= N)
+      p1 = nx.on ? FuPrefetch{nx.xl, nx.nl, nx.porg + G::NEW, true} : FuPrefetch{org.xl, org.nl, porg, true};
+    fu_tile<A16, CLAMP>(T, n, porg, jd0, ph, va, p0, Sv, carry, dA);
+    fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + G::TW, ph, vb, p1, Sv, carry, dA);
   }
+  dlast = carry;
+}
 
-  // ==== 2. hand-off 1: last decimated sample ====
-  if (!last) {
-    if (l == 0) {
-      fu::st_agent(slot + 0, __float_as_uint(carry.x));
-      fu::st_agent(slot + 1, __float_as_uint(carry.y));
-    }
-    fu::publish(flag + 0, a.epoch, l);
-  }
-  f2 dprev;
-  if (first) {
-    dprev = f2{ci[4], ci[5]};
-  } else {
-    fu::wait_for(pflag + 0, a.epoch, a.err);
-    dprev = f2{__uint_as_float(fu::ld_agent(pslot_ + 0)), __uint_as_float(fu::ld_agent(pslot_ + 1))};
-  }
-  if (l == 0) Phi[0] = fm_disc_pk(dA, dprev, C.k);
-  wave_lds_fence();
+// The back of one range (LpCascade, audio FIR) from Phi[0 .. L), with one
+// hand-off to the next range that depends on nothing but this range's phi:
+//  - the zero-state pass gives every chunk's zero-state entering state and the
+//    range's zero-state end state a_w. The true state entering range w+1 is
+//    a_w + A^L (true state entering w) = a_w, since ||A^L|| is negligible (the
+//    host checks it);
+//  - the last 128 IIR outputs of this range (the next range's FIR history) are
+//    the zero-state recurrence over them: their true values differ by A^{L-128}
+//    times the entering state, also negligible;
+// so both are published right after the zero-state pass, and a range waits only
+// for its predecessor's zero-state pass (no wait chain). P is this wave's
+// pair-image region (may alias Phi: Phi is read into registers first).
+template <int N>
+__device__ __forceinline__ void fu_back_range(const WbfmArgs& a, const WbfmFrontConst& C, const WbfmFusedConst& Bc,
+                                              const FuRange& g, float* Phi, f2* P, int* consumed, int consumed_tag) {
+  using Y = fu::Geo<N>;
+  constexpr int L = Y::L, NH = Y::NH, CH = Y::CH;
+  constexpr int TL = 64 - fu::PB / CH;  // first lane whose half-B chunk lies in the last 128
+  const int l = threadIdx.x & 63;
+  const int ch = g.ch;
+  const long long A = g.A;
+  const int Lr = g.Lr;
+  const bool first = g.first, last = g.last;
+  uint32_t* slot = a.hand + static_cast<long long>(g.r) * kFuSlot;
+  const uint32_t* pslot_ = a.hand + static_cast<long long>(g.r - 1) * kFuSlot;
+  uint32_t* flag = a.flags + 3LL * g.r;
+  const uint32_t* pflag = a.flags + 3LL * (g.r - 1);
+  const float* __restrict__ ci = a.carry_in + ch * kWbfmCarry;
 
-  // ==== 3. LpCascade zero-state pass, f64 scan per half ====
+  // ==== zero-state pass, f64 scan per half ====
   const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
   f2 xs[CH];
 #pragma unroll
@@ -1034,6 +1130,9 @@ __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(con
     xs[i + 2] = f2{u.z, w.z};
     xs[i + 3] = f2{u.w, w.w};
   }
+  wave_lds_fence();
+  if (consumed && l == 0)  // Phi may be refilled by the front wave
+    __hip_atomic_store(consumed, consumed_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   f2 s[4] = {f2{0, 0}, f2{0, 0}, f2{0, 0}, f2{0, 0}};
 #pragma unroll
   for (int i = 0; i < CH; ++i) (void)bq.lp4(s, xs[i]);
@@ -1056,57 +1155,71 @@ __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(con
       matvec_acc<4>(Bc.pw + st * 16, o[1], q[1]);
     }
   }
-  double aggA[4], agg[4];  // zero-state state after half A; after the whole range
+  // zero-state entering states (range-relative): half A lane l: exclusive prefix
+  // A; half B lane l: A^{CH l} aggA + exclusive prefix B
+  double aggA[4], agg[4], ez[2][4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     aggA[k] = __shfl(q[0][k], 63, 64);
     agg[k] = __shfl(q[1][k], 63, 64);
   }
-  matvec_acc<4>(Bc.mh, aggA, agg);
+  matvec_acc<4>(Bc.mh, aggA, agg);  // zero-state end state of the range
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double o = __shfl_up(q[h][k], 1, 64);
+      ez[h][k] = l == 0 ? 0.0 : o;
+    }
+  matvec_acc<4>(a.lanemats_fu + l * 16, aggA, ez[1]);
+  fu::trace(a, g.r, 2);
 
-  // ==== 4. hand-off 2: zero-state aggregate -> entering state ====
+  // ==== hand-off: publish (end state, last 128 outputs), then take the predecessor's ====
   if (!last) {
+    f2 e[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) e[k] = f2{0.0f, static_cast<float>(ez[1][k])};
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const f2 f = bq.lp4(e, xs[i]);  // half B (.y): the range's last CH*64 outputs
+      if (l >= TL) fu::st_agent(slot + 16 + (l - TL) * CH + i, __float_as_uint(f.y));
+    }
     if (l < 8) {
       const int kk = l >> 1;
       const double v8 = kk == 0 ? agg[0] : kk == 1 ? agg[1] : kk == 2 ? agg[2] : agg[3];
       const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v8));
       fu::st_agent(slot + 2 + l, (l & 1) ? static_cast<uint32_t>(b >> 32) : static_cast<uint32_t>(b));
     }
-    fu::publish(flag + 1, a.epoch, l);
+    fu::publish(flag + 0, a.epoch, l);
   }
   double sw[4];
+  float hist[2];  // f[t - 128], t = l, l + 64: this range's FIR history
   if (first) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) sw[k] = ci[k];
+    hist[0] = ci[8 + l];
+    hist[1] = ci[8 + 64 + l];
   } else {
-    fu::wait_for(pflag + 1, a.epoch, a.err);
+    fu::wait_for(pflag + 0, a.epoch, a.err);
 #pragma unroll
     for (int k = 0; k < 4; ++k) sw[k] = fu::u2d(fu::ld_agent(pslot_ + 2 + 2 * k), fu::ld_agent(pslot_ + 3 + 2 * k));
+    hist[0] = __uint_as_float(fu::ld_agent(pslot_ + 16 + l));
+    hist[1] = __uint_as_float(fu::ld_agent(pslot_ + 16 + 64 + l));
   }
-  // entering states: half A lane l: A^{CH l} sw + exclusive prefix A; half B lane
-  // l: A^{CH l} (A^NH sw + aggA) + exclusive prefix B
+  fu::trace(a, g.r, 3);
+  // true entering states: zero-state ones plus the entering state's propagation,
+  // half A: A^{CH l} sw; half B: A^{CH l} A^NH sw
   f2 ef[4];
   {
-    double sB[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) sB[k] = aggA[k];
+    double sB[4] = {0, 0, 0, 0};
     matvec_acc<4>(Bc.mh, sw, sB);
-    double e[2][4];
+    matvec_acc<4>(a.lanemats_fu + l * 16, sw, ez[0]);
+    matvec_acc<4>(a.lanemats_fu + l * 16, sB, ez[1]);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const double o = __shfl_up(q[h][k], 1, 64);
-        e[h][k] = l == 0 ? 0.0 : o;
-      }
-    matvec_acc<4>(a.lanemats_fu + l * 16, sw, e[0]);
-    matvec_acc<4>(a.lanemats_fu + l * 16, sB, e[1]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ef[k] = f2{static_cast<float>(e[0][k]), static_cast<float>(e[1][k])};
+    for (int k = 0; k < 4; ++k) ef[k] = f2{static_cast<float>(ez[0][k]), static_cast<float>(ez[1][k])};
   }
-  wave_lds_fence();  // every lane holds its phi (the pair image overwrites Phi)
 
-  // ==== 5. pass 2 (reference recurrence) -> P[j] = (f[j], f[j+NH]) ====
+  // ==== pass 2 (reference recurrence) -> P[j] = (f[j], f[j+NH]) ====
   {
     const int jl = Lr - 1;  // local index of the channel's last sample (last range)
     float cap[4] = {0, 0, 0, 0};
@@ -1136,39 +1249,16 @@ __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(con
     }
   }
   wave_lds_fence();
-  // pairs j in [-128, 0): .y = f[j + NH] (this range's own f at NH-128 .. NH-1)
+  // pairs j in [-128, 0): .x = the FIR history, .y = f[j + NH] (this range's own)
 #pragma unroll
   for (int r2 = 0; r2 < 2; ++r2) {
     const int t = l + 64 * r2;  // j = t - 128
-    P[Y::pslot(t)].y = P[Y::pslot(t + NH)].x;
-  }
-
-  // ==== 6. hand-off 3: last 128 IIR outputs -> FIR history ====
-  if (!last) {
-#pragma unroll
-    for (int r2 = 0; r2 < 2; ++r2) {
-      const int t = l + 64 * r2;  // f[L - 128 + t] = P[NH - 128 + t].y
-      fu::st_agent(slot + 16 + t, __float_as_uint(P[Y::pslot(NH - 128 + t + fu::PB)].y));
-    }
-    fu::publish(flag + 2, a.epoch, l);
-  }
-  if (first) {
-#pragma unroll
-    for (int r2 = 0; r2 < 2; ++r2) {
-      const int t = l + 64 * r2;
-      P[Y::pslot(t)].x = ci[8 + t];  // f[t - 128] of the previous call
-    }
-  } else {
-    fu::wait_for(pflag + 2, a.epoch, a.err);
-#pragma unroll
-    for (int r2 = 0; r2 < 2; ++r2) {
-      const int t = l + 64 * r2;
-      P[Y::pslot(t)].x = __uint_as_float(fu::ld_agent(pslot_ + 16 + t));
-    }
+    P[Y::pslot(t)] = f2{hist[r2], P[Y::pslot(t + NH)].x};
   }
   wave_lds_fence();
+  fu::trace(a, g.r, 4);
 
-  // ==== 7. audio FIR (fir.rs:57-66) over [A, B) ====
+  // ==== audio FIR (fir.rs:57-66) over [A, B) ====
   // lane l: outputs j = CH l + i and j + NH (i < CH); tap k = 16 kb + kk of
   // output i reads f[j - k]: window m = i + 15 - kk of the CH+15 pairs from
   // e = CH l - 16 kb - 15 + 128 = CH (l - 16kb/CH) + 113; slot = (CH+1)(l -
@@ -1209,6 +1299,7 @@ __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(con
       }
     }
   }
+  fu::trace(a, g.r, 5);
   if (last) {  // the next call's FIR history: f[n_dec - 128 .. n_dec)
 #pragma unroll
     for (int r2 = 0; r2 < 2; ++r2) {
@@ -1216,6 +1307,115 @@ __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(con
       const int j = Lr - 128 + t;  // >= -128
       const float f = j < NH ? P[Y::pslot(j + fu::PB)].x : P[Y::pslot(j - NH + fu::PB)].y;
       a.carry_out[ch * kWbfmCarry + 8 + t] = f;
+    }
+  }
+  wave_lds_fence();  // P / Phi reads done before the caller reuses them
+}
+
+// Single-role form: one wave per range (front, then back).
+template <int N, bool A16, bool CLAMP>
+__global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(const WbfmArgs a,
+                                                                             const WbfmFrontConst C,
+                                                                             const WbfmFusedConst Bc, int wpc) {
+  using G = fu::G;
+  using Y = fu::Geo<N>;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[Y::LdsBytes];
+  __shared__ __attribute__((aligned(16))) float Gt[128];
+  f2* U = reinterpret_cast<f2*>(lds);                          // front image ...
+  float* Phi = reinterpret_cast<float*>(lds + G::LDS_F2 * 8);  // ... and phi, then
+  f2* P = reinterpret_cast<f2*>(lds);                          // the FIR pairs over both
+  Gt[threadIdx.x] = C.g[threadIdx.x];
+  Gt[threadIdx.x + 64] = C.g[threadIdx.x + 64];
+  const FuRange g = fu_range<N>(a, blockIdx.x, wpc);
+  fu::trace(a, g.r, 0);
+  const FuPrefetch org = fu_origin(a, g);
+  f2 va[G::KL][2], vb[G::KL][2];
+  front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, threadIdx.x, va);
+  front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, threadIdx.x, vb);
+  f2 dA = f2{0, 0}, dlast = f2{0, 0};
+  fu_front_range<N, A16, CLAMP>(a, C, g, U, Phi, Gt, va, vb, FuPrefetch{nullptr, 0, 0, false}, dA, dlast);
+  fu::trace(a, g.r, 1);
+  if (a.fu_abl & 1) {  // timing only: front alone (phi kept alive)
+    if (Phi[threadIdx.x] == 1234.5f) a.y[threadIdx.x] = Phi[threadIdx.x];
+    return;
+  }
+  fu_back_range<N>(a, C, Bc, g, Phi, P, nullptr, 0);
+}
+
+// Role-split form: a workgroup of two waves walks ranges r = blockIdx.x + k G.
+// Wave 0 (front) streams range k into Phi[k & 1] (prefetching the next range's
+// first tiles across the boundary, so the input stream never pauses); wave 1
+// (back) runs hand-offs, LpCascade and the audio FIR of range k while the front
+// wave already works on range k+1. LDS flags (workgroup scope) order the two:
+// ready[b] = k+1 when range k's phi are in Phi[b]; consumed[b] = k+1 when the
+// back wave has read them. The grid is at most the resident capacity, so every
+// range's predecessor (range r-1, another workgroup, same k) is running.
+template <int N, bool A16, bool CLAMP>
+__global__ __launch_bounds__(128, 2) void k_wbfm_duo(const WbfmArgs a, const WbfmFrontConst C,
+                                                     const WbfmFusedConst Bc, int wpc, int nranges) {
+  using G = fu::G;
+  using Y = fu::Geo<N>;
+  constexpr int L = Y::L;
+  constexpr int PBytes = Y::PSlots * 8;
+  __shared__ __attribute__((aligned(16))) f2 U[G::LDS_F2];
+  __shared__ __attribute__((aligned(16))) float Phi[2][L];
+  __shared__ __attribute__((aligned(16))) f2 P[PBytes / 8];
+  __shared__ __attribute__((aligned(16))) float Gt[128];
+  __shared__ int ready[2], consumed[2];
+  __shared__ f2 dsh[2][2];  // per buffer: d[A], d[A+L-1]
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (threadIdx.x < 2) {
+    ready[threadIdx.x] = 0;
+    consumed[threadIdx.x] = 0;
+  }
+  Gt[threadIdx.x] = C.g[threadIdx.x];
+  __syncthreads();
+  const int G_ = gridDim.x;
+  if (wave == 0) {  // ---- front wave ----
+    int r = blockIdx.x;
+    if (r >= nranges) return;
+    FuRange g = fu_range<N>(a, r, wpc);
+    FuPrefetch org = fu_origin(a, g);
+    f2 va[G::KL][2], vb[G::KL][2];
+    front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, l, va);
+    front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, l, vb);
+    for (int k = 0; r < nranges; ++k, r += G_) {
+      const int b = k & 1;
+      if (k >= 2)  // the back wave has read range k-2's phi from this buffer
+        for (int it = 0; it < (1 << 24); ++it) {
+          if (__hip_atomic_load(&consumed[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= k - 1) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+      fu::trace(a, r, 0);
+      const bool more = r + G_ < nranges;
+      FuPrefetch nx{nullptr, 0, 0, false};
+      FuRange gn = g;
+      if (more) {
+        gn = fu_range<N>(a, r + G_, wpc);
+        nx = fu_origin(a, gn);
+      }
+      f2 dA = f2{0, 0}, dlast = f2{0, 0};
+      fu_front_range<N, A16, CLAMP>(a, C, g, U, Phi[b], Gt, va, vb, nx, dA, dlast);
+      if (l == 0) {
+        dsh[b][0] = dA;
+        dsh[b][1] = dlast;
+      }
+      wave_lds_fence();
+      if (l == 0) __hip_atomic_store(&ready[b], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      fu::trace(a, r, 1);
+      g = gn;
+    }
+  } else {  // ---- back wave ----
+    int k = 0;
+    for (int r = blockIdx.x; r < nranges; ++k, r += G_) {
+      const int b = k & 1;
+      for (int it = 0; it < (1 << 24); ++it) {
+        if (__hip_atomic_load(&ready[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == k + 1) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      asm volatile("" ::: "memory");
+      const FuRange g = fu_range<N>(a, r, wpc);
+      fu_back_range<N>(a, C, Bc, g, Phi[b], P, &consumed[b], k + 1);
     }
   }
 }
@@ -1312,6 +1512,31 @@ void launch_wbfm_fused(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFus
   const bool a16 = (reinterpret_cast<uintptr_t>(a.x) % 16 == 0) && (a.x_stride % 2 == 0);
   const int wpc = static_cast<int>((a.n_dec + kFuL - 1) / kFuL);
   const int grid = wpc * nch;
+  static const int kernel = [] {  // 1: one wave per range (default), 2: role-split
+    const char* e = std::getenv("ORION_WBFM_KERNEL");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (kernel == 2) {
+    // persistent: at most the resident capacity, so every range's predecessor runs
+    static int cap = 0;
+    if (cap == 0) {
+      int per_cu = 0, dev = 0, ncu = 0;
+      ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_duo<kFuN, true, false>, 128, 0));
+      ORION_HIP(hipGetDevice(&dev));
+      ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      cap = std::max(1, per_cu) * std::max(1, ncu);
+    }
+    const int g2 = std::min(grid, cap);
+    if (a.n < 2LL * Fw<2>::NEW) {
+      if (a16) k_wbfm_duo<kFuN, true, true><<<g2, 128, 0, s>>>(a, f, b, wpc, grid);
+      else k_wbfm_duo<kFuN, false, true><<<g2, 128, 0, s>>>(a, f, b, wpc, grid);
+    } else {
+      if (a16) k_wbfm_duo<kFuN, true, false><<<g2, 128, 0, s>>>(a, f, b, wpc, grid);
+      else k_wbfm_duo<kFuN, false, false><<<g2, 128, 0, s>>>(a, f, b, wpc, grid);
+    }
+    ORION_LAUNCH_CHECK();
+    return;
+  }
   if (a.n < 2LL * Fw<2>::NEW) {
     if (a16) k_wbfm_fused<kFuN, true, true><<<grid, 64, 0, s>>>(a, f, b, wpc);
     else k_wbfm_fused<kFuN, false, true><<<grid, 64, 0, s>>>(a, f, b, wpc);

@@ -106,7 +106,10 @@ struct WbfmArgs {
   uint32_t* flags;                                  // [slots][3] epoch of the last publish
   int* err;                                         // set if a hand-off wait timed out
   uint32_t epoch;                                   // this launch's tag (never 0)
+  long long* trace;                                 // debug: per-wave phase timestamps (or null)
+  int fu_abl;                                       // timing ablations of the fused kernel (0)
 };
+constexpr int kFuTracePoints = 10;
 void launch_wbfm(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmBackConst& b, int nch,
                  hipStream_t s);
 // Fused chain: requires ||A^kFuL|| negligible (the block checks it); returns the
