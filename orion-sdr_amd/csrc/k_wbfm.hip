@@ -323,6 +323,34 @@ __device__ __forceinline__ void front2_decim(const f2* __restrict__ U, int l, co
   }
 }
 
+// The same FIR software-pipelined over the phases: phase c+1's window reads and
+// tap loads are issued before phase c's FMAs, so their latency (and the full
+// lgkmcnt drain a scalar tap load forces) overlaps a phase of arithmetic. Same
+// summation order as front2_decim (bit-identical).
+template <int R>
+__device__ __forceinline__ void front2_decim_pipe(const f2* __restrict__ U, int l, const float* __restrict__ g,
+                                                  f2 (&d)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) d[r] = f2{0.0f, 0.0f};
+  f4 wa[Fw<R>::WIN], wb[Fw<R>::WIN];
+  float ta[Q], tb[Q];
+  front2_taps(g, 0, ta);
+  front2_window<R>(U, l, 0, wa);
+#pragma unroll 1
+  for (int c = 0; c < M - 2; c += 2) {
+    front2_taps(g, c + 1, tb);
+    front2_window<R>(U, l, c + 1, wb);
+    front2_phase<R>(wa, ta, d);
+    front2_taps(g, c + 2, ta);
+    front2_window<R>(U, l, c + 2, wa);
+    front2_phase<R>(wb, tb, d);
+  }
+  front2_taps(g, M - 1, tb);
+  front2_window<R>(U, l, M - 1, wb);
+  front2_phase<R>(wa, ta, d);
+  front2_phase<R>(wb, tb, d);
+}
+
 // Same FIR with the taps in LDS (phase-major, 16 floats per phase = 4 broadcast
 // ds_read_b128): every operand wait is then an LDS wait the compiler can count
 // (scalar tap loads share lgkmcnt and force a full drain per phase), so with the
@@ -901,6 +929,16 @@ struct FuPrefetch {  // where the tile two ahead starts
   bool on;
 };
 
+#ifndef ORION_FU_ABL
+#define ORION_FU_ABL 0  // timing experiments only (separate builds): 2 no decim FIR, 4 no staging
+#endif
+#ifndef ORION_FU_PIPE
+#define ORION_FU_PIPE 0  // software-pipelined decimating FIR (front2_decim_pipe; measured slower: SGPR spills)
+#endif
+#ifndef ORION_FU_DEPTH
+#define ORION_FU_DEPTH 2  // front tiles in flight per wave (2 or 3; 3 measured no faster)
+#endif
+
 template <bool A16, bool CLAMP>
 __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, long long jd0, const f2 (&ph)[8][2],
                                         f2 (&v)[8][2], const FuPrefetch& pf, f2 Sv, f2& carry, f2& dA) {
@@ -924,6 +962,11 @@ __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, 
   const bool bnd = porg < 0 || porg + 8LL * (G::TW + Q) > T.a.n;
 #pragma unroll
   for (int k = 0; k < G::KL; ++k) {
+    if constexpr (ORION_FU_ABL & 4) {  // timing experiment: no staging (loads kept alive)
+      if (k == 0) U[T.s0] = v[0][0] + v[1][0] + v[2][0] + v[3][0] + v[4][0] + v[5][0] + v[6][0] + v[7][0];
+      if (k == 0) U[T.s1] = v[0][1] + v[1][1] + v[2][1] + v[3][1] + v[4][1] + v[5][1] + v[6][1] + v[7][1];
+      continue;
+    }
     U[T.s0 + 16 * k] = cmul_rot_pk(v[k][0], ph[k][0]);
     U[T.s1 + 16 * k] = cmul_rot_pk(v[k][1], ph[k][1]);
     if (k % 4 == 3) asm volatile("" ::: "memory");
@@ -947,7 +990,14 @@ __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, 
   }
   wave_lds_fence();
   f2 d[R];
-  front2_decim<R>(U, l, T.C.g, d);
+  if constexpr (ORION_FU_ABL & 2) {  // timing experiment: no decimating FIR
+    d[0] = U[l];
+    d[1] = U[l + 64];
+  } else if constexpr (ORION_FU_PIPE) {
+    front2_decim_pipe<R>(U, l, T.C.g, d);
+  } else {
+    front2_decim<R>(U, l, T.C.g, d);
+  }
   const f2 S = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.x), n)),
                   __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.y), n))};
 #pragma unroll
@@ -1079,13 +1129,89 @@ __device__ __forceinline__ void fu_front_range(const WbfmArgs& a, const WbfmFron
   for (int n = 0; n < N; n += 2, porg += 2 * G::NEW) {
     const long long jd0 = g.A + static_cast<long long>(n) * G::TW;
     FuPrefetch p0{org.xl, org.nl, porg + 2 * G::NEW, true}, p1{org.xl, org.nl, porg + 3 * G::NEW, true};
-    // past the range: the next range's first tiles, or (none) a harmless re-read
-    if (n + 2 >= N) p0 = nx.on ? FuPrefetch{nx.xl, nx.nl, nx.porg, true} : FuPrefetch{org.xl, org.nl, porg, true};
-    if (n + 3 >= N)
-      p1 = nx.on ? FuPrefetch{nx.xl, nx.nl, nx.porg + G::NEW, true} : FuPrefetch{org.xl, org.nl, porg, true};
+    // past the range: the next range's first tiles, or (none) a dummy read of the
+    // channel's first tile, shared by all of the channel's ranges so that it hits
+    // in L2 (re-reading this range's own tile would cost HBM: 2 tiles in N)
+    const FuPrefetch dummy{org.xl, org.nl, -8LL * Q, true};
+    if (n + 2 >= N) p0 = nx.on ? FuPrefetch{nx.xl, nx.nl, nx.porg, true} : dummy;
+    if (n + 3 >= N) p1 = nx.on ? FuPrefetch{nx.xl, nx.nl, nx.porg + G::NEW, true} : dummy;
     fu_tile<A16, CLAMP>(T, n, porg, jd0, ph, va, p0, Sv, carry, dA);
     fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + G::TW, ph, vb, p1, Sv, carry, dA);
   }
+  dlast = carry;
+}
+
+// The same front with three tiles in flight (va, vb, vc: tiles 0, 1, 2 on
+// entry). The prefetch for tile n + 3 is issued while tile n is consumed, so the
+// decimating FIR of tile n overlaps the loads of three tiles. N = 1 (mod 3): a
+// loop over groups of three, then the last four tiles peeled.
+template <int N, bool A16, bool CLAMP>
+__device__ __forceinline__ void fu_front_range3(const WbfmArgs& a, const WbfmFrontConst& C, const FuRange& g,
+                                                f2* U, float* Phi, const float* Gt, f2 (&va)[8][2], f2 (&vb)[8][2],
+                                                f2 (&vc)[8][2], f2& dA, f2& dlast) {
+  static_assert(N % 3 == 1 && N >= 4, "three-deep front: N = 1 (mod 3)");
+  using G = fu::G;
+  const int l = threadIdx.x & 63;
+  const f2* __restrict__ tabc = a.tab + static_cast<long long>(g.ch) * kWbfmNS;
+  const f2* __restrict__ xc = a.x + g.ch * a.x_stride;
+  const f2* __restrict__ hc = a.hist_in + g.ch * kWbfmHist;
+  const FuPrefetch org = fu_origin(a, g);
+  const f4 tv = *reinterpret_cast<const f4*>(tabc + 8 * Q + 2 * l);
+  const f2 tb0 = f2{tv.x, tv.y}, tb1 = f2{tv.z, tv.w};
+  f2 ph[G::KL][2];
+#pragma unroll
+  for (int k = 0; k < G::KL; ++k) {
+    const f2 ek = tabc[128 * k];
+    ph[k][0] = cmul(tb0, ek);
+    ph[k][1] = cmul(tb1, ek);
+  }
+  const f2 cn = tabc[G::NEW];
+  const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
+  const FuTile T{a, C, U, Phi, Gt, xc, hc, tabc, g.ch, l, c0 * G::LR + (8 * Q + 2 * l + c0) / 8,
+                 c1 * G::LR + (8 * Q + 2 * l + 1 + c1) / 8, f2{cn.x, -cn.y}, g.first};
+  {  // halo rows of the first tile (p = 2l, 2l+1): clamped here, exact via the boundary fixup
+    const long long P0 = org.porg + 2 * l;
+    const long long hi = (org.nl & ~1LL) - 2;
+    const long long Pc = P0 < 0 ? 0 : (P0 > hi ? hi : P0);
+    const f2 x0 = org.xl[Pc], x1 = org.xl[Pc + 1];
+    const f4 th = *reinterpret_cast<const f4*>(tabc + 2 * l);
+    U[c0 * G::LR + (2 * l + c0) / 8] = cmul_rot(x0, f2{th.x, th.y});
+    U[c1 * G::LR + (2 * l + 1 + c1) / 8] = cmul_rot(x1, f2{th.z, th.w});
+  }
+  {  // p = -l (row c = l, i = 0), l = 1..7: used only by d[A-1] (see fu_front_range)
+    const long long Pm = max(org.porg - (l & 7), 0LL);
+    const f2 xm = xc[Pm];
+    const f2 tc = tabc[l & 7];
+    if (!g.first && l >= 1 && l < 8) U[l * G::LR] = cmul_rot(xm, f2{tc.x, -tc.y});
+  }
+  const f2 Sv = phasor_q64(static_cast<uint64_t>(a.k0 + org.porg + 1 + static_cast<long long>(l) * G::NEW),
+                           a.step[g.ch]);
+  f2 carry = f2{0.0f, 0.0f};
+  if (g.first) {  // d[-1]: the last decimated sample of the previous call (fm.rs:29 on reset)
+    const float* ci = a.carry_in + g.ch * kWbfmCarry;
+    carry = f2{ci[4], ci[5]};
+  }
+  // tile m's prefetch descriptor: past the range, the channel's first tile (an
+  // L2-resident dummy; see fu_front_range)
+  auto pf = [&](int m) {
+    return m < N ? FuPrefetch{org.xl, org.nl, org.porg + static_cast<long long>(m) * G::NEW, true}
+                 : FuPrefetch{org.xl, org.nl, -8LL * Q, true};
+  };
+  auto tile = [&](int n, f2(&v)[8][2]) {
+    fu_tile<A16, CLAMP>(T, n, org.porg + static_cast<long long>(n) * G::NEW,
+                        g.A + static_cast<long long>(n) * G::TW, ph, v, pf(n + 3), Sv, carry, dA);
+  };
+  int n = 0;
+#pragma unroll 1
+  for (; n < N - 4; n += 3) {
+    tile(n, va);
+    tile(n + 1, vb);
+    tile(n + 2, vc);
+  }
+  tile(n, va);
+  tile(n + 1, vb);
+  tile(n + 2, vc);
+  tile(n + 3, va);
   dlast = carry;
 }
 
@@ -1313,10 +1439,11 @@ __device__ __forceinline__ void fu_back_range(const WbfmArgs& a, const WbfmFront
 }
 
 // Single-role form: one wave per range (front, then back).
-template <int N, bool A16, bool CLAMP>
+template <int N, bool A16, bool CLAMP, bool PERS>
 __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(const WbfmArgs a,
                                                                              const WbfmFrontConst C,
-                                                                             const WbfmFusedConst Bc, int wpc) {
+                                                                             const WbfmFusedConst Bc, int wpc,
+                                                                             int total) {
   using G = fu::G;
   using Y = fu::Geo<N>;
   __shared__ __attribute__((aligned(16))) unsigned char lds[Y::LdsBytes];
@@ -1326,20 +1453,51 @@ __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(con
   f2* P = reinterpret_cast<f2*>(lds);                          // the FIR pairs over both
   Gt[threadIdx.x] = C.g[threadIdx.x];
   Gt[threadIdx.x + 64] = C.g[threadIdx.x + 64];
-  const FuRange g = fu_range<N>(a, blockIdx.x, wpc);
-  fu::trace(a, g.r, 0);
-  const FuPrefetch org = fu_origin(a, g);
   f2 va[G::KL][2], vb[G::KL][2];
-  front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, threadIdx.x, va);
-  front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, threadIdx.x, vb);
   f2 dA = f2{0, 0}, dlast = f2{0, 0};
-  fu_front_range<N, A16, CLAMP>(a, C, g, U, Phi, Gt, va, vb, FuPrefetch{nullptr, 0, 0, false}, dA, dlast);
-  fu::trace(a, g.r, 1);
-  if (a.fu_abl & 1) {  // timing only: front alone (phi kept alive)
-    if (Phi[threadIdx.x] == 1234.5f) a.y[threadIdx.x] = Phi[threadIdx.x];
-    return;
+  if constexpr (!PERS) {  // one range per wave (gridDim.x = total)
+    const FuRange g = fu_range<N>(a, blockIdx.x, wpc);
+    fu::trace(a, g.r, 0);
+    const FuPrefetch org = fu_origin(a, g);
+    front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, threadIdx.x, va);
+    front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, threadIdx.x, vb);
+    if constexpr (ORION_FU_DEPTH == 3) {
+      f2 vc[G::KL][2];
+      front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + 2 * G::NEW, threadIdx.x, vc);
+      fu_front_range3<N, A16, CLAMP>(a, C, g, U, Phi, Gt, va, vb, vc, dA, dlast);
+    } else {
+      fu_front_range<N, A16, CLAMP>(a, C, g, U, Phi, Gt, va, vb, FuPrefetch{nullptr, 0, 0, false}, dA, dlast);
+    }
+    fu::trace(a, g.r, 1);
+    if (a.fu_abl & 1) {  // timing only: front alone (phi kept alive)
+      if (Phi[threadIdx.x] == 1234.5f) a.y[threadIdx.x] = Phi[threadIdx.x];
+      return;
+    }
+    fu_back_range<N>(a, C, Bc, g, Phi, P, nullptr, 0);
+  } else {
+    // persistent (gridDim.x <= resident capacity): ranges r = blockIdx.x + k
+    // gridDim.x, each range's first two tiles prefetched across the previous
+    // range's back phase
+    int r = blockIdx.x;
+    const FuPrefetch org = fu_origin(a, fu_range<N>(a, r, wpc));
+    front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, threadIdx.x, va);
+    front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, threadIdx.x, vb);
+#pragma unroll 1
+    for (; r < total; r += gridDim.x) {
+      const FuRange g = fu_range<N>(a, r, wpc);
+      fu::trace(a, g.r, 0);
+      const int rn = r + static_cast<int>(gridDim.x);
+      const FuPrefetch nx = rn < total ? fu_origin(a, fu_range<N>(a, rn, wpc)) : FuPrefetch{nullptr, 0, 0, false};
+      fu_front_range<N, A16, CLAMP>(a, C, g, U, Phi, Gt, va, vb, nx, dA, dlast);
+      fu::trace(a, g.r, 1);
+      if (a.fu_abl & 1) {
+        if (Phi[threadIdx.x] == 1234.5f) a.y[threadIdx.x] = Phi[threadIdx.x];
+        wave_lds_fence();
+        continue;
+      }
+      fu_back_range<N>(a, C, Bc, g, Phi, P, nullptr, 0);
+    }
   }
-  fu_back_range<N>(a, C, Bc, g, Phi, P, nullptr, 0);
 }
 
 // Role-split form: a workgroup of two waves walks ranges r = blockIdx.x + k G.
@@ -1416,6 +1574,86 @@ __global__ __launch_bounds__(128, 2) void k_wbfm_duo(const WbfmArgs a, const Wbf
       asm volatile("" ::: "memory");
       const FuRange g = fu_range<N>(a, r, wpc);
       fu_back_range<N>(a, C, Bc, g, Phi[b], P, &consumed[b], k + 1);
+    }
+  }
+}
+
+// Role-split form with NF front waves per back wave: a workgroup of NF + 1
+// waves; front wave f walks ranges r = (NF k + f) G + blockIdx.x (k = 0, 1, ..),
+// so a range's predecessor belongs to the neighbouring workgroup at the same
+// step (no hand-off chain across workgroups). Every front streams continuously
+// into its own Phi[f]; the back wave takes the NF ranges of step k in order,
+// reads each one's phi into registers (consumed[f] = k + 1) and runs its
+// hand-off, LpCascade and audio FIR while the fronts stream on. The fronts keep
+// the input stream busy through the backs (a CU holds 2 such workgroups: 2 NF
+// streaming waves), instead of every wave of a CU pausing its stream for its
+// own back phase at the same time. Grid: at most the resident capacity.
+template <int N, bool A16, bool CLAMP, int NF>
+__global__ __launch_bounds__(64 * (NF + 1), 2) void k_wbfm_team(const WbfmArgs a, const WbfmFrontConst C,
+                                                                const WbfmFusedConst Bc, int wpc, int nranges) {
+  using G = fu::G;
+  using Y = fu::Geo<N>;
+  constexpr int L = Y::L;
+  __shared__ __attribute__((aligned(16))) f2 U[NF][G::LDS_F2];
+  __shared__ __attribute__((aligned(16))) float Phi[NF][L];
+  __shared__ __attribute__((aligned(16))) f2 P[Y::PSlots];
+  __shared__ __attribute__((aligned(16))) float Gt[128];
+  __shared__ int ready[NF], consumed[NF];
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (threadIdx.x < NF) {
+    ready[threadIdx.x] = 0;
+    consumed[threadIdx.x] = 0;
+  }
+  if (threadIdx.x < 128) Gt[threadIdx.x] = C.g[threadIdx.x];
+  __syncthreads();
+  const int G_ = gridDim.x;
+  if (wave < NF) {  // ---- front wave f ----
+    const int f = wave;
+    int r = f * G_ + blockIdx.x;
+    if (r >= nranges) return;
+    FuRange g = fu_range<N>(a, r, wpc);
+    const FuPrefetch org = fu_origin(a, g);
+    f2 va[G::KL][2], vb[G::KL][2];
+    front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, l, va);
+    front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, l, vb);
+    for (int k = 0; r < nranges; ++k) {
+      if (k >= 1)  // the back wave has read range k-1's phi from Phi[f]
+        for (int it = 0; it < (1 << 24); ++it) {
+          if (__hip_atomic_load(&consumed[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= k) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+      fu::trace(a, r, 0);
+      const int rn = r + NF * G_;
+      FuPrefetch nx{nullptr, 0, 0, false};
+      FuRange gn = g;
+      if (rn < nranges) {
+        gn = fu_range<N>(a, rn, wpc);
+        nx = fu_origin(a, gn);
+      }
+      f2 dA = f2{0, 0}, dlast = f2{0, 0};
+      fu_front_range<N, A16, CLAMP>(a, C, g, U[f], Phi[f], Gt, va, vb, nx, dA, dlast);
+      wave_lds_fence();
+      if (l == 0) __hip_atomic_store(&ready[f], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      fu::trace(a, r, 1);
+      g = gn;
+      r = rn;
+    }
+  } else {  // ---- back wave ----
+    for (int k = 0;; ++k) {
+      for (int f = 0; f < NF; ++f) {
+        const int r = (NF * k + f) * G_ + blockIdx.x;
+        if (r >= nranges) return;
+        for (int it = 0; it < (1 << 24); ++it) {
+          if (__hip_atomic_load(&ready[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == k + 1) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        asm volatile("" ::: "memory");
+        if (a.fu_abl & 1) {  // timing only: fronts alone
+          if (l == 0) __hip_atomic_store(&consumed[f], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          continue;
+        }
+        fu_back_range<N>(a, C, Bc, fu_range<N>(a, r, wpc), Phi[f], P, &consumed[f], k + 1);
+      }
     }
   }
 }
@@ -1537,13 +1775,54 @@ void launch_wbfm_fused(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFus
     ORION_LAUNCH_CHECK();
     return;
   }
-  if (a.n < 2LL * Fw<2>::NEW) {
-    if (a16) k_wbfm_fused<kFuN, true, true><<<grid, 64, 0, s>>>(a, f, b, wpc);
-    else k_wbfm_fused<kFuN, false, true><<<grid, 64, 0, s>>>(a, f, b, wpc);
-  } else {
-    if (a16) k_wbfm_fused<kFuN, true, false><<<grid, 64, 0, s>>>(a, f, b, wpc);
-    else k_wbfm_fused<kFuN, false, false><<<grid, 64, 0, s>>>(a, f, b, wpc);
+  if (kernel == 4) {  // team: 3 front waves + 1 back wave per workgroup
+    constexpr int NF = 3;
+    static int cap = 0;
+    if (cap == 0) {
+      int per_cu = 0, dev = 0, ncu = 0;
+      ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_team<kFuN, true, false, NF>,
+                                                             64 * (NF + 1), 0));
+      ORION_HIP(hipGetDevice(&dev));
+      ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      cap = std::max(1, per_cu) * std::max(1, ncu);
+    }
+    const int g4 = std::min((grid + NF - 1) / NF, cap);
+    const bool clamp = a.n < 2LL * Fw<2>::NEW;
+#define ORION_TEAM(A, C) k_wbfm_team<kFuN, A, C, NF><<<g4, 64 * (NF + 1), 0, s>>>(a, f, b, wpc, grid)
+    if (clamp) { if (a16) ORION_TEAM(true, true); else ORION_TEAM(false, true); }
+    else { if (a16) ORION_TEAM(true, false); else ORION_TEAM(false, false); }
+#undef ORION_TEAM
+    ORION_LAUNCH_CHECK();
+    return;
   }
+  int g1 = grid;
+  // experiments only: dynamic LDS padding per wave (caps the waves per CU)
+  static const int dyn = [] {
+    const char* e = std::getenv("ORION_WBFM_DYNLDS");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (kernel == 3) {  // persistent single-role: at most the resident capacity
+    static int cap = 0;
+    if (cap == 0) {
+      int per_cu = 0, dev = 0, ncu = 0;
+      ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_fused<kFuN, true, false, true>, 64, dyn));
+      ORION_HIP(hipGetDevice(&dev));
+      ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      cap = std::max(1, per_cu) * std::max(1, ncu);
+    }
+    g1 = std::min(grid, cap);
+  }
+  const bool clamp = a.n < 2LL * Fw<2>::NEW;
+  const bool pers = g1 < grid;
+#define ORION_FU(A, C, P) k_wbfm_fused<kFuN, A, C, P><<<g1, 64, dyn, s>>>(a, f, b, wpc, grid)
+  if (pers) {
+    if (clamp) { if (a16) ORION_FU(true, true, true); else ORION_FU(false, true, true); }
+    else { if (a16) ORION_FU(true, false, true); else ORION_FU(false, false, true); }
+  } else {
+    if (clamp) { if (a16) ORION_FU(true, true, false); else ORION_FU(false, true, false); }
+    else { if (a16) ORION_FU(true, false, false); else ORION_FU(false, false, false); }
+  }
+#undef ORION_FU
   ORION_LAUNCH_CHECK();
 }
 

@@ -31,7 +31,8 @@ __all__ = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(os.path.dirname(_HERE), "lib", "liborion_sdr_amd.so")
+# ORION_SDR_LIB: an alternative build of the same library (timing experiments)
+_LIB = os.environ.get("ORION_SDR_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "liborion_sdr_amd.so")
 
 
 def lib_path() -> str:
