@@ -47,9 +47,15 @@ __device__ __forceinline__ f2 cmul_rot(f2 x, f2 p) {
 // cmul_rot with the same roundings, written as packed-f32 ops (v_pk_mul_f32 +
 // v_pk_fma_f32, the negation folded into a source modifier): t = (b*d, a*d)
 // rounded, then (fma(a, c, -t.x), fma(b, c, t.y)) for x = (a, b), p = (c, d).
+// Written in VOP3P asm: the compiler does not fold the half-negation into the
+// FMA's neg_lo modifier and emits a v_pk_add + v_mov instead (4 VALU, not 2).
 __device__ __forceinline__ f2 cmul_rot_pk(f2 x, f2 p) {
-  const f2 t = f2{x.y, x.x} * f2{p.y, p.y};
-  return __builtin_elementwise_fma(x, f2{p.x, p.x}, f2{-t.x, t.y});
+  f2 t, r;
+  // t.lo = x.hi * p.hi, t.hi = x.lo * p.hi
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,1]" : "=v"(t) : "v"(x), "v"(p));
+  // r.lo = fma(x.lo, p.lo, -t.lo), r.hi = fma(x.hi, p.lo, t.hi)
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(x), "v"(p), "v"(t));
+  return r;
 }
 // Plain complex multiply (ours, not a reference op order).
 __device__ __forceinline__ f2 cmul(f2 a, f2 b) {
@@ -103,6 +109,36 @@ __device__ __forceinline__ float fm_disc_pk(f2 z, f2 p, float k) {
   const f2 b = f2{z.y, z.x} * f2{p.y, p.y};
   const f2 s = a + f2{b.x, -b.y};
   return atan2_approx(s.y, s.x) * k;
+}
+
+// atan2_approx with the ratio from the hardware reciprocal (v_rcp_f32, 1 ulp)
+// instead of the IEEE division sequence (~11 VALU): used where the chain is held
+// to a tolerance rather than bit-exactness (the fused WBFM front).
+__device__ __forceinline__ float atan2_approx_rcp(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const bool swap = ax < ay;
+  const float mn = swap ? ax : ay;
+  const float mx = swap ? ay : ax;
+  const float r = mn * __builtin_amdgcn_rcpf(mx + 1.1920929e-7f);
+  const float r2 = r * r;
+  float phi = r * (0.7853981633974483f + r2 * (-0.2447f + r2 * 0.0663f));
+  if (swap) phi = 1.5707963267948966f - phi;
+  const float sgn = (y < 0.0f) ? -1.0f : 1.0f;
+  return (x < 0.0f) ? (3.14159265358979323846f - phi) * sgn : phi * sgn;
+}
+__device__ __forceinline__ f2 fm_prod_pk(f2 z, f2 p) {
+  f2 a, b, q;
+  // a = (z.lo p.lo, z.hi p.lo)
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(a) : "v"(z), "v"(p));
+  // b = (z.hi p.hi, z.lo p.hi)
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,1]" : "=v"(b) : "v"(z), "v"(p));
+  // q = (a.lo + b.lo, a.hi - b.hi)
+  asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(q) : "v"(a), "v"(b));
+  return q;
+}
+__device__ __forceinline__ float fm_disc_pk_rcp(f2 z, f2 p, float k) {
+  const f2 s = fm_prod_pk(z, p);
+  return atan2_approx_rcp(s.y, s.x) * k;
 }
 
 // PmQuadratureDemod, demodulate/pm.rs:56-57: num-complex z * conj(prev),

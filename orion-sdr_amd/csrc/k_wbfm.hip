@@ -1018,8 +1018,8 @@ __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, 
     carry = cmul(acc, S);
   }
   const f2 pv = f2{wave_shr1(d[R - 1].x, carry.x), wave_shr1(d[R - 1].y, carry.y)};
-  T.Phi[G::TW * n + 2 * l] = fm_disc_pk(d[0], pv, T.C.k);
-  T.Phi[G::TW * n + 2 * l + 1] = fm_disc_pk(d[1], d[0], T.C.k);
+  T.Phi[G::TW * n + 2 * l] = fm_disc_pk_rcp(d[0], pv, T.C.k);
+  T.Phi[G::TW * n + 2 * l + 1] = fm_disc_pk_rcp(d[1], d[0], T.C.k);
   if (n == 0) dA = d[0];
   carry = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[R - 1].x), 63)),
              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[R - 1].y), 63))};

@@ -77,7 +77,10 @@ struct WbfmBackConst {
   double mw[16];              // A^(64 C): one wave's span
 };
 // Fused single-kernel chain (k_wbfm_fused): one wave per range of kFuL outputs.
-constexpr int kFuN = 16;                             // front tiles (128 outputs) per range
+#ifndef ORION_FU_N
+#define ORION_FU_N 16
+#endif
+constexpr int kFuN = ORION_FU_N;                     // front tiles (128 outputs) per range
 constexpr int kFuL = kFuN * 128;                     // 2048 outputs per wave range
 constexpr int kFuC = kFuL / 128;                     // IIR samples per lane and half (16)
 constexpr int kFuTail = 128;                         // IIR outputs handed to the next range
