@@ -331,6 +331,33 @@ class WbfmBlock final : public Block {
       std::copy(m.begin(), m.end(), lf.begin() + L * 16);
     }
     lanemats_fu_.upload(lf.data(), lf.size() * sizeof(double));
+    // segmented chain constants: chunks of kSgC per lane, halves of kSgL/2
+    std::memset(&cs_, 0, sizeof(cs_));
+    for (size_t k = 0; k < a.size(); ++k) cs_.a[k] = a[k];
+    cs_.b0 = bq.b0; cs_.b1 = bq.b1; cs_.b2 = bq.b2; cs_.a1 = bq.a1; cs_.a2 = bq.a2;
+    auto ps = mat_pow(ss.A, 4, kSgC);
+    for (int s = 0; s < 6; ++s) {
+      for (int i = 0; i < 16; ++i) cs_.pw[s * 16 + i] = ps[i];
+      ps = mat_mul(ps, ps, 4);
+    }
+    const auto msh = mat_pow(ss.A, 4, kSgL / 2);
+    for (int i = 0; i < 16; ++i) cs_.mh[i] = msh[i];
+    std::vector<double> ls(64 * 16);
+    for (int L = 0; L < 64; ++L) {
+      const auto m = mat_pow(ss.A, 4, static_cast<uint64_t>(kSgC) * L);
+      std::copy(m.begin(), m.end(), ls.begin() + L * 16);
+    }
+    lanemats_sg_.upload(ls.data(), ls.size() * sizeof(double));
+    // The segmented chain starts every segment's first sub-range from a zero
+    // state and hands the next sub-range that sub-range's zero-state end state
+    // and last 128 outputs: exact when A^(kSgL - 128) is below f32 resolution
+    // relative to A^0 = I (~1e-16 for the WBFM defaults).
+    {
+      const auto m = mat_pow(ss.A, 4, kSgL - 128);
+      double fro = 0.0;
+      for (double v : m) fro += v * v;
+      seg_ok_ = std::sqrt(fro) < 1e-10;
+    }
     // The fused chain hands each range only its predecessor's zero-state IIR
     // aggregate, exact when A^kFuL (the state carried across one whole range)
     // is below f32 resolution relative to A^0 = I; the 4th-order Butterworth at
@@ -396,15 +423,22 @@ class WbfmBlock final : public Block {
       a.hist_out = hist_[nxt].as<f2>();
       a.lanemats = lanemats_.as<double>();
       static const char* path = std::getenv("ORION_WBFM_PATH");  // "split": force the two-kernel path
-      const bool fused = fused_ok_ && !(path && std::strcmp(path, "split") == 0);
+      // default: the segmented kernel; "fused": one wave per 2048-output range;
+      // "split": the two-kernel path (also the fallback for slow IIR poles)
+      const bool want_split = path && std::strcmp(path, "split") == 0;
+      const bool want_fused = path && std::strcmp(path, "fused") == 0;
+      const bool seg = seg_ok_ && !want_split && !want_fused;
+      const bool fused = (fused_ok_ && want_fused) || seg;
       if (fused) {
-        const long long slots = wbfm_fused_slots(static_cast<long long>(n_dec), nch_);
+        const long long slots = seg ? wbfm_seg_slots(static_cast<long long>(n_dec), nch_)
+                                    : wbfm_fused_slots(static_cast<long long>(n_dec), nch_);
         if (static_cast<size_t>(slots) * kFuSlot * 4 > hand_.size()) {
           hand_.resize(static_cast<size_t>(slots) * kFuSlot * 4);
           flags_.resize(static_cast<size_t>(slots) * 3 * 4);
           flags_.zero(s);  // epochs start at 1: a zeroed flag never matches
         }
         a.lanemats_fu = lanemats_fu_.as<double>();
+        a.lanemats_sg = lanemats_sg_.as<double>();
         a.hand = hand_.as<uint32_t>();
         a.flags = flags_.as<uint32_t>();
         a.err = err_.as<int>();
@@ -424,7 +458,8 @@ class WbfmBlock final : public Block {
           flags_.zero(s);
           epoch_ = 0;
         }
-        launch_wbfm_fused(a, cf_, cu_, nch_, s);
+        if (seg) launch_wbfm_seg(a, cf_, cs_, nch_, s);
+        else launch_wbfm_fused(a, cf_, cu_, nch_, s);
         if (trace_path) {  // debug: dump this launch's timestamps (overwrites: last launch wins)
           std::vector<long long> h(static_cast<size_t>(slots) * kFuTracePoints);
           ORION_HIP(hipMemcpyAsync(h.data(), trace_.as<void>(), h.size() * 8, hipMemcpyDeviceToHost, s));
@@ -469,10 +504,10 @@ class WbfmBlock final : public Block {
   std::vector<float> h_dec_, h_aud_;
   WbfmFrontConst cf_;
   WbfmBackConst cb_;
-  WbfmFusedConst cu_;
-  bool fused_ok_ = false;
+  WbfmFusedConst cu_, cs_;
+  bool fused_ok_ = false, seg_ok_ = false;
   uint32_t epoch_ = 0;
-  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, lanemats_fu_, hand_, flags_, err_, trace_;
+  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, lanemats_fu_, lanemats_sg_, hand_, flags_, err_, trace_;
   int cur_ = 0;
   uint64_t k0_ = 0;
 };

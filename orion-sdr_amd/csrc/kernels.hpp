@@ -105,6 +105,7 @@ struct WbfmArgs {
   const double* lanemats;                           // A^(C L), L = 0..63 (16 doubles each)
   // fused chain only
   const double* lanemats_fu;                        // A^(kFuC L), L = 0..63
+  const double* lanemats_sg;                        // A^(kSgC L), L = 0..63 (k_wbfm_seg)
   uint32_t* hand;                                   // [slots][kFuSlot] hand-off data
   uint32_t* flags;                                  // [slots][3] epoch of the last publish
   int* err;                                         // set if a hand-off wait timed out
@@ -118,6 +119,12 @@ void launch_wbfm(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmBackConst
 // Fused chain: requires ||A^kFuL|| negligible (the block checks it); returns the
 // number of hand-off slots it needs for (n_dec, nch).
 long long wbfm_fused_slots(long long n_dec, int nch);
+// Segmented fused chain (k_wbfm_seg): sub-ranges of kSgL outputs, one round of
+// waves. Requires ||A^(kSgL - 128)|| negligible (the block checks it).
+constexpr int kSgL = 1024;                           // outputs per sub-range
+constexpr int kSgC = kSgL / 128;                     // IIR samples per lane and half (8)
+long long wbfm_seg_slots(long long n_dec, int nch);
+void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch, hipStream_t s);
 void launch_wbfm_fused(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
                        hipStream_t s);
 

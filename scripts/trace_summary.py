@@ -17,14 +17,23 @@ NAMES = ["front (N tiles)", "zero-state pass + scan", "publish + wait", "pass 2 
          "audio FIR + store"]
 
 
+SEG_NAMES = ["front + sub-range backs", "wait for predecessor", "sub-range 0 back"]
+
+
 def main(path):
+    global NAMES
     t = np.fromfile(path, dtype=np.int64)
-    t = t[: len(t) // PTS * PTS].reshape(-1, PTS)[:, :6]
+    t = t[: len(t) // PTS * PTS].reshape(-1, PTS)
+    if (t[:, 4] == 0).all():  # k_wbfm_seg: 4 points
+        t, NAMES = t[:, :4], SEG_NAMES
+    else:
+        t = t[:, :6]
     t = t[(t > 0).all(axis=1)]
     if len(t) == 0:
         raise SystemExit("no complete wave records")
     us = (t - t[:, :1].min()) / 100.0  # 100 MHz ticks -> us from the first wave start
-    print(f"waves: {len(t)}   kernel span: {us[:, 5].max():.1f} us   (first start 0, last start "
+    E = t.shape[1] - 1
+    print(f"waves: {len(t)}   kernel span: {us[:, E].max():.1f} us   (first start 0, last start "
           f"{us[:, 0].max():.1f} us)")
     d = np.diff(us, axis=1)
     print(f"{'phase':28s} {'mean':>8s} {'p10':>8s} {'p50':>8s} {'p90':>8s} {'max':>8s}  (us)")
@@ -32,7 +41,7 @@ def main(path):
         c = d[:, i]
         print(f"{n:28s} {c.mean():8.2f} {np.percentile(c, 10):8.2f} {np.percentile(c, 50):8.2f} "
               f"{np.percentile(c, 90):8.2f} {c.max():8.2f}")
-    tot = us[:, 5] - us[:, 0]
+    tot = us[:, E] - us[:, 0]
     print(f"{'whole wave':28s} {tot.mean():8.2f} {np.percentile(tot, 10):8.2f} {np.percentile(tot, 50):8.2f} "
           f"{np.percentile(tot, 90):8.2f} {tot.max():8.2f}")
     starts = np.sort(us[:, 0])
