@@ -7,8 +7,9 @@ C2-sized channel (2^26 cf32 @ 10 Msps, its own tuning offset; BASELINE.json
 configs[1]). Channels are independent: no collective on the data path
 ("scaling": "weak"); the only collectives are the timing barrier / max.
 
-The roofline object prices the one kernel the chain runs (k_wbfm) with HIP
-events on the stream it is launched on: algorithmic bytes per launch
+The roofline object prices the one kernel the chain runs (k_wbfm_seg2) with
+HIP events on the stream it is launched on (one pair around the K launches, so
+inter-launch gaps count against it): algorithmic bytes per launch
 (8 B cf32 in + 4 B f32 audio out per 8 inputs = 8.5 B per input sample, SURVEY
 §8d) / average kernel time, against the 8.0 TB/s HBM3E peak. The cpu_baseline
 is the scalar oracle ("port" of the reference Rust, 1 thread, the reference is
@@ -181,21 +182,23 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    # kernel timing: HIP events on the stream the kernel is launched on
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # kernel timing: one pair of HIP events on the launch stream brackets the K
+    # back-to-back launches (per-step events would add their own packets between
+    # the kernels); the average includes the inter-launch gaps (conservative)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        evs[i][0].record(stream)
+    ev0.record(stream)
+    for _ in range(args.steps):
         step()
-        evs[i][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, dist, dev)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     total = samples * world * args.steps
     value = total / elapsed / 1e6

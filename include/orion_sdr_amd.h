@@ -98,8 +98,9 @@ int orion_cw_envelope_demod_set_gain(orion_block* b, float g);
 /* The WBFM chain composed per docs/demodulate.md:128-133 (no single reference
  * type): Rotator(-f_off, fs) -> FirDecimator(fs, m, dec_cutoff, dec_trans) ->
  * FmQuadratureDemod(fs/m, dev_hz, audio_bw) -> FirLowpass(fs/m, audio_pass,
- * audio_trans). cf32 -> f32 in two gfx950 kernels per call (m must be 8):
- * front = NCO + polyphase decimation + discriminator, back = LpCascade + audio FIR. */
+ * audio_trans). cf32 -> f32 in one gfx950 kernel per call (m must be 8): NCO +
+ * polyphase decimation + discriminator + LpCascade + audio FIR, intermediates on
+ * chip (two kernels for IIR designs that decay too slowly; see configure). */
 typedef struct {
   float fs, f_off, dec_cutoff, dec_trans, dev_hz, audio_bw, audio_pass, audio_trans;
   size_t m;
@@ -107,6 +108,18 @@ typedef struct {
 orion_block* orion_wbfm_chain_new(const orion_wbfm_params* p);
 /* nch channels sharing the design, each with its own tuning offset f_off[ch]. */
 orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float* f_off, size_t nch);
+/* Engine tuning and tests (no reference counterpart): the kernel path of a WBFM
+ * chain handle. ORION_WBFM_AUTO picks the segmented single kernel when the
+ * LpCascade decays fast enough for it (the WBFM defaults), else two kernels;
+ * max_segments > 0 caps the segmented kernel's waves (0 = the resident
+ * capacity). ORION_E_TYPE if b is not a WBFM chain, ORION_E_ARG if the design
+ * cannot run on that path. */
+#define ORION_WBFM_AUTO 0
+#define ORION_WBFM_SEGMENTED 1  /* one kernel, one round of segments, FIR spread over tiles */
+#define ORION_WBFM_RANGES 2     /* one kernel, one wave per 2048-output range */
+#define ORION_WBFM_SPLIT 3      /* two kernels (front, back), any IIR design */
+#define ORION_WBFM_SEGMENTED_V1 4
+int orion_wbfm_chain_configure(orion_block* b, int path, int max_segments);
 
 /* ---- Block contract (core.rs:12-22) ------------------------------------ */
 /* Host buffers (synchronous). */

@@ -422,18 +422,22 @@ class WbfmBlock final : public Block {
       a.hist_in = hist_[cur_].as<f2>();
       a.hist_out = hist_[nxt].as<f2>();
       a.lanemats = lanemats_.as<double>();
-      static const char* path = std::getenv("ORION_WBFM_PATH");  // "split": force the two-kernel path
-      // default: the segmented kernel; "fused": one wave per 2048-output range;
-      // "split": the two-kernel path (also the fallback for slow IIR poles)
-      const bool want_split = path && std::strcmp(path, "split") == 0;
-      const bool want_fused = path && std::strcmp(path, "fused") == 0;
-      const bool seg = seg_ok_ && !want_split && !want_fused;
-      const bool fused = (fused_ok_ && want_fused) || seg;
+      int path = path_;
+      if (path == kPathAuto) {
+        static const char* env = std::getenv("ORION_WBFM_PATH");  // timing experiments
+        path = seg_ok_ ? kPathSeg2 : kPathSplit;
+        if (env && std::strcmp(env, "split") == 0) path = kPathSplit;
+        if (env && std::strcmp(env, "fused") == 0 && fused_ok_) path = kPathRange;
+        if (env && std::strcmp(env, "seg") == 0 && seg_ok_) path = kPathSeg;
+      }
+      const bool seg = path == kPathSeg || path == kPathSeg2;
+      const bool fused = seg || path == kPathRange;
       if (fused) {
         const long long slots = seg ? wbfm_seg_slots(static_cast<long long>(n_dec), nch_)
                                     : wbfm_fused_slots(static_cast<long long>(n_dec), nch_);
-        if (static_cast<size_t>(slots) * kFuSlot * 4 > hand_.size()) {
-          hand_.resize(static_cast<size_t>(slots) * kFuSlot * 4);
+        const size_t words = path == kPathSeg2 ? kSg2Slot : kFuSlot;
+        if (static_cast<size_t>(slots) * words * 4 > hand_.size()) hand_.resize(static_cast<size_t>(slots) * words * 4);
+        if (static_cast<size_t>(slots) * 3 * 4 > flags_.size()) {
           flags_.resize(static_cast<size_t>(slots) * 3 * 4);
           flags_.zero(s);  // epochs start at 1: a zeroed flag never matches
         }
@@ -458,7 +462,7 @@ class WbfmBlock final : public Block {
           flags_.zero(s);
           epoch_ = 0;
         }
-        if (seg) launch_wbfm_seg(a, cf_, cs_, nch_, s);
+        if (seg) launch_wbfm_seg(a, cf_, cs_, nch_, max_seg_, path == kPathSeg2, s);
         else launch_wbfm_fused(a, cf_, cu_, nch_, s);
         if (trace_path) {  // debug: dump this launch's timestamps (overwrites: last launch wins)
           std::vector<long long> h(static_cast<size_t>(slots) * kFuTracePoints);
@@ -489,6 +493,14 @@ class WbfmBlock final : public Block {
     k0_ = 0;
   }
   std::vector<float> taps(int which) const override { return which == 0 ? h_dec_ : h_aud_; }
+  int configure(int path, int max_seg) {
+    if (path < kPathAuto || path > kPathSeg || max_seg < 0) return -3;
+    if ((path == kPathSeg2 || path == kPathSeg) && !seg_ok_) return -3;
+    if (path == kPathRange && !fused_ok_) return -3;
+    path_ = path;
+    max_seg_ = max_seg;
+    return 0;
+  }
   void check_device_errors() override {
     int e = 0;
     ORION_HIP(hipMemcpy(&e, err_.as<void>(), sizeof(int), hipMemcpyDeviceToHost));
@@ -506,6 +518,7 @@ class WbfmBlock final : public Block {
   WbfmBackConst cb_;
   WbfmFusedConst cu_, cs_;
   bool fused_ok_ = false, seg_ok_ = false;
+  int path_ = kPathAuto, max_seg_ = 0;
   uint32_t epoch_ = 0;
   DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, lanemats_fu_, lanemats_sg_, hand_, flags_, err_, trace_;
   int cur_ = 0;
@@ -532,6 +545,11 @@ int fir_lowpass_iq_filter_aligned(Block* b, void* io, size_t n, hipStream_t s) {
 }
 std::unique_ptr<Block> make_wbfm_chain(const WbfmParams& p, const std::vector<float>& f_off) {
   return std::make_unique<WbfmBlock>(p, f_off);
+}
+int wbfm_chain_configure(Block* b, int path, int max_segments) {
+  auto* w = dynamic_cast<WbfmBlock*>(b);
+  if (!w) return -4;
+  return w->configure(path, max_segments);
 }
 
 }  // namespace orion

@@ -153,6 +153,16 @@ orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float*
   return make([&] { return orion::make_wbfm_chain(wbfm_params(p), std::vector<float>(f_off, f_off + nch)); });
 }
 
+int orion_wbfm_chain_configure(orion_block* b, int path, int max_segments) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    const int rc = orion::wbfm_chain_configure(b->impl.get(), path, max_segments);
+    if (rc == -4) return fail(ORION_E_TYPE, "not a WBFM chain");
+    if (rc != 0) return fail(ORION_E_ARG, "WBFM path unavailable for this design (or bad arguments)");
+    return ORION_OK;
+  });
+}
+
 int orion_block_process(orion_block* b, const void* in, size_t n_in, void* out, size_t out_cap,
                         orion_work_report* wr) {
   if (!b) return fail(ORION_E_NULL, "null handle");

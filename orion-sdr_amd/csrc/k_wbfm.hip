@@ -994,6 +994,8 @@ __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, 
   if constexpr (ORION_FU_ABL & 2) {  // timing experiment: no decimating FIR
     d[0] = U[l];
     d[1] = U[l + 64];
+  } else if constexpr (ORION_FU_PIPE == 2) {
+    front2_decim_lds<R>(U, l, T.Gt, d);
   } else if constexpr (ORION_FU_PIPE) {
     front2_decim_pipe<R>(U, l, T.C.g, d);
   } else {
@@ -1531,7 +1533,7 @@ __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(con
 #endif
 #ifndef ORION_SEG_ABL
 #define ORION_SEG_ABL 0  // timing experiments only (separate builds): 1 no sub-range backs, 2 no
-                         // zero-state pass, 4 no deferred back
+                         // zero-state pass, 4 no deferred back, 8 no spread FIR blocks (seg2)
 #endif
 #ifndef ORION_SEG_PRIO_Q16
 #define ORION_SEG_PRIO_Q16 9
@@ -1907,6 +1909,340 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
   fu::trace(a, g.r, 3);
 }
 
+// ---- segmented chain, FIR-spread form ---------------------------------------------
+// k_wbfm_seg2: k_wbfm_seg's one round of segments, with the back of the chain
+// split so that the input stream is never held up by the audio FIR:
+//   * at the end of sub-range k only its IIR runs (zero-state pass, f64 scan,
+//     the reference recurrence -> the FIR pair image P, about a quarter of a
+//     back), covered by the two prefetched tiles;
+//   * sub-range k's audio FIR runs as 8 blocks of 16 taps, one after each front
+//     tile of sub-range k+1 (P stays resident: the phi of a sub-range have an
+//     LDS buffer of their own); the last sub-range's FIR runs at the end;
+//   * the first sub-range of a segment that is not the channel's first needs
+//     the state at the END of the previous segment. Instead of waiting for it,
+//     the segment hands that sub-range's 1024 phi to its predecessor (agent-
+//     scope sc1 stores + a flag, published after its first 8 tiles), and the
+//     predecessor, which ends holding exactly that state and the last 128 IIR
+//     outputs, runs the sub-range's IIR and FIR after its own. It reads the phi
+//     long after they were published, so its wait is a formality; no wave ever
+//     waits for another's end. The segment itself starts sub-range 1 from the
+//     zero-state end state and zero-state last 128 outputs of sub-range 0
+//     (exact to f32 when ||A^896|| is negligible: the host checks it).
+namespace sg2 {
+using Y = sg::Y;  // L 1024, NH 512, CH 8
+constexpr int L = Y::L, NH = Y::NH, CH = Y::CH;
+
+// LpCascade states of one sub-range from its exact entering state s_in, with no
+// per-lane transition matrices (those are vector loads, which would queue behind
+// the in-flight tile prefetch): s_in is folded into lane 0 of half A's
+// Kogge-Stone scan, half A's end state into lane 0 of half B's. xs = the lane's
+// two chunks (half A, half B); ef = the state entering each (.x A, .y B), f32;
+// end = the state after the sub-range (f64, wave-uniform).
+__device__ __forceinline__ void scan_states(const WbfmFusedConst& Bc, const float* __restrict__ Phi, int l,
+                                            const double (&s_in)[4], f2 (&xs)[CH], f2 (&ef)[4],
+                                            double (&end)[4]) {
+#pragma unroll
+  for (int i = 0; i < CH; i += 4) {
+    const f4 u = *reinterpret_cast<const f4*>(Phi + CH * l + i);
+    const f4 w = *reinterpret_cast<const f4*>(Phi + NH + CH * l + i);
+    xs[i] = f2{u.x, w.x};
+    xs[i + 1] = f2{u.y, w.y};
+    xs[i + 2] = f2{u.z, w.z};
+    xs[i + 3] = f2{u.w, w.w};
+  }
+  wave_lds_fence();
+  const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
+  f2 s[4] = {f2{0, 0}, f2{0, 0}, f2{0, 0}, f2{0, 0}};
+#pragma unroll
+  for (int i = 0; i < CH; ++i) (void)bq.lp4(s, xs[i]);
+  double qa[4], qb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    qa[k] = s[k].x;
+    qb[k] = s[k].y;
+  }
+  if (l == 0) matvec_acc<4>(Bc.pw, s_in, qa);  // pw[0] = A^CH
+  wave_scan_inclusive<4>(qa, Bc.pw, l);
+  double sb[4];  // the state at the end of half A
+#pragma unroll
+  for (int k = 0; k < 4; ++k) sb[k] = sg::uni(__shfl(qa[k], 63, 64));
+  if (l == 0) matvec_acc<4>(Bc.pw, sb, qb);
+  wave_scan_inclusive<4>(qb, Bc.pw, l);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    end[k] = sg::uni(__shfl(qb[k], 63, 64));
+    const double ea = __shfl_up(qa[k], 1, 64), eb = __shfl_up(qb[k], 1, 64);
+    ef[k] = f2{static_cast<float>(l == 0 ? s_in[k] : ea), static_cast<float>(l == 0 ? sb[k] : eb)};
+  }
+}
+
+// Zero-state pass of a segment's first sub-range: its zero-state end state sw
+// and zero-state last 128 outputs hist (f[L - 128 + l + 64 r]); tmp: 128 floats
+// of free LDS.
+__device__ __forceinline__ void zs_first(const WbfmFusedConst& Bc, const float* Phi, float* tmp, int l,
+                                         double (&sw)[4], float (&hist)[2]) {
+  constexpr int TL = 64 - fu::PB / CH;  // lanes whose half-B chunk lies in the last 128
+  const double zero[4] = {0, 0, 0, 0};
+  f2 xs[CH], ef[4];
+  scan_states(Bc, Phi, l, zero, xs, ef, sw);
+  const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const f2 f = bq.lp4(ef, xs[i]);
+    if (l >= TL) tmp[(l - TL) * CH + i] = f.y;
+  }
+  wave_lds_fence();
+  hist[0] = tmp[l];
+  hist[1] = tmp[l + 64];
+  wave_lds_fence();
+}
+
+// IIR of one sub-range [0, Lr) from its exact entering state sw and FIR history
+// hist (f[-128 + l + 64 r]): the reference recurrence -> P[j] = (f[j], f[j + NH])
+// for j in [-128, NH). Returns the state after f[Lr - 1] in sw and
+// f[Lr - 128 + l + 64 r] in hist. chan_last: also the carried IIR state and FIR
+// history of the next call.
+__device__ __forceinline__ void iir(const WbfmArgs& a, const WbfmFusedConst& Bc, int ch, int Lr, bool chan_last,
+                                    const float* Phi, f2* P, int l, double (&sw)[4], float (&hist)[2]) {
+  f2 xs[CH], ef[4];
+  double end[4];
+  scan_states(Bc, Phi, l, sw, xs, ef, end);
+  const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
+  const int jl = Lr - 1;
+  const int hl = jl < NH ? jl / CH : (jl - NH) / CH;  // the lane that computes f[jl]
+  float cap[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int j = CH * l + i;
+    const f2 f = bq.lp4(ef, xs[i]);
+    P[Y::pslot(j + fu::PB)] = f;
+    if (j == jl) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cap[k] = ef[k].x;
+    }
+    if (j + NH == jl) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cap[k] = ef[k].y;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    sw[k] = static_cast<double>(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(cap[k]), hl)));
+  if (chan_last && l == 0) {
+    float* co = a.carry_out + ch * kWbfmCarry;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) co[k] = static_cast<float>(sw[k]);
+  }
+  wave_lds_fence();
+#pragma unroll
+  for (int r2 = 0; r2 < 2; ++r2) {  // pairs j in [-128, 0): (history, f[j + NH])
+    const int t = l + 64 * r2;
+    P[Y::pslot(t)] = f2{hist[r2], P[Y::pslot(t + NH)].x};
+  }
+  wave_lds_fence();
+#pragma unroll
+  for (int r2 = 0; r2 < 2; ++r2) {  // this sub-range's last 128 outputs: the next one's history
+    const int t = l + 64 * r2;
+    const int j = Lr - 128 + t;  // >= -128
+    hist[r2] = j < NH ? P[Y::pslot(j + fu::PB)].x : P[Y::pslot(j - NH + fu::PB)].y;
+    if (chan_last) a.carry_out[ch * kWbfmCarry + 8 + t] = hist[r2];
+  }
+}
+
+// Audio FIR (fir.rs:57-66) taps 16 kb .. 16 kb + 15 of the sub-range in P, both
+// halves at once (pairs): lane l owns outputs j = CH l + i and j + NH.
+__device__ __forceinline__ void fir_block(const WbfmFusedConst& Bc, const f2* __restrict__ P, int l, int kb,
+                                          f2 (&acc)[CH]) {
+  // tap k = 16 kb + kk of output i reads pair e = CH l + i - k + PB = CH (l - 16kb/CH) + 113 + m,
+  // m = i + 15 - kk; slot = e + e / CH
+  const f2* __restrict__ Pl = P + (CH + 1) * (l - 16 * kb / CH) + 113;
+  f2 w[CH + 15];
+#pragma unroll
+  for (int m = 0; m < CH + 15; ++m) w[m] = Pl[m + (113 + m) / CH];
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    const f2 tap = splat2(Bc.a[16 * kb + kk]);
+#pragma unroll
+    for (int i = 0; i < CH; ++i) acc[i] = fma2(tap, w[i + 15 - kk], acc[i]);
+  }
+}
+
+__device__ __forceinline__ void fir_store(const WbfmArgs& a, int ch, long long A0, int Lr, int l, f2 (&acc)[CH]) {
+  float* __restrict__ y = a.y + ch * a.y_stride + A0;
+  if (Lr == L && (reinterpret_cast<uintptr_t>(y) & 15) == 0) {
+    float4* ya = reinterpret_cast<float4*>(y + CH * l);
+    float4* yb = reinterpret_cast<float4*>(y + NH + CH * l);
+#pragma unroll
+    for (int i = 0; i < CH; i += 4) {
+      ya[i / 4] = float4{acc[i].x, acc[i + 1].x, acc[i + 2].x, acc[i + 3].x};
+      yb[i / 4] = float4{acc[i].y, acc[i + 1].y, acc[i + 2].y, acc[i + 3].y};
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int j = CH * l + i;
+      if (j < Lr) y[j] = acc[i].x;
+      if (j + NH < Lr) y[j + NH] = acc[i].y;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < CH; ++i) acc[i] = f2{0.0f, 0.0f};
+}
+}  // namespace sg2
+
+template <bool A16, bool CLAMP>
+__global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const WbfmFrontConst C,
+                                                     const WbfmFusedConst Bc, int spc, int S) {
+  using G = fu::G;
+  constexpr int TW = G::TW;
+  __shared__ __attribute__((aligned(16))) f2 U[G::LDS_F2];
+  __shared__ __attribute__((aligned(16))) float Phi[sg2::L];
+  __shared__ __attribute__((aligned(16))) f2 P[sg2::Y::PSlots];
+  __shared__ __attribute__((aligned(16))) float Gt[128];
+  const int l = threadIdx.x & 63;
+  Gt[l] = C.g[l];
+  Gt[l + 64] = C.g[l + 64];
+  FuRange g;
+  g.r = blockIdx.x;
+  g.ch = g.r / spc;
+  g.wl = g.r - g.ch * spc;
+  g.A = static_cast<long long>(g.wl) * S;
+  g.B = min(g.A + S, a.n_dec);
+  g.Lr = static_cast<int>(g.B - g.A);
+  g.first = g.wl == 0;
+  g.last = g.B == a.n_dec;
+  const int nsub = (g.Lr + sg2::L - 1) / sg2::L;
+  const int ntiles = nsub * sg::NS;
+  const bool late = blockIdx.x >= (gridDim.x >> 1);
+  fu::trace(a, g.r, 0);
+
+  // ---- front setup (as fu_front_range) ----
+  const FuPrefetch org = fu_origin(a, g);
+  f2 va[G::KL][2], vb[G::KL][2];
+  front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, l, va);
+  front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, l, vb);
+  const f2* __restrict__ tabc = a.tab + static_cast<long long>(g.ch) * kWbfmNS;
+  const f2* __restrict__ xc = a.x + g.ch * a.x_stride;
+  const f2* __restrict__ hc = a.hist_in + g.ch * kWbfmHist;
+  const f2 cn = tabc[G::NEW];
+  const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
+  const FuTile T{a, C, U, Phi, Gt, xc, hc, tabc, g.ch, l, c0 * G::LR + (8 * Q + 2 * l + c0) / 8,
+                 c1 * G::LR + (8 * Q + 2 * l + 1 + c1) / 8, f2{cn.x, -cn.y}, g.first};
+  long long porg = org.porg;
+  {  // halo rows of the first tile (clamped here, exact via the boundary fixup)
+    const long long P0 = porg + 2 * l;
+    const long long hi = (org.nl & ~1LL) - 2;
+    const long long Pc = P0 < 0 ? 0 : (P0 > hi ? hi : P0);
+    const f2 x0 = org.xl[Pc], x1 = org.xl[Pc + 1];
+    const f4 th = *reinterpret_cast<const f4*>(tabc + 2 * l);
+    U[c0 * G::LR + (2 * l + c0) / 8] = cmul_rot(x0, f2{th.x, th.y});
+    U[c1 * G::LR + (2 * l + 1 + c1) / 8] = cmul_rot(x1, f2{th.z, th.w});
+  }
+  {  // p = -l (row c = l, i = 0), l = 1..7: used only by d[A-1]
+    const long long Pm = max(porg - (l & 7), 0LL);
+    const f2 xm = xc[Pm];
+    const f2 tc = tabc[l & 7];
+    if (!g.first && l >= 1 && l < 8) U[l * G::LR] = cmul_rot(xm, f2{tc.x, -tc.y});
+  }
+  f2 tb0, tb1;  // e^{j theta (8Q + 2l + r)}
+  {
+    const f4 tv = *reinterpret_cast<const f4*>(tabc + 8 * Q + 2 * l);
+    tb0 = f2{tv.x, tv.y};
+    tb1 = f2{tv.z, tv.w};
+  }
+  f2 Sv = f2{0, 0};
+  f2 carry = f2{0.0f, 0.0f}, dA = f2{0, 0};
+  double sw[4] = {0, 0, 0, 0};  // IIR state entering the next sub-range
+  float hist[2] = {0, 0};       // its FIR history
+  if (g.first) {  // the carried state of the previous call (fm.rs:29 on reset)
+    const float* __restrict__ ci = a.carry_in + g.ch * kWbfmCarry;
+    carry = f2{ci[4], ci[5]};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sw[k] = ci[k];
+    hist[0] = ci[8 + l];
+    hist[1] = ci[8 + 64 + l];
+  }
+  const FuPrefetch dummy{org.xl, org.nl, -8LL * Q, true};  // past the segment: an L2-resident tile
+  f2 acc[sg2::CH];
+#pragma unroll
+  for (int i = 0; i < sg2::CH; ++i) acc[i] = f2{0.0f, 0.0f};
+  bool pend = false;  // a sub-range's FIR spread over this sub-range's tiles
+  long long pA0 = 0;
+  int pLr = 0;
+
+#pragma unroll 1
+  for (int sub = 0, n = 0; sub < nsub; ++sub) {
+    f2 ph[G::KL][2];  // per-lane staging phasors, rebuilt per sub-range (dead during the IIR)
+    {                 // from tb (registers) and uniform e^{j theta 128 k} (scalar loads)
+#pragma unroll
+      for (int k = 0; k < G::KL; ++k) {
+        const f2 ek = tabc[128 * k];
+        ph[k][0] = cmul(tb0, ek);
+        ph[k][1] = cmul(tb1, ek);
+      }
+    }
+#pragma unroll 1
+    for (int tin = 0; tin < sg::NS; tin += 2, n += 2, porg += 2 * G::NEW) {
+      if (kSegPrio) {  // see k_wbfm_seg
+        if ((16 * n < kSegPrioQ16 * ntiles) == late) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+      if ((n & 63) == 0)  // lane l: the common phasor of tile n + l
+        Sv = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1 + static_cast<long long>(l) * G::NEW),
+                        a.step[g.ch]);
+      const long long jd0 = g.A + static_cast<long long>(n) * TW;
+      const FuPrefetch p0 = n + 2 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 2 * G::NEW, true} : dummy;
+      const FuPrefetch p1 = n + 3 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 3 * G::NEW, true} : dummy;
+      fu_tile<A16, CLAMP>(T, n, porg, jd0, ph, va, p0, Sv, carry, dA, Phi + TW * tin, n & 63);
+      if (pend && !(ORION_SEG_ABL & 8)) sg2::fir_block(Bc, P, l, tin, acc);
+      fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + TW, ph, vb, p1, Sv, carry, dA, Phi + TW * (tin + 1),
+                          (n + 1) & 63);
+      if (pend && !(ORION_SEG_ABL & 8)) sg2::fir_block(Bc, P, l, tin + 1, acc);
+    }
+    if (pend) {
+      sg2::fir_store(a, g.ch, pA0, pLr, l, acc);
+      pend = false;
+    }
+    const long long A0 = g.A + static_cast<long long>(sub) * sg2::L;
+    const int Lr = static_cast<int>(min(static_cast<long long>(sg2::L), g.B - A0));
+    if (sub == 0 && !g.first) {
+      // zero-state pass only; the phi go to the predecessor, which has the true state
+      sg2::zs_first(Bc, Phi, reinterpret_cast<float*>(P), l, sw, hist);
+      uint32_t* slot = a.hand + static_cast<long long>(g.r) * sg2::L;
+#pragma unroll
+      for (int i = 0; i < sg2::L / 64; ++i) fu::st_agent(slot + l + 64 * i, __float_as_uint(Phi[l + 64 * i]));
+      fu::publish(a.flags + 3LL * g.r, a.epoch, l);
+    } else if (!(ORION_SEG_ABL & 1)) {
+      sg2::iir(a, Bc, g.ch, Lr, g.last && sub == nsub - 1, Phi, P, l, sw, hist);
+      pend = true;
+      pA0 = A0;
+      pLr = Lr;
+    }
+  }
+  fu::trace(a, g.r, 1);
+  if (pend) {
+#pragma unroll 1
+    for (int kb = 0; kb < 8; ++kb) sg2::fir_block(Bc, P, l, kb, acc);
+    sg2::fir_store(a, g.ch, pA0, pLr, l, acc);
+  }
+  if (!g.last && !(ORION_SEG_ABL & 4)) {  // the successor segment's first sub-range
+    const long long As = g.B, Bs = min(As + S, a.n_dec);
+    const int Lrs = static_cast<int>(min(static_cast<long long>(sg2::L), Bs - As));
+    const bool s_last = Bs == a.n_dec && Bs - As <= sg2::L;
+    fu::wait_for(a.flags + 3LL * (g.r + 1), a.epoch, a.err);
+    fu::trace(a, g.r, 2);
+    const uint32_t* slot = a.hand + static_cast<long long>(g.r + 1) * sg2::L;
+#pragma unroll
+    for (int i = 0; i < sg2::L / 64; ++i) Phi[l + 64 * i] = __uint_as_float(fu::ld_agent(slot + l + 64 * i));
+    wave_lds_fence();
+    sg2::iir(a, Bc, g.ch, Lrs, s_last, Phi, P, l, sw, hist);
+#pragma unroll 1
+    for (int kb = 0; kb < 8; ++kb) sg2::fir_block(Bc, P, l, kb, acc);
+    sg2::fir_store(a, g.ch, As, Lrs, l, acc);
+  }
+  fu::trace(a, g.r, 3);
+}
+
 // Role-split form: a workgroup of two waves walks ranges r = blockIdx.x + k G.
 // Wave 0 (front) streams range k into Phi[k & 1] (prefetching the next range's
 // first tiles across the boundary, so the input stream never pauses); wave 1
@@ -2158,20 +2494,21 @@ long long wbfm_seg_slots(long long n_dec, int nch) {
 // One round: as many segments as resident waves (per channel: the channel's share,
 // at least one sub-range per segment), each a whole number of sub-ranges.
 void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
-                     hipStream_t s) {
-  static_assert(sg::L == kSgL, "sub-range geometry");
+                     int max_segments, bool spread, hipStream_t s) {
+  static_assert(sg::L == kSgL && sg2::L == kSgL, "sub-range geometry");
   if (a.n_dec <= 0 || nch <= 0) return;
   static int cap = 0;
   if (cap == 0) {
     int per_cu = 0, dev = 0, ncu = 0;
-    ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_seg<true, false>, 64, 0));
+    ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_seg2<true, false>, 64, 0));
     ORION_HIP(hipGetDevice(&dev));
     ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     cap = std::max(1, per_cu) * std::max(1, ncu);
-    if (const char* e = std::getenv("ORION_WBFM_SEGCAP")) cap = std::max(1, std::atoi(e));  // experiments
   }
+  const long long capx = max_segments > 0 ? max_segments : cap;
   const long long nsub_ch = (a.n_dec + kSgL - 1) / kSgL;
-  long long spc = std::max<long long>(1, std::min<long long>((cap + nch - 1) / nch, nsub_ch));
+  // at most the resident capacity (k_wbfm_seg2's end waits on a later segment)
+  long long spc = std::max<long long>(1, std::min<long long>(capx / nch, nsub_ch));
   const long long S = (nsub_ch + spc - 1) / spc * kSgL;
   spc = (a.n_dec + S - 1) / S;
   const long long grid = spc * nch;
@@ -2179,13 +2516,16 @@ void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFused
   const bool a16 = (reinterpret_cast<uintptr_t>(a.x) % 16 == 0) && (a.x_stride % 2 == 0);
   const bool clamp = a.n < 2LL * Fw<2>::NEW;
   const int gi = static_cast<int>(grid), sp = static_cast<int>(spc), Si = static_cast<int>(S);
-  if (clamp) {
-    if (a16) k_wbfm_seg<true, true><<<gi, 64, 0, s>>>(a, f, b, sp, Si);
-    else k_wbfm_seg<false, true><<<gi, 64, 0, s>>>(a, f, b, sp, Si);
-  } else {
-    if (a16) k_wbfm_seg<true, false><<<gi, 64, 0, s>>>(a, f, b, sp, Si);
-    else k_wbfm_seg<false, false><<<gi, 64, 0, s>>>(a, f, b, sp, Si);
+#define ORION_SEG(K)                                                   \
+  if (clamp) {                                                         \
+    if (a16) K<true, true><<<gi, 64, 0, s>>>(a, f, b, sp, Si);         \
+    else K<false, true><<<gi, 64, 0, s>>>(a, f, b, sp, Si);            \
+  } else {                                                             \
+    if (a16) K<true, false><<<gi, 64, 0, s>>>(a, f, b, sp, Si);        \
+    else K<false, false><<<gi, 64, 0, s>>>(a, f, b, sp, Si);           \
   }
+  if (spread) { ORION_SEG(k_wbfm_seg2) } else { ORION_SEG(k_wbfm_seg) }
+#undef ORION_SEG
   ORION_LAUNCH_CHECK();
 }
 

@@ -123,8 +123,12 @@ long long wbfm_fused_slots(long long n_dec, int nch);
 // waves. Requires ||A^(kSgL - 128)|| negligible (the block checks it).
 constexpr int kSgL = 1024;                           // outputs per sub-range
 constexpr int kSgC = kSgL / 128;                     // IIR samples per lane and half (8)
+constexpr int kSg2Slot = kSgL;                       // u32 words per k_wbfm_seg2 hand-off slot (phi)
 long long wbfm_seg_slots(long long n_dec, int nch);
-void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch, hipStream_t s);
+// spread: k_wbfm_seg2 (FIR spread over the next sub-range's tiles, first sub-range
+// handed to the predecessor); else k_wbfm_seg. max_segments > 0 caps the waves.
+void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
+                     int max_segments, bool spread, hipStream_t s);
 void launch_wbfm_fused(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
                        hipStream_t s);
 

@@ -85,6 +85,7 @@ def _load():
         "orion_cw_envelope_demod_set_gain": (i, [vp, f]),
         "orion_wbfm_chain_new": (vp, [C.POINTER(WbfmParams)]),
         "orion_wbfm_chain_batch_new": (vp, [C.POINTER(WbfmParams), fp, sz]),
+        "orion_wbfm_chain_configure": (i, [vp, i, i]),
         "orion_block_process": (i, [vp, vp, sz, vp, sz, C.POINTER(WorkReport)]),
         "orion_block_process_device": (i, [vp, vp, sz, vp, sz, vp, C.POINTER(WorkReport)]),
         "orion_block_reset": (i, [vp]), "orion_block_free": (None, [vp]),
@@ -350,6 +351,14 @@ class WbfmChain(_Block):
             offs = np.ascontiguousarray(offs)
             h = _L.orion_wbfm_chain_batch_new(C.byref(p), _fptr(offs), offs.size)
         super().__init__(h)
+
+    _PATHS = {"auto": 0, "segmented": 1, "ranges": 2, "split": 3, "segmented_v1": 4}
+
+    def configure(self, path: str = "auto", max_segments: int = 0):
+        """Engine tuning / tests (no reference counterpart): the kernel path and a
+        cap on the segmented kernel's waves (include/orion_sdr_amd.h)."""
+        _check(_L.orion_wbfm_chain_configure(self._h, self._PATHS[path], int(max_segments)))
+        return self
 
 
 # ---- designs (host) ----------------------------------------------------------

@@ -273,6 +273,42 @@ def test_wbfm_full_size_windowed(gpu_lib, oracle):
         report(f"wbfm 2^26 window@{start} nrmse", nrmse(g, ref), 1e-5)
 
 
+@pytest.mark.parametrize("path,max_seg,n", [
+    ("segmented", 3, 1 << 20),      # 3 segments of 43 sub-ranges (> 64 tiles: phasor refresh)
+    ("segmented", 1, 600_000),      # one segment, ragged last sub-range
+    ("segmented", 7, 4097 * 8 + 5),  # one sub-range per segment, 2-output last segment
+    ("segmented", 2, 8 * 1024 + 8),  # second segment of one output
+    ("segmented_v1", 3, 1 << 20),
+    ("ranges", 0, 1 << 20),
+    ("split", 0, 1 << 20)])
+def test_wbfm_kernel_paths(gpu_lib, oracle, path, max_seg, n):
+    """Every WBFM kernel path and segment geometry against the oracle."""
+    x = wbfm_input(n)
+    got = gpu_lib.WbfmChain().configure(path, max_seg).process(x)
+    report(f"wbfm path={path} max_segments={max_seg} n={n} nrmse", nrmse(got, oracle.wbfm(x)), 1e-5)
+
+
+@pytest.mark.parametrize("max_seg", [2, 5])
+def test_wbfm_segmented_streaming_and_channels(gpu_lib, oracle, max_seg):
+    """Carried state across calls and independent channels with several
+    multi-sub-range segments per channel."""
+    x = wbfm_input(700_000)
+    for chunk in (300_003, 131_072):
+        got = stream(gpu_lib.WbfmChain().configure("segmented", max_seg), x, chunk)
+        report(f"wbfm segmented max_segments={max_seg} chunk={chunk} nrmse", nrmse(got, oracle.wbfm(x, chunk=chunk)), 1e-5)
+    offs = np.array([1.5e6, -2.2e6, 0.7e6], np.float32)
+    xc = np.stack([wbfm_input(1 << 18, f_off=float(f), seed=0x55 ^ c) for c, f in enumerate(offs)])
+    got = gpu_lib.WbfmChain(f_off=offs).configure("segmented", 3 * max_seg).process(xc)
+    report(f"wbfm segmented 3 ch max_segments={3 * max_seg} nrmse", nrmse(got, oracle.wbfm_channels(xc, offs, 3)), 1e-5)
+
+
+def test_wbfm_configure_errors(gpu_lib):
+    with pytest.raises(gpu_lib.OrionError):
+        gpu_lib.WbfmChain().configure("segmented", -1)
+    fm = gpu_lib.FmQuadratureDemod(48e3, 2500, 5000)
+    assert gpu_lib._L.orion_wbfm_chain_configure(fm._h, 0, 0) == -4  # ORION_E_TYPE: not a WBFM chain
+
+
 # ---- Python API contract (python/tests/test_unit.py:37-127) ----------------------------
 def test_api_validation(gpu_lib):
     N = 4096
