@@ -6,22 +6,31 @@
 //   -> FmQuadratureDemod         (demodulate/fm.rs:45-77: discriminator + LpCascade)
 //   -> FirLowpass                (dsp/fir.rs:47-66, the audio filter).
 //
-// k_wbfm_front — persistent: 4 workgroups (256 lanes) per CU, each streaming a
-//   contiguous range of tiles (one XCD owns one contiguous eighth, so the
-//   120-sample halo a tile shares with its neighbour is an L2 hit). Per tile of
-//   512 decimated outputs: the 4224 cf32 inputs were prefetched into registers
-//   (16-B loads) during the previous tile; they are NCO-mixed with a per-position
-//   phasor table (registers) and scattered into the polyphase LDS image, the
-//   next tile's loads are issued, and the polyphase FIR runs at the kept outputs
-//   (two per lane, packed FMA, taps from SGPRs). The tile's common phasor factor
-//   multiplies the 512 decimated outputs; the discriminator (atan2_approx op for
-//   op) produces 511 phi values (tiles overlap by one decimated sample).
-// k_wbfm_back — one workgroup per 4096 audio outputs: LpCascade over phi by a
-//   state-carry scan (19 samples per lane, f64 Kogge-Stone + cross-wave carry,
-//   re-run with the reference's f32 TDF-II update), started 768 samples early
-//   from a zero state (pole radius 0.953: the transient is < 1e-8 of the state
-//   after 641 samples); then the 125-tap audio FIR, register-blocked and packed.
-// The first tile / workgroup of each channel starts from the exact state carried
+// Building blocks (one 64-lane wave each, no workgroup barriers):
+//   front tile (fu_tile)  — 1024 cf32 inputs -> 128 decimated outputs: the tile's
+//     inputs were prefetched two tiles ahead (16-B nontemporal loads into
+//     registers), are NCO-mixed with per-lane phasors and scattered into an
+//     8-row polyphase LDS image (17-column halo carried from the previous tile),
+//     the 127-tap polyphase FIR runs at the kept outputs (two per lane, packed
+//     FMA, taps from SGPRs), the tile's common phasor multiplies them, and the
+//     discriminator (atan2_approx op for op) writes 128 phi.
+//   sub-range IIR — LpCascade over 1024 phi: a zero-state packed pass over two
+//     halves, f64 Kogge-Stone scans, then the reference's f32 TDF-II recurrence
+//     -> the audio FIR's pair image (f[j], f[j+512]); audio FIR = 125 taps in
+//     8 blocks of 16, one v_pk_fma_f32 per tap for both halves.
+// Kernels:
+//   k_wbfm_seg2  (default) — one round of waves; each walks a segment of
+//     1024-output sub-ranges, the IIR between tiles and the audio FIR spread
+//     over the next sub-range's tiles; a segment's first sub-range is handed to
+//     its predecessor (see the comment at the kernel).
+//   k_wbfm_seg   — the same segments with each sub-range's whole back run at
+//     once and the first sub-range deferred to the end (ORION_WBFM_SEGMENTED_V1).
+//   k_wbfm_fused — one wave per 2048-output range, two rounds of waves, zero-
+//     state IIR hand-off between neighbouring ranges (ORION_WBFM_RANGES).
+//   k_wbfm_front2 + k_wbfm_back — the two-kernel path (phi through HBM, a
+//     510-sample IIR warm-up per 2048 outputs): any IIR design, used when the
+//     LpCascade decays too slowly for the hand-offs above (ORION_WBFM_SPLIT).
+// The first tile / sub-range of each channel starts from the exact state carried
 // from the previous call (last decimated sample, 128 raw inputs, IIR state, last
 // 128 IIR outputs), so k calls equal one call on the concatenation.
 #include <algorithm>
@@ -48,169 +57,6 @@ static_assert(2 * NT * (KP - 1) + 2 * NT - 1 >= PW::NS - 1, "staging coverage");
 // the loads stay in flight (a branchy prefetch makes the compiler merge register
 // copies behind an s_waitcnt vmcnt(0)). Tiles that reach before x[0] or past
 // x[n-1] are re-loaded exactly (history / zero padding) at staging time.
-template <bool A16>
-__device__ __forceinline__ void front_load(const WbfmArgs& a, int ch, long long porg, int t,
-                                           f2 (&v)[KP][2]) {
-  const bool tiny = a.n < 2;  // nothing safe to clamp into: read the history buffer
-  const f2* __restrict__ x = tiny ? a.hist_in : a.x + ch * a.x_stride;
-  const long long hi = (tiny ? kWbfmHist : (a.n & ~1LL)) - 2;
-#pragma unroll
-  for (int k = 0; k < KP; ++k) {
-    const int p = 2 * t + 2 * NT * k;
-    if (p < PW::NS) {
-      long long P = porg + p;
-      P = P < 0 ? 0 : (P > hi ? hi : P);
-      if constexpr (A16) {
-        const f4 w = *reinterpret_cast<const f4*>(x + P);
-        v[k][0] = f2{w.x, w.y};
-        v[k][1] = f2{w.z, w.w};
-      } else {
-        v[k][0] = x[P];
-        v[k][1] = x[P + 1];
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ bool front_boundary(const WbfmArgs& a, long long porg) {
-  return porg < 0 || porg + PW::NS > a.n;
-}
-
-// ABL (timing ablations, never used by the product path; outputs are wrong):
-//   1 no global input loads, 2 no polyphase FIR, 4 no NCO mix, 8 no discriminator,
-//   16 no audio FIR, 32 no LpCascade scan, 64 skip the back kernel.
-template <bool A16, int ABL>
-__global__ __launch_bounds__(NT, 4) void k_wbfm_front(const WbfmArgs a, const WbfmFrontConst C,
-                                                      int tiles_per_ch, int nch) {
-  __shared__ __attribute__((aligned(16))) f2 U[PW::LDS_F2];
-  __shared__ __attribute__((aligned(16))) f2 D[T];
-  const int t = threadIdx.x;
-  // Tile range of this workgroup: XCD (blockIdx % 8) owns a contiguous eighth of
-  // the (channel, tile) space; its G/8 workgroups interleave through it.
-  const int total = tiles_per_ch * nch;
-  const int g8 = gridDim.x >> 3;
-  const int per = (total + 7) >> 3;
-  const int lo = (blockIdx.x & 7) * per;
-  const int hi = min(lo + per, total);
-  // Staging slots of this thread: p = 2t + 512k, p+1; the phase c is the same
-  // for every k (512 = 0 mod 8), so slot(p + 512k) = slot(p) + 64k.
-  const int s0 = PW::slot(2 * t), s1 = PW::slot(2 * t + 1);
-
-  f2 v[KP][2];
-  f2 tb0 = f2{1.0f, 0.0f}, tb1 = f2{1.0f, 0.0f};  // e^{j theta 2t}, e^{j theta (2t+1)}
-  const f2* __restrict__ tabc = a.tab;
-  uint64_t step = 0;
-  f2 cprev = f2{1.0f, 0.0f};
-  int cur_ch = -1;
-  int u = lo + static_cast<int>(blockIdx.x >> 3);
-  if (u < hi) {
-    const int ch = u / tiles_per_ch;
-    const long long Jd = static_cast<long long>(u - ch * tiles_per_ch) * kWbfmPhi - 1;
-    if constexpr (ABL & 1) {
-#pragma unroll
-      for (int k = 0; k < KP; ++k) v[k][0] = v[k][1] = f2{static_cast<float>(t), 1.0f};
-    } else {
-      front_load<A16>(a, ch, static_cast<long long>(M) * (Jd - Q), t, v);
-    }
-  }
-  for (; u < hi; u += g8) {
-    const int ch = u / tiles_per_ch;
-    const int b = u - ch * tiles_per_ch;
-    const long long J = static_cast<long long>(b) * kWbfmPhi;  // first phi of this tile
-    const long long Jd = J - 1;                                 // first decimated output
-    const long long porg = static_cast<long long>(M) * (Jd - Q);
-    if (ch != cur_ch) {  // per-channel constants, loaded before any prefetch is in flight
-      tabc = a.tab + static_cast<long long>(ch) * PW::NS;
-      const f4 tv = *reinterpret_cast<const f4*>(tabc + 2 * t);
-      tb0 = f2{tv.x, tv.y};
-      tb1 = f2{tv.z, tv.w};
-      step = a.step[ch];
-      const float* ci = a.carry_in + ch * kWbfmCarry;
-      cprev = f2{ci[4], ci[5]};  // d[-1]: the last decimated sample of the previous call
-      cur_ch = ch;
-    }
-    // ---- stage: NCO mix, polyphase scatter ----
-    // e^{j theta (2t + 512k)} = e^{j theta 2t} * e^{j theta 512k}; the second
-    // factor is uniform (scalar loads of tab[512k]). A boundary tile (before x[0]
-    // or past x[n-1]) replaces the clamped prefetch by the exact samples.
-    const bool bnd = front_boundary(a, porg);
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      const int p = 2 * t + 2 * NT * k;
-      if (p < PW::NS) {
-        f2 x0 = v[k][0], x1 = v[k][1];
-        if (bnd) {
-          const f2* __restrict__ xc = a.x + ch * a.x_stride;
-          const f2* __restrict__ hc = a.hist_in + ch * kWbfmHist;
-          x0 = load_hist(xc, a.n, hc, kWbfmHist, porg + p);
-          x1 = load_hist(xc, a.n, hc, kWbfmHist, porg + p + 1);
-        }
-        if constexpr (ABL & 4) {
-          U[s0 + 64 * k] = x0;
-          U[s1 + 64 * k] = x1;
-        } else {
-          const f2 ek = tabc[2 * NT * k];
-          U[s0 + 64 * k] = cmul_rot(x0, cmul(tb0, ek));
-          U[s1 + 64 * k] = cmul_rot(x1, cmul(tb1, ek));
-        }
-      }
-    }
-    // ---- prefetch the next tile (lands during this tile's compute) ----
-    {
-      const int un = u + g8;
-      if (un < hi) {
-        const int chn = un / tiles_per_ch;
-        const long long Jdn = static_cast<long long>(un - chn * tiles_per_ch) * kWbfmPhi - 1;
-        if constexpr (!(ABL & 1)) front_load<A16>(a, chn, static_cast<long long>(M) * (Jdn - Q), t, v);
-      }
-    }
-    lds_barrier();  // LDS-only: the prefetch stays in flight
-
-    // ---- polyphase FIR at the kept outputs; common phasor of the tile ----
-    {
-      f2 acc[PW::R];
-      if constexpr (ABL & 2) {
-        acc[0] = U[PW::R * t];
-        acc[1] = U[PW::R * t + 1];
-      } else {
-        PW::compute(U, t, [&](int c, int q) { return C.g[c * Q + q]; }, acc);
-      }
-      const f2 S = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1), step);
-      D[2 * t] = cmul(acc[0], S);
-      D[2 * t + 1] = cmul(acc[1], S);
-      if (b == 0 && t == 0) D[0] = cprev;
-    }
-    lds_barrier();
-
-    // ---- FM discriminator (fm.rs:60-68) ----
-    float* __restrict__ phi = a.phi + ch * a.phi_stride;
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int i = 2 * t + r;
-      const long long j = J + i;
-      if constexpr (ABL & 8) {
-        if (i < kWbfmPhi && j < a.n_dec) phi[j] = D[i + 1].x + D[i].y;
-      } else {
-        if (i < kWbfmPhi && j < a.n_dec) phi[j] = fm_disc(D[i + 1], D[i], C.k);
-      }
-    }
-    // ---- carried state: last decimated sample and raw history ----
-    if (J <= a.n_dec - 1 && a.n_dec - 1 < J + kWbfmPhi) {
-      float* co = a.carry_out + ch * kWbfmCarry;
-      if (t == 0) {
-        const f2 last = D[a.n_dec - 1 - Jd];
-        co[4] = last.x;
-        co[5] = last.y;
-        co[6] = 0.0f;
-        co[7] = 0.0f;
-      }
-      if (t < kWbfmHist)
-        a.hist_out[ch * kWbfmHist + t] =
-            load_hist(a.x + ch * a.x_stride, a.n, a.hist_in + ch * kWbfmHist, kWbfmHist, a.n - kWbfmHist + t);
-    }
-  }
-}
-
 // ---- front, wave-independent form ----------------------------------------------
 // One wave per workgroup and no s_barrier anywhere: every LDS hand-off is inside
 // one wave (DS operations of a wave complete in order; wave_lds_fence keeps the
@@ -319,61 +165,6 @@ __device__ __forceinline__ void front2_decim(const f2* __restrict__ U, int l, co
     float t[Q];
     front2_window<R>(U, l, c, w);
     front2_taps(g, c, t);
-    front2_phase<R>(w, t, d);
-  }
-}
-
-// The same FIR software-pipelined over the phases: phase c+1's window reads and
-// tap loads are issued before phase c's FMAs, so their latency (and the full
-// lgkmcnt drain a scalar tap load forces) overlaps a phase of arithmetic. Same
-// summation order as front2_decim (bit-identical).
-template <int R>
-__device__ __forceinline__ void front2_decim_pipe(const f2* __restrict__ U, int l, const float* __restrict__ g,
-                                                  f2 (&d)[R]) {
-#pragma unroll
-  for (int r = 0; r < R; ++r) d[r] = f2{0.0f, 0.0f};
-  f4 wa[Fw<R>::WIN], wb[Fw<R>::WIN];
-  float ta[Q], tb[Q];
-  front2_taps(g, 0, ta);
-  front2_window<R>(U, l, 0, wa);
-#pragma unroll 1
-  for (int c = 0; c < M - 2; c += 2) {
-    front2_taps(g, c + 1, tb);
-    front2_window<R>(U, l, c + 1, wb);
-    front2_phase<R>(wa, ta, d);
-    front2_taps(g, c + 2, ta);
-    front2_window<R>(U, l, c + 2, wa);
-    front2_phase<R>(wb, tb, d);
-  }
-  front2_taps(g, M - 1, tb);
-  front2_window<R>(U, l, M - 1, wb);
-  front2_phase<R>(wa, ta, d);
-  front2_phase<R>(wb, tb, d);
-}
-
-// Same FIR with the taps in LDS (phase-major, 16 floats per phase = 4 broadcast
-// ds_read_b128): every operand wait is then an LDS wait the compiler can count
-// (scalar tap loads share lgkmcnt and force a full drain per phase), so with the
-// 8 phases unrolled the next phase's reads overlap this phase's FMAs.
-template <int R>
-__device__ __forceinline__ void front2_decim_lds(const f2* __restrict__ U, int l, const float* __restrict__ Gt,
-                                                 f2 (&d)[R]) {
-#pragma unroll
-  for (int r = 0; r < R; ++r) d[r] = f2{0.0f, 0.0f};
-#pragma unroll
-  for (int c = 0; c < M; ++c) {
-    f4 w[Fw<R>::WIN];
-    front2_window<R>(U, l, c, w);
-    const f4* tq = reinterpret_cast<const f4*>(Gt + c * Q);
-    float t[Q];
-#pragma unroll
-    for (int i = 0; i < Q / 4; ++i) {
-      const f4 v = tq[i];
-      t[4 * i] = v.x;
-      t[4 * i + 1] = v.y;
-      t[4 * i + 2] = v.z;
-      t[4 * i + 3] = v.w;
-    }
     front2_phase<R>(w, t, d);
   }
 }
@@ -932,12 +723,6 @@ struct FuPrefetch {  // where the tile two ahead starts
 #ifndef ORION_FU_ABL
 #define ORION_FU_ABL 0  // timing experiments only (separate builds): 2 no decim FIR, 4 no staging
 #endif
-#ifndef ORION_FU_PIPE
-#define ORION_FU_PIPE 0  // software-pipelined decimating FIR (front2_decim_pipe; measured slower: SGPR spills)
-#endif
-#ifndef ORION_FU_DEPTH
-#define ORION_FU_DEPTH 2  // front tiles in flight per wave (2 or 3; 3 measured no faster)
-#endif
 
 template <bool A16, bool CLAMP>
 __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, long long jd0, const f2 (&ph)[8][2],
@@ -994,10 +779,6 @@ __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, 
   if constexpr (ORION_FU_ABL & 2) {  // timing experiment: no decimating FIR
     d[0] = U[l];
     d[1] = U[l + 64];
-  } else if constexpr (ORION_FU_PIPE == 2) {
-    front2_decim_lds<R>(U, l, T.Gt, d);
-  } else if constexpr (ORION_FU_PIPE) {
-    front2_decim_pipe<R>(U, l, T.C.g, d);
   } else {
     front2_decim<R>(U, l, T.C.g, d);
   }
@@ -1145,81 +926,6 @@ __device__ __forceinline__ void fu_front_range(const WbfmArgs& a, const WbfmFron
   dlast = carry;
 }
 
-// The same front with three tiles in flight (va, vb, vc: tiles 0, 1, 2 on
-// entry). The prefetch for tile n + 3 is issued while tile n is consumed, so the
-// decimating FIR of tile n overlaps the loads of three tiles. N = 1 (mod 3): a
-// loop over groups of three, then the last four tiles peeled.
-template <int N, bool A16, bool CLAMP>
-__device__ __forceinline__ void fu_front_range3(const WbfmArgs& a, const WbfmFrontConst& C, const FuRange& g,
-                                                f2* U, float* Phi, const float* Gt, f2 (&va)[8][2], f2 (&vb)[8][2],
-                                                f2 (&vc)[8][2], f2& dA, f2& dlast) {
-  static_assert(N % 3 == 1 && N >= 4, "three-deep front: N = 1 (mod 3)");
-  using G = fu::G;
-  const int l = threadIdx.x & 63;
-  const f2* __restrict__ tabc = a.tab + static_cast<long long>(g.ch) * kWbfmNS;
-  const f2* __restrict__ xc = a.x + g.ch * a.x_stride;
-  const f2* __restrict__ hc = a.hist_in + g.ch * kWbfmHist;
-  const FuPrefetch org = fu_origin(a, g);
-  const f4 tv = *reinterpret_cast<const f4*>(tabc + 8 * Q + 2 * l);
-  const f2 tb0 = f2{tv.x, tv.y}, tb1 = f2{tv.z, tv.w};
-  f2 ph[G::KL][2];
-#pragma unroll
-  for (int k = 0; k < G::KL; ++k) {
-    const f2 ek = tabc[128 * k];
-    ph[k][0] = cmul(tb0, ek);
-    ph[k][1] = cmul(tb1, ek);
-  }
-  const f2 cn = tabc[G::NEW];
-  const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
-  const FuTile T{a, C, U, Phi, Gt, xc, hc, tabc, g.ch, l, c0 * G::LR + (8 * Q + 2 * l + c0) / 8,
-                 c1 * G::LR + (8 * Q + 2 * l + 1 + c1) / 8, f2{cn.x, -cn.y}, g.first};
-  {  // halo rows of the first tile (p = 2l, 2l+1): clamped here, exact via the boundary fixup
-    const long long P0 = org.porg + 2 * l;
-    const long long hi = (org.nl & ~1LL) - 2;
-    const long long Pc = P0 < 0 ? 0 : (P0 > hi ? hi : P0);
-    const f2 x0 = org.xl[Pc], x1 = org.xl[Pc + 1];
-    const f4 th = *reinterpret_cast<const f4*>(tabc + 2 * l);
-    U[c0 * G::LR + (2 * l + c0) / 8] = cmul_rot(x0, f2{th.x, th.y});
-    U[c1 * G::LR + (2 * l + 1 + c1) / 8] = cmul_rot(x1, f2{th.z, th.w});
-  }
-  {  // p = -l (row c = l, i = 0), l = 1..7: used only by d[A-1] (see fu_front_range)
-    const long long Pm = max(org.porg - (l & 7), 0LL);
-    const f2 xm = xc[Pm];
-    const f2 tc = tabc[l & 7];
-    if (!g.first && l >= 1 && l < 8) U[l * G::LR] = cmul_rot(xm, f2{tc.x, -tc.y});
-  }
-  const f2 Sv = phasor_q64(static_cast<uint64_t>(a.k0 + org.porg + 1 + static_cast<long long>(l) * G::NEW),
-                           a.step[g.ch]);
-  f2 carry = f2{0.0f, 0.0f};
-  if (g.first) {  // d[-1]: the last decimated sample of the previous call (fm.rs:29 on reset)
-    const float* ci = a.carry_in + g.ch * kWbfmCarry;
-    carry = f2{ci[4], ci[5]};
-  }
-  // tile m's prefetch descriptor: past the range, the channel's first tile (an
-  // L2-resident dummy; see fu_front_range)
-  auto pf = [&](int m) {
-    return m < N ? FuPrefetch{org.xl, org.nl, org.porg + static_cast<long long>(m) * G::NEW, true}
-                 : FuPrefetch{org.xl, org.nl, -8LL * Q, true};
-  };
-  auto tile = [&](int n, f2(&v)[8][2]) {
-    fu_tile<A16, CLAMP>(T, n, org.porg + static_cast<long long>(n) * G::NEW,
-                        g.A + static_cast<long long>(n) * G::TW, ph, v, pf(n + 3), Sv, carry, dA,
-                        T.Phi + G::TW * n, n);
-  };
-  int n = 0;
-#pragma unroll 1
-  for (; n < N - 4; n += 3) {
-    tile(n, va);
-    tile(n + 1, vb);
-    tile(n + 2, vc);
-  }
-  tile(n, va);
-  tile(n + 1, vb);
-  tile(n + 2, vc);
-  tile(n + 3, va);
-  dlast = carry;
-}
-
 // The back of one range (LpCascade, audio FIR) from Phi[0 .. L), with one
 // hand-off to the next range that depends on nothing but this range's phi:
 //  - the zero-state pass gives every chunk's zero-state entering state and the
@@ -1234,7 +940,7 @@ __device__ __forceinline__ void fu_front_range3(const WbfmArgs& a, const WbfmFro
 // pair-image region (may alias Phi: Phi is read into registers first).
 template <int N>
 __device__ __forceinline__ void fu_back_range(const WbfmArgs& a, const WbfmFrontConst& C, const WbfmFusedConst& Bc,
-                                              const FuRange& g, float* Phi, f2* P, int* consumed, int consumed_tag) {
+                                              const FuRange& g, float* Phi, f2* P) {
   using Y = fu::Geo<N>;
   constexpr int L = Y::L, NH = Y::NH, CH = Y::CH;
   constexpr int TL = 64 - fu::PB / CH;  // first lane whose half-B chunk lies in the last 128
@@ -1262,8 +968,6 @@ __device__ __forceinline__ void fu_back_range(const WbfmArgs& a, const WbfmFront
     xs[i + 3] = f2{u.w, w.w};
   }
   wave_lds_fence();
-  if (consumed && l == 0)  // Phi may be refilled by the front wave
-    __hip_atomic_store(consumed, consumed_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   f2 s[4] = {f2{0, 0}, f2{0, 0}, f2{0, 0}, f2{0, 0}};
 #pragma unroll
   for (int i = 0; i < CH; ++i) (void)bq.lp4(s, xs[i]);
@@ -1466,19 +1170,13 @@ __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(con
     const FuPrefetch org = fu_origin(a, g);
     front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, threadIdx.x, va);
     front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, threadIdx.x, vb);
-    if constexpr (ORION_FU_DEPTH == 3) {
-      f2 vc[G::KL][2];
-      front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + 2 * G::NEW, threadIdx.x, vc);
-      fu_front_range3<N, A16, CLAMP>(a, C, g, U, Phi, Gt, va, vb, vc, dA, dlast);
-    } else {
-      fu_front_range<N, A16, CLAMP>(a, C, g, U, Phi, Gt, va, vb, FuPrefetch{nullptr, 0, 0, false}, dA, dlast);
-    }
+    fu_front_range<N, A16, CLAMP>(a, C, g, U, Phi, Gt, va, vb, FuPrefetch{nullptr, 0, 0, false}, dA, dlast);
     fu::trace(a, g.r, 1);
     if (a.fu_abl & 1) {  // timing only: front alone (phi kept alive)
       if (Phi[threadIdx.x] == 1234.5f) a.y[threadIdx.x] = Phi[threadIdx.x];
       return;
     }
-    fu_back_range<N>(a, C, Bc, g, Phi, P, nullptr, 0);
+    fu_back_range<N>(a, C, Bc, g, Phi, P);
   } else {
     // persistent (gridDim.x <= resident capacity): ranges r = blockIdx.x + k
     // gridDim.x, each range's first two tiles prefetched across the previous
@@ -1500,7 +1198,7 @@ __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(con
         wave_lds_fence();
         continue;
       }
-      fu_back_range<N>(a, C, Bc, g, Phi, P, nullptr, 0);
+      fu_back_range<N>(a, C, Bc, g, Phi, P);
     }
   }
 }
@@ -2243,164 +1941,6 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
   fu::trace(a, g.r, 3);
 }
 
-// Role-split form: a workgroup of two waves walks ranges r = blockIdx.x + k G.
-// Wave 0 (front) streams range k into Phi[k & 1] (prefetching the next range's
-// first tiles across the boundary, so the input stream never pauses); wave 1
-// (back) runs hand-offs, LpCascade and the audio FIR of range k while the front
-// wave already works on range k+1. LDS flags (workgroup scope) order the two:
-// ready[b] = k+1 when range k's phi are in Phi[b]; consumed[b] = k+1 when the
-// back wave has read them. The grid is at most the resident capacity, so every
-// range's predecessor (range r-1, another workgroup, same k) is running.
-template <int N, bool A16, bool CLAMP>
-__global__ __launch_bounds__(128, 2) void k_wbfm_duo(const WbfmArgs a, const WbfmFrontConst C,
-                                                     const WbfmFusedConst Bc, int wpc, int nranges) {
-  using G = fu::G;
-  using Y = fu::Geo<N>;
-  constexpr int L = Y::L;
-  constexpr int PBytes = Y::PSlots * 8;
-  __shared__ __attribute__((aligned(16))) f2 U[G::LDS_F2];
-  __shared__ __attribute__((aligned(16))) float Phi[2][L];
-  __shared__ __attribute__((aligned(16))) f2 P[PBytes / 8];
-  __shared__ __attribute__((aligned(16))) float Gt[128];
-  __shared__ int ready[2], consumed[2];
-  __shared__ f2 dsh[2][2];  // per buffer: d[A], d[A+L-1]
-  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
-  if (threadIdx.x < 2) {
-    ready[threadIdx.x] = 0;
-    consumed[threadIdx.x] = 0;
-  }
-  Gt[threadIdx.x] = C.g[threadIdx.x];
-  __syncthreads();
-  const int G_ = gridDim.x;
-  if (wave == 0) {  // ---- front wave ----
-    int r = blockIdx.x;
-    if (r >= nranges) return;
-    FuRange g = fu_range<N>(a, r, wpc);
-    FuPrefetch org = fu_origin(a, g);
-    f2 va[G::KL][2], vb[G::KL][2];
-    front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, l, va);
-    front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, l, vb);
-    for (int k = 0; r < nranges; ++k, r += G_) {
-      const int b = k & 1;
-      if (k >= 2)  // the back wave has read range k-2's phi from this buffer
-        for (int it = 0; it < (1 << 24); ++it) {
-          if (__hip_atomic_load(&consumed[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= k - 1) break;
-          __builtin_amdgcn_s_sleep(2);
-        }
-      fu::trace(a, r, 0);
-      const bool more = r + G_ < nranges;
-      FuPrefetch nx{nullptr, 0, 0, false};
-      FuRange gn = g;
-      if (more) {
-        gn = fu_range<N>(a, r + G_, wpc);
-        nx = fu_origin(a, gn);
-      }
-      f2 dA = f2{0, 0}, dlast = f2{0, 0};
-      fu_front_range<N, A16, CLAMP>(a, C, g, U, Phi[b], Gt, va, vb, nx, dA, dlast);
-      if (l == 0) {
-        dsh[b][0] = dA;
-        dsh[b][1] = dlast;
-      }
-      wave_lds_fence();
-      if (l == 0) __hip_atomic_store(&ready[b], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      fu::trace(a, r, 1);
-      g = gn;
-    }
-  } else {  // ---- back wave ----
-    int k = 0;
-    for (int r = blockIdx.x; r < nranges; ++k, r += G_) {
-      const int b = k & 1;
-      for (int it = 0; it < (1 << 24); ++it) {
-        if (__hip_atomic_load(&ready[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == k + 1) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
-      asm volatile("" ::: "memory");
-      const FuRange g = fu_range<N>(a, r, wpc);
-      fu_back_range<N>(a, C, Bc, g, Phi[b], P, &consumed[b], k + 1);
-    }
-  }
-}
-
-// Role-split form with NF front waves per back wave: a workgroup of NF + 1
-// waves; front wave f walks ranges r = (NF k + f) G + blockIdx.x (k = 0, 1, ..),
-// so a range's predecessor belongs to the neighbouring workgroup at the same
-// step (no hand-off chain across workgroups). Every front streams continuously
-// into its own Phi[f]; the back wave takes the NF ranges of step k in order,
-// reads each one's phi into registers (consumed[f] = k + 1) and runs its
-// hand-off, LpCascade and audio FIR while the fronts stream on. The fronts keep
-// the input stream busy through the backs (a CU holds 2 such workgroups: 2 NF
-// streaming waves), instead of every wave of a CU pausing its stream for its
-// own back phase at the same time. Grid: at most the resident capacity.
-template <int N, bool A16, bool CLAMP, int NF>
-__global__ __launch_bounds__(64 * (NF + 1), 2) void k_wbfm_team(const WbfmArgs a, const WbfmFrontConst C,
-                                                                const WbfmFusedConst Bc, int wpc, int nranges) {
-  using G = fu::G;
-  using Y = fu::Geo<N>;
-  constexpr int L = Y::L;
-  __shared__ __attribute__((aligned(16))) f2 U[NF][G::LDS_F2];
-  __shared__ __attribute__((aligned(16))) float Phi[NF][L];
-  __shared__ __attribute__((aligned(16))) f2 P[Y::PSlots];
-  __shared__ __attribute__((aligned(16))) float Gt[128];
-  __shared__ int ready[NF], consumed[NF];
-  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63;
-  if (threadIdx.x < NF) {
-    ready[threadIdx.x] = 0;
-    consumed[threadIdx.x] = 0;
-  }
-  if (threadIdx.x < 128) Gt[threadIdx.x] = C.g[threadIdx.x];
-  __syncthreads();
-  const int G_ = gridDim.x;
-  if (wave < NF) {  // ---- front wave f ----
-    const int f = wave;
-    int r = f * G_ + blockIdx.x;
-    if (r >= nranges) return;
-    FuRange g = fu_range<N>(a, r, wpc);
-    const FuPrefetch org = fu_origin(a, g);
-    f2 va[G::KL][2], vb[G::KL][2];
-    front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, l, va);
-    front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, l, vb);
-    for (int k = 0; r < nranges; ++k) {
-      if (k >= 1)  // the back wave has read range k-1's phi from Phi[f]
-        for (int it = 0; it < (1 << 24); ++it) {
-          if (__hip_atomic_load(&consumed[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= k) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-      fu::trace(a, r, 0);
-      const int rn = r + NF * G_;
-      FuPrefetch nx{nullptr, 0, 0, false};
-      FuRange gn = g;
-      if (rn < nranges) {
-        gn = fu_range<N>(a, rn, wpc);
-        nx = fu_origin(a, gn);
-      }
-      f2 dA = f2{0, 0}, dlast = f2{0, 0};
-      fu_front_range<N, A16, CLAMP>(a, C, g, U[f], Phi[f], Gt, va, vb, nx, dA, dlast);
-      wave_lds_fence();
-      if (l == 0) __hip_atomic_store(&ready[f], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      fu::trace(a, r, 1);
-      g = gn;
-      r = rn;
-    }
-  } else {  // ---- back wave ----
-    for (int k = 0;; ++k) {
-      for (int f = 0; f < NF; ++f) {
-        const int r = (NF * k + f) * G_ + blockIdx.x;
-        if (r >= nranges) return;
-        for (int it = 0; it < (1 << 24); ++it) {
-          if (__hip_atomic_load(&ready[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == k + 1) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        asm volatile("" ::: "memory");
-        if (a.fu_abl & 1) {  // timing only: fronts alone
-          if (l == 0) __hip_atomic_store(&consumed[f], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          continue;
-        }
-        fu_back_range<N>(a, C, Bc, fu_range<N>(a, r, wpc), Phi[f], P, &consumed[f], k + 1);
-      }
-    }
-  }
-}
-
 }  // namespace
 
 namespace {
@@ -2442,42 +1982,6 @@ void launch_front2(bool a16, long long n_dec, int nch, int ncu, const WbfmArgs& 
   } else {
     if (a16) k_wbfm_front2<R, true, 0><<<fp.grid, 64, 0, s>>>(a, f, fp.L, fp.wpc);
     else k_wbfm_front2<R, false, 0><<<fp.grid, 64, 0, s>>>(a, f, fp.L, fp.wpc);
-  }
-}
-
-template <int ABL>
-void launch_abl(const Front2Plan& fp, dim3 gb, const WbfmArgs& a, const WbfmFrontConst& f,
-                const WbfmBackConst& b, hipStream_t s) {
-  k_wbfm_front2<kFrontR, true, ABL & ~(16 | 32 | 64)><<<fp.grid, 64, 0, s>>>(a, f, fp.L, fp.wpc);
-  if constexpr (!(ABL & 64)) k_wbfm_back<ABL & 48><<<gb, NT, 0, s>>>(a, b);
-}
-
-void launch_wbfm_ablation(int abl, bool a16, const Front2Plan& fp, dim3 gb, const WbfmArgs& a,
-                          const WbfmFrontConst& f, const WbfmBackConst& b, hipStream_t s) {
-  if (!a16) throw HipError("ablation runs need 16-B aligned input");
-  switch (abl) {
-    case 1: launch_abl<1>(fp, gb, a, f, b, s); break;
-    case 2: launch_abl<2>(fp, gb, a, f, b, s); break;
-    case 4: launch_abl<4>(fp, gb, a, f, b, s); break;
-    case 8: launch_abl<8>(fp, gb, a, f, b, s); break;
-    case 3: launch_abl<3>(fp, gb, a, f, b, s); break;
-    case 14: launch_abl<14>(fp, gb, a, f, b, s); break;
-    case 15: launch_abl<15>(fp, gb, a, f, b, s); break;
-    case 16: launch_abl<16>(fp, gb, a, f, b, s); break;
-    case 32: launch_abl<32>(fp, gb, a, f, b, s); break;
-    case 48: launch_abl<48>(fp, gb, a, f, b, s); break;
-    case 128: launch_abl<128>(fp, gb, a, f, b, s); break;
-    case 143: launch_abl<143>(fp, gb, a, f, b, s); break;
-    case 142: launch_abl<142>(fp, gb, a, f, b, s); break;
-    case 128 | 1: launch_abl<128 | 1>(fp, gb, a, f, b, s); break;
-    case 512 | 1: launch_abl<512 | 1>(fp, gb, a, f, b, s); break;
-    case 512: launch_abl<512>(fp, gb, a, f, b, s); break;
-    case 14 | 256: launch_abl<14 | 256>(fp, gb, a, f, b, s); break;
-    case 14 | 512: launch_abl<14 | 512>(fp, gb, a, f, b, s); break;
-    case 14 | 1024: launch_abl<14 | 1024>(fp, gb, a, f, b, s); break;
-    case 14 | 256 | 512 | 1024: launch_abl<14 | 256 | 512 | 1024>(fp, gb, a, f, b, s); break;
-    case 15 | 256 | 512 | 1024: launch_abl<15 | 256 | 512 | 1024>(fp, gb, a, f, b, s); break;
-    default: throw HipError("unknown ORION_WBFM_ABL value " + std::to_string(abl));
   }
 }
 
@@ -2535,51 +2039,10 @@ void launch_wbfm_fused(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFus
   const bool a16 = (reinterpret_cast<uintptr_t>(a.x) % 16 == 0) && (a.x_stride % 2 == 0);
   const int wpc = static_cast<int>((a.n_dec + kFuL - 1) / kFuL);
   const int grid = wpc * nch;
-  static const int kernel = [] {  // 1: one wave per range (default), 2: role-split
+  static const int kernel = [] {  // 1: one wave per range, 3: persistent (experiments)
     const char* e = std::getenv("ORION_WBFM_KERNEL");
     return e ? std::atoi(e) : 1;
   }();
-  if (kernel == 2) {
-    // persistent: at most the resident capacity, so every range's predecessor runs
-    static int cap = 0;
-    if (cap == 0) {
-      int per_cu = 0, dev = 0, ncu = 0;
-      ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_duo<kFuN, true, false>, 128, 0));
-      ORION_HIP(hipGetDevice(&dev));
-      ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-      cap = std::max(1, per_cu) * std::max(1, ncu);
-    }
-    const int g2 = std::min(grid, cap);
-    if (a.n < 2LL * Fw<2>::NEW) {
-      if (a16) k_wbfm_duo<kFuN, true, true><<<g2, 128, 0, s>>>(a, f, b, wpc, grid);
-      else k_wbfm_duo<kFuN, false, true><<<g2, 128, 0, s>>>(a, f, b, wpc, grid);
-    } else {
-      if (a16) k_wbfm_duo<kFuN, true, false><<<g2, 128, 0, s>>>(a, f, b, wpc, grid);
-      else k_wbfm_duo<kFuN, false, false><<<g2, 128, 0, s>>>(a, f, b, wpc, grid);
-    }
-    ORION_LAUNCH_CHECK();
-    return;
-  }
-  if (kernel == 4) {  // team: 3 front waves + 1 back wave per workgroup
-    constexpr int NF = 3;
-    static int cap = 0;
-    if (cap == 0) {
-      int per_cu = 0, dev = 0, ncu = 0;
-      ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_team<kFuN, true, false, NF>,
-                                                             64 * (NF + 1), 0));
-      ORION_HIP(hipGetDevice(&dev));
-      ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-      cap = std::max(1, per_cu) * std::max(1, ncu);
-    }
-    const int g4 = std::min((grid + NF - 1) / NF, cap);
-    const bool clamp = a.n < 2LL * Fw<2>::NEW;
-#define ORION_TEAM(A, C) k_wbfm_team<kFuN, A, C, NF><<<g4, 64 * (NF + 1), 0, s>>>(a, f, b, wpc, grid)
-    if (clamp) { if (a16) ORION_TEAM(true, true); else ORION_TEAM(false, true); }
-    else { if (a16) ORION_TEAM(true, false); else ORION_TEAM(false, false); }
-#undef ORION_TEAM
-    ORION_LAUNCH_CHECK();
-    return;
-  }
   int g1 = grid;
   // experiments only: dynamic LDS padding per wave (caps the waves per CU)
   static const int dyn = [] {
@@ -2611,15 +2074,6 @@ void launch_wbfm_fused(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFus
   ORION_LAUNCH_CHECK();
 }
 
-namespace {
-
-int env_int(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
-
-}  // namespace
-
 int device_cus() {
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
@@ -2633,28 +2087,10 @@ void launch_wbfm(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmBackConst
                  hipStream_t s) {
   if (a.n_dec <= 0 || nch <= 0) return;
   static const int ncu = device_cus();
-  static const int abl = env_int("ORION_WBFM_ABL", 0);      // timing ablations only
-  static const int variant = env_int("ORION_WBFM_FRONT", 2);  // 1: persistent barrier form
   const bool a16 = (reinterpret_cast<uintptr_t>(a.x) % 16 == 0) && (a.x_stride % 2 == 0);
   const dim3 gb(div_up(a.n_dec, kBackA), nch);
-  static const int rsel = env_int("ORION_WBFM_R", kFrontR);  // experiments: 2, 4, 6
-  const Front2Plan fp = front2_plan<kFrontR>(a.n_dec, nch, ncu);
-  if (abl != 0) {
-    launch_wbfm_ablation(abl, a16, fp, gb, a, f, b, s);
-  } else if (variant == 1) {
-    const int G = ((4 * ncu) + 7) / 8 * 8;  // 4 resident workgroups per CU, a multiple of 8 (XCDs)
-    const int tiles = div_up(a.n_dec, kWbfmPhi);
-    const long long total = static_cast<long long>(tiles) * nch;
-    const int grid = total < G ? static_cast<int>((total + 7) / 8 * 8) : G;
-    if (a16) k_wbfm_front<true, 0><<<grid, NT, 0, s>>>(a, f, tiles, nch);
-    else k_wbfm_front<false, 0><<<grid, NT, 0, s>>>(a, f, tiles, nch);
-    k_wbfm_back<0><<<gb, NT, 0, s>>>(a, b);
-  } else {
-    if (rsel == 2) launch_front2<2>(a16, a.n_dec, nch, ncu, a, f, s);
-    else if (rsel == 4) launch_front2<4>(a16, a.n_dec, nch, ncu, a, f, s);
-    else launch_front2<6>(a16, a.n_dec, nch, ncu, a, f, s);
-    k_wbfm_back<0><<<gb, NT, 0, s>>>(a, b);
-  }
+  launch_front2<kFrontR>(a16, a.n_dec, nch, ncu, a, f, s);
+  k_wbfm_back<0><<<gb, NT, 0, s>>>(a, b);
   ORION_LAUNCH_CHECK();
 }
 
