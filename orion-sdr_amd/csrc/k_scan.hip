@@ -274,6 +274,230 @@ __global__ __launch_bounds__(NT) void k_scan_apply(const ScanArgs a) {
   for (int e2 = t; e2 < cnt; e2 += NT) y[e2] = sb[pos(e2)];
 }
 
+
+// ---- single-pass LpDcCascade (SsbProductDemod, AmEnvelopeDemod AbsApprox) ----
+// One workgroup per chunk of one channel, the grid chunk-major (blockIdx.x =
+// c * nch + ch), so every chunk's predecessor was dispatched earlier. The input
+// is read once (the three-kernel scan reads it twice):
+//   * LP4: the chunk's 4096 staged samples start kSpWarm samples before its
+//     first output, from a zero state (the LP poles decay below 1e-10 of the
+//     state within kSpWarm samples: the host checks ||A_lp^kSpWarm||); chunk 0
+//     has no warm-up and starts from the carried state. Block-level scan as in
+//     k_scan_apply, then the reference's f32 update re-run -> exact LP output x.
+//   * DC blocker (y = x - x1 + r y1, pole ~1 - 2.6e-4: it never forgets): a
+//     1-dim scan of (r^len, zero-state aggregate) pairs inside the block and a
+//     decoupled look-back across chunks (thread 0): each chunk publishes its
+//     aggregate, then its inclusive prefix; the state entering chunk c is read
+//     from the nearest predecessor that has published a prefix.
+// Look-back records (u32 words, agent-scope sc1 stores + flags): [0,2) zero-
+// state aggregate, [2,4) r^len, [4,6) inclusive prefix, 6 flag(aggregate),
+// 7 flag(prefix); flags hold the launch epoch.
+__device__ __forceinline__ void sp_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t sp_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sp_st64(uint32_t* p, double v) {
+  const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
+  sp_st(p, static_cast<uint32_t>(b));
+  sp_st(p + 1, static_cast<uint32_t>(b >> 32));
+}
+__device__ __forceinline__ double sp_ld64(const uint32_t* p) {
+  const unsigned long long lo = sp_ld(p), hi = sp_ld(p + 1);
+  return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
+}
+// (m1, d1) then (m2, d2): y -> m2 (m1 y + d1) + d2
+__device__ __forceinline__ void dc_combine(double m1, double d1, double& m2, double& d2) {
+  d2 = __builtin_fma(m2, d1, d2);
+  m2 = m2 * m1;
+}
+
+template <Pre PR>
+__global__ __launch_bounds__(NT) void k_lpdc_sp(const ScanArgs a, const double* __restrict__ mlp, int nch,
+                                               uint32_t* __restrict__ rec, uint32_t epoch) {
+  constexpr int S = 4;
+  __shared__ float sb[PADN];
+  __shared__ double tot[4][S];
+  __shared__ double dtot[4][2];
+  __shared__ double excl_sh;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int ch = static_cast<int>(blockIdx.x % nch);
+  const int c = static_cast<int>(blockIdx.x / nch);
+  const int warm = c == 0 ? 0 : kSpWarm;
+  const long long o0 = c == 0 ? 0 : CH + static_cast<long long>(c - 1) * (CH - kSpWarm);
+  const long long base = o0 - warm;                          // first staged sample
+  const int cnt = static_cast<int>(min(static_cast<long long>(CH), a.n - base));  // staged samples
+  const int nchunk = a.n <= CH ? 1 : 1 + static_cast<int>((a.n - CH + (CH - kSpWarm) - 1) / (CH - kSpWarm));
+  const bool last = c == nchunk - 1;
+  const float* __restrict__ ci = a.carry_in + ch * kScanCarry;
+  const RecLP4 lp{{a.c.b0, a.c.b1, a.c.b2, a.c.a1, a.c.a2}};
+  const float r = a.c.r;
+  stage<PR>(a, ch, base, cnt, sb);
+  __syncthreads();
+
+  // ---- LP4: zero-state lane aggregates, block scan, exact re-run ----
+  float xs[C];
+#pragma unroll
+  for (int i = 0; i < C; ++i) xs[i] = sb[pos(t * C + i)];
+  float s0[S] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < C; ++i)
+    if (t * C + i < cnt) (void)lp.step(s0, xs[i]);
+  double q[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) q[i] = s0[i];
+  wave_scan_inclusive<S>(q, mlp + ScanMatsLayout::kPwc * S * S, lane);
+  if (lane == 63)
+#pragma unroll
+    for (int i = 0; i < S; ++i) tot[wave][i] = q[i];
+  __syncthreads();
+  double cw[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) cw[i] = c == 0 ? static_cast<double>(ci[i]) : 0.0;
+  for (int w = 0; w < wave; ++w) {
+    double v[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) v[i] = tot[w][i];
+    matvec_acc<S>(mlp + ScanMatsLayout::kM64 * S * S, cw, v);
+#pragma unroll
+    for (int i = 0; i < S; ++i) cw[i] = v[i];
+  }
+  double e[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const double o = __shfl_up(q[i], 1, 64);
+    e[i] = lane == 0 ? 0.0 : o;
+  }
+  matvec_acc<S>(mlp + (ScanMatsLayout::kLane + lane) * S * S, cw, e);
+  float ef[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) ef[i] = static_cast<float>(e[i]);
+#pragma unroll
+  for (int i = 0; i < C; ++i)
+    if (t * C + i < cnt) xs[i] = lp.step(ef, xs[i]);  // LP output x (f32, reference update)
+  __syncthreads();  // every lane has read its sb inputs
+#pragma unroll
+  for (int i = 0; i < C; ++i) sb[pos(t * C + i)] = xs[i];
+  __syncthreads();
+
+  // ---- DC blocker: zero-state lane pairs (r^k, y_k), block scan ----
+  const float xprev0 = t * C == 0 ? ci[4] : sb[pos(t * C - 1)];  // x before the lane's first sample
+  double m = 1.0, d = 0.0;
+  {
+    float xp = xprev0, y = 0.0f;
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      const int ei = t * C + i;
+      if (ei >= warm && ei < cnt) {
+        y = (xs[i] - xp) + r * y;
+        m *= static_cast<double>(r);
+      }
+      xp = xs[i];
+    }
+    d = y;
+  }
+  // inclusive scan of (m, d) over the wave, then over the waves
+  double mi = m, di = d;
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    const int dd = 1 << s;
+    const double mo = __shfl_up(mi, dd, 64), do_ = __shfl_up(di, dd, 64);
+    if (lane >= dd) dc_combine(mo, do_, mi, di);
+  }
+  if (lane == 63) {
+    dtot[wave][0] = mi;
+    dtot[wave][1] = di;
+  }
+  __syncthreads();
+  double wm = 1.0, wd = 0.0;  // pairs of the waves before this one
+  for (int w = 0; w < wave; ++w) {
+    double m2 = dtot[w][0], d2 = dtot[w][1];
+    dc_combine(wm, wd, m2, d2);
+    wm = m2;
+    wd = d2;
+  }
+  if (t == 0) {  // chunk aggregate, look-back, prefix
+    double bm = 1.0, bd = 0.0;
+    for (int w = 0; w < 4; ++w) {
+      double m2 = dtot[w][0], d2 = dtot[w][1];
+      dc_combine(bm, bd, m2, d2);
+      bm = m2;
+      bd = d2;
+    }
+    uint32_t* my = rec + (static_cast<long long>(ch) * nchunk + c) * 8;
+    if (!last) {
+      sp_st64(my, bd);
+      sp_st64(my + 2, bm);
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the record is visible before its flag
+      sp_st(my + 6, epoch);
+    }
+    double excl = 0.0, mult = 1.0;
+    int k = c - 1;
+    for (; k >= 0; --k) {
+      const uint32_t* pr = rec + (static_cast<long long>(ch) * nchunk + k) * 8;
+      int it = 0;
+      while (sp_ld(pr + 6) != epoch && sp_ld(pr + 7) != epoch && ++it < (1 << 22)) __builtin_amdgcn_s_sleep(2);
+      if (sp_ld(pr + 7) == epoch) {
+        excl = __builtin_fma(mult, sp_ld64(pr + 4), excl);
+        break;
+      }
+      excl = __builtin_fma(mult, sp_ld64(pr), excl);
+      mult *= sp_ld64(pr + 2);
+    }
+    if (k < 0) excl = __builtin_fma(mult, static_cast<double>(ci[5]), excl);  // the carried y1
+    if (!last) {
+      sp_st64(my + 4, __builtin_fma(bm, excl, bd));
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      sp_st(my + 7, epoch);
+    }
+    excl_sh = excl;
+  }
+  __syncthreads();
+  // the state entering this lane: exclusive pair within the block applied to excl
+  double em = __shfl_up(mi, 1, 64), ed = __shfl_up(di, 1, 64);
+  if (lane == 0) {
+    em = 1.0;
+    ed = 0.0;
+  }
+  dc_combine(wm, wd, em, ed);  // waves before, then lanes before
+  float y = static_cast<float>(__builtin_fma(em, excl_sh, ed));
+  {
+    float xp = xprev0;
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      const int ei = t * C + i;
+      float out = 0.0f;
+      if (ei >= warm && ei < cnt) {
+        y = (xs[i] - xp) + r * y;  // dsp/iir.rs:161 (y1 - dc_x1) + r * dc_y1
+        out = y;
+      }
+      xp = xs[i];
+      xs[i] = out;
+    }
+  }
+  if (last && t * C <= cnt - 1 && cnt - 1 < t * C + C) {  // carried state of the next call
+    float* co = a.carry_out + ch * kScanCarry;
+#pragma unroll
+    for (int i = 0; i < S; ++i) co[i] = ef[i];  // ef ran to the lane's last valid sample
+    const int il = cnt - 1 - t * C;
+    float xl = 0.0f;
+#pragma unroll
+    for (int i = 0; i < C; ++i)
+      if (i == il) xl = sb[pos(t * C + i)];
+    co[4] = xl;
+    co[5] = y;
+    co[6] = ci[6];
+    co[7] = ci[7];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < C; ++i) sb[pos(t * C + i)] = xs[i];
+  __syncthreads();
+  float* yo = static_cast<float*>(a.y) + ch * a.y_stride + o0;
+  for (int e2 = warm + t; e2 < cnt; e2 += NT) yo[e2 - warm] = sb[pos(e2)];
+}
+
 template <RecK RK, Pre PR, Post PO>
 void run3(const ScanArgs& a, int nch, hipStream_t s) {
   const int nblk = div_up(a.n, CH);
@@ -293,6 +517,21 @@ int scan_state_dim(RecK rec) {
     case RecK::DC: return 2;
     default: return 1;
   }
+}
+
+long long lpdc_sp_chunks(long long n) {
+  return n <= CH ? 1 : 1 + (n - CH + (CH - kSpWarm) - 1) / (CH - kSpWarm);
+}
+
+void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, uint32_t* rec, uint32_t epoch,
+                    hipStream_t s) {
+  if (a.n <= 0 || nch <= 0) return;
+  const long long grid = lpdc_sp_chunks(a.n) * nch;
+  if (grid > (1LL << 31) - 1) throw HipError("single-pass scan grid too large");
+  if (pre == Pre::Ssb) k_lpdc_sp<Pre::Ssb><<<static_cast<int>(grid), NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+  else if (pre == Pre::AmAbs) k_lpdc_sp<Pre::AmAbs><<<static_cast<int>(grid), NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+  else throw std::invalid_argument("single-pass LpDc scan: unsupported front end");
+  ORION_LAUNCH_CHECK();
 }
 
 void launch_scan(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, hipStream_t s) {

@@ -75,6 +75,14 @@ struct ScanArgs {
 };
 
 void launch_scan(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, hipStream_t s);
+// Single-pass LpDcCascade (Pre::Ssb / Pre::AmAbs): LP4 warm-up of kSpWarm samples
+// per chunk (valid when ||A_lp^kSpWarm|| is negligible), DC state by decoupled
+// look-back. mats_lp: ScanMatsLayout for the LP4 state space (S = 4); rec:
+// lpdc_sp_chunks(n) * nch * 8 u32 look-back records; epoch: this launch's tag.
+constexpr int kSpWarm = 256;
+long long lpdc_sp_chunks(long long n);
+void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, uint32_t* rec, uint32_t epoch,
+                    hipStream_t s);
 int scan_state_dim(RecK rec);
 
 }  // namespace orion

@@ -2,6 +2,7 @@
 #include "scan_blocks.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 
 #include "scan.hpp"
@@ -14,7 +15,26 @@ class ScanStage {
  public:
   ScanStage(RecK rec, Pre pre, Post post, const StateSpace& ss, const ScanCoef& c, int nch)
       : rec_(rec), pre_(pre), post_(post), c_(c), nch_(nch), S_(ss.S) {
-    const int S = S_;
+    const auto mats = build_mats(ss);
+    mats_.upload(mats.data(), mats.size() * sizeof(double));
+    for (auto& c0 : carry_) c0.resize(static_cast<size_t>(nch_) * kScanCarry * sizeof(float));
+    // LpDcCascade after an SSB / AM-abs front end: single pass when the LP4
+    // forgets its state within the kSpWarm-sample warm-up (SsbProductDemod at
+    // 48 kHz: ||A^256|| ~ 1e-20)
+    if (rec == RecK::LPDC && (pre == Pre::Ssb || pre == Pre::AmAbs)) {
+      const StateSpace lp = lp_cascade_ss(BiquadCoeffs{c.b0, c.b1, c.b2, c.a1, c.a2});
+      const auto m = mat_pow(lp.A, 4, kSpWarm);
+      double fro = 0.0;
+      for (double v : m) fro += v * v;
+      sp_ok_ = std::sqrt(fro) < 1e-10;
+      if (sp_ok_) {
+        const auto ml = build_mats(lp);
+        mats_lp_.upload(ml.data(), ml.size() * sizeof(double));
+      }
+    }
+  }
+  static std::vector<double> build_mats(const StateSpace& ss) {
+    const int S = ss.S;
     std::vector<double> mats(static_cast<size_t>(ScanMatsLayout::kCount) * S * S, 0.0);
     auto put = [&](int idx, const std::vector<double>& m) {
       std::copy(m.begin(), m.end(), mats.begin() + static_cast<size_t>(idx) * S * S);
@@ -32,9 +52,10 @@ class ScanStage {
       p = mat_mul(p, p, S);
     }
     for (int L = 0; L < 64; ++L) put(ScanMatsLayout::kLane + L, mat_pow(ss.A, S, static_cast<uint64_t>(kScanC) * L));
-    mats_.upload(mats.data(), mats.size() * sizeof(double));
-    for (auto& c0 : carry_) c0.resize(static_cast<size_t>(nch_) * kScanCarry * sizeof(float));
+    return mats;
   }
+  // 0 auto (single pass where valid), 1 force the three-kernel scan (tests)
+  void set_mode(int m) { mode_ = m; }
   void set_osc(const Oscillator& o) {
     step_ = o.step_q64;
     const auto t = phasor_table(o.theta, kScanCH);
@@ -68,7 +89,21 @@ class ScanStage {
     a.carry_in = carry_[cur_].as<float>();
     a.carry_out = carry_[cur_ ^ 1].as<float>();
     a.c = c_;
-    launch_scan(rec_, pre_, post_, a, nch_, s);
+    if (sp_ok_ && mode_ == 0) {
+      const size_t words = static_cast<size_t>(lpdc_sp_chunks(n)) * nch_ * 8;
+      if (words * 4 > rec_buf_.size()) {
+        rec_buf_.resize(words * 4);
+        rec_buf_.zero(s);
+        epoch_ = 0;
+      }
+      if (++epoch_ == 0xFFFFFFFFu) {  // never reuse a tag that may sit in a record
+        rec_buf_.zero(s);
+        epoch_ = 1;
+      }
+      launch_lpdc_sp(pre_, a, mats_lp_.as<double>(), nch_, rec_buf_.as<uint32_t>(), epoch_, s);
+    } else {
+      launch_scan(rec_, pre_, post_, a, nch_, s);
+    }
     cur_ ^= 1;
   }
 
@@ -80,8 +115,11 @@ class ScanStage {
   int nch_, S_;
   bool translate_ = false;
   uint64_t step_ = 0;
-  DevBuf mats_, tab_, carry_[2], ws_;
+  DevBuf mats_, tab_, carry_[2], ws_, mats_lp_, rec_buf_;
   int cur_ = 0;
+  bool sp_ok_ = false;
+  int mode_ = 0;
+  uint32_t epoch_ = 0;
 };
 
 ScanCoef coef_lp(const BiquadCoeffs& b) {

@@ -199,6 +199,24 @@ def test_pm_ssb_am_cw(gpu_lib, oracle):
     report("ssb batch nrmse", nrmse(got, oracle.ssb_demod_channels(x, FS, 1500.0, 2800.0, 8)), 1e-4)
 
 
+def test_single_pass_lpdc_geometry(gpu_lib, oracle):
+    """Single-pass LpDcCascade (SSB, AM AbsApprox): chunk-boundary lengths
+    (4096 = one chunk, 4097, 4096 + 3840 + 1), calls of ragged length carrying
+    the state, and multi-chunk look-back across channels."""
+    a = real_tone(FS, 1200.0, 200_000, 0.4)
+    iq = oracle.add_awgn(oracle.ssb_mod(a, FS, 2800.0, 1500.0), 1e-3, 7)
+    ref = oracle.ssb_demod(iq, FS, 1500.0, 2800.0)
+    for n in (4096, 4097, 4096 + 3840 + 1, 4096 + 3 * 3840):
+        report(f"ssb single-pass n={n} nrmse", nrmse(gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0).process(iq[:n]),
+                                                     ref[:n]), 1e-4)
+    got = stream(gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0), iq, 7937)
+    report("ssb single-pass streamed 7937 nrmse", nrmse(got, ref), 1e-4)
+    am = oracle.am_mod(real_tone(FS, 1000.0, 100_000, 0.5), FS, 0.0, 0.8, 0.5)
+    got = stream(gpu_lib.AmEnvelopeDemod(FS, 5000, abs_approx=True), am, 33_333)
+    report("am abs single-pass streamed nrmse",
+           nrmse(got, oracle.am_demod(am, FS, 5000.0, abs_approx=(0.9482, 0.3920))), 1e-5)
+
+
 def test_reference_roundtrips_on_gpu(gpu_lib, oracle):
     """tests/roundtrip/*.rs thresholds through the GPU demodulators."""
     a = real_tone(FS, 1000.0, 32768, 0.5)

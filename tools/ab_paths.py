@@ -20,7 +20,8 @@ s = torch.cuda.current_stream(dev)
 res = {p: [] for p in paths}
 for rnd in range(6):
     for p in paths:
-        blk.configure(p)
+        name, _, ms = p.partition(":")
+        blk.configure(name, int(ms or 0))
         blk.process_device(x, out, s.cuda_stream)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
