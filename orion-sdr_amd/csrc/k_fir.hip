@@ -3,6 +3,9 @@
 //   FirDecimator::process                   dsp/decim.rs:44-76 (kept outputs only)
 //   FirLowpass::process                     dsp/fir.rs:47-66   (real)
 //   FirLowpassIq::process / filter_aligned  dsp/fir.rs:229-297 (complex, real taps)
+#include <algorithm>
+#include <cstdlib>
+
 #include "kernels.hpp"
 #include "poly.hpp"
 
@@ -95,6 +98,169 @@ __global__ __launch_bounds__(NT) void k_decim8(const f2* __restrict__ x, long lo
       if (j < n_out) out[j] = acc[r];
     }
     __syncthreads();
+  }
+}
+
+// ------------------------------------------- wave-independent decimator ---
+// k_decim_w<Q>: FirDecimator with M = 8 and K <= 8Q taps (C3: 255 taps, Q = 32)
+// in the WBFM front's form. One 64-lane wave per contiguous range of decimated
+// outputs of one channel (as many waves as are resident, one round), walked in
+// tiles of TW = 128 outputs / 1024 new inputs. A tile's inputs are prefetched
+// two tiles ahead into registers (16-B nontemporal loads) and scattered into an
+// 8-row polyphase LDS image (pitch TW+Q+2 = 2 mod 16: conflict-free
+// ds_write_b64); the image's Q+2 leading columns are the previous tile's last
+// ones, copied inside LDS. Each lane computes outputs 2l, 2l+1 from (Q+2)/2
+// conflict-free ds_read_b128 and 2Q packed FMAs per phase (taps from SGPRs) and
+// stores them with one 16-B store (a wave writes 1 KB contiguously). No
+// workgroup barriers, so the register prefetch stays in flight.
+template <int Q>
+struct Dw {
+  static constexpr int TW = 128;         // outputs per tile
+  static constexpr int NEW = 8 * TW;     // new inputs per tile
+  static constexpr int KL = NEW / 128;   // 2-sample loads per lane per tile
+  static constexpr int LR = TW + Q + 2;  // row pitch (2 mod 16)
+  static constexpr int LDS_F2 = 8 * LR;
+  static constexpr int WIN = (2 + Q) / 2;  // b128 window reads per lane and phase
+  static constexpr int HALO = Q + 2;       // columns carried tile to tile
+  static_assert(LR % 16 == 2, "row pitch");
+};
+
+// New inputs of the tile whose staged sample 0 is x[porg]: x[porg + 8Q + 2l + 128k (+1)].
+// CLAMP = false (n >= 2 NEW): the uniform base is clamped into [0, n - NEW];
+// boundary tiles are rewritten exactly at staging. CLAMP: per-lane clamp.
+template <int Q, bool A16, bool CLAMP>
+__device__ __forceinline__ void dw_load(const f2* __restrict__ x, long long n, long long porg, int l,
+                                        f2 (&v)[Dw<Q>::KL][2]) {
+  const long long B = porg + 8 * Q;
+  const f2* __restrict__ xb;
+  int lo = 0, hi = 0;
+  if constexpr (CLAMP) {
+    constexpr long long kSat = 1LL << 30;
+    lo = static_cast<int>(max(-B, -kSat));
+    hi = static_cast<int>(min(max((n - 2 - B) & ~1LL, -kSat), kSat));
+    xb = x + B;
+  } else {
+    xb = x + min(max(B, 0LL), (n - Dw<Q>::NEW) & ~1LL);
+  }
+#pragma unroll
+  for (int k = 0; k < Dw<Q>::KL; ++k) {
+    const int o = CLAMP ? min(max(2 * l + 128 * k, lo), hi) : 2 * l + 128 * k;
+    if constexpr (A16) {
+      const f4 w = __builtin_nontemporal_load(reinterpret_cast<const f4*>(xb + o));
+      v[k][0] = f2{w.x, w.y};
+      v[k][1] = f2{w.z, w.w};
+    } else {
+      v[k][0] = xb[o];
+      v[k][1] = xb[o + 1];
+    }
+  }
+}
+
+template <int Q, bool A16, bool CLAMP>
+__device__ __forceinline__ void dw_tile(f2* __restrict__ U, int l, int n, long long porg, long long J,
+                                        const f2* __restrict__ xc, long long nx, const f2* __restrict__ hc,
+                                        int hist_len, f2 (&v)[Dw<Q>::KL][2], const f2* __restrict__ pfx,
+                                        long long pfn, long long pforg, const Taps256& g, int s0, int s1,
+                                        f2* __restrict__ outc, long long n_out) {
+  using D = Dw<Q>;
+  if (n > 0) {  // halo: the previous tile's columns TW .. TW+Q+1 -> 0 .. Q+1
+#pragma unroll
+    for (int r2 = 0; r2 < (8 * D::HALO / 2 + 63) / 64; ++r2) {
+      const int e = l + 64 * r2;
+      if (e < 8 * D::HALO / 2) {
+        const int c = e / (D::HALO / 2), h = e - (D::HALO / 2) * c;
+        const f4 w = *reinterpret_cast<const f4*>(U + c * D::LR + D::TW + 2 * h);
+        *reinterpret_cast<f4*>(U + c * D::LR + 2 * h) = w;
+      }
+    }
+    wave_lds_fence();
+  }
+#pragma unroll
+  for (int k = 0; k < D::KL; ++k) {
+    U[s0 + 16 * k] = v[k][0];
+    U[s1 + 16 * k] = v[k][1];
+  }
+  asm volatile("" ::: "memory");
+  dw_load<Q, A16, CLAMP>(pfx, pfn, pforg, l, v);  // the tile two ahead (unconditional: see fu_tile)
+  const bool bnd = porg < 0 || porg + 8LL * (D::TW + Q) > nx;
+  if (bnd || n == 0) {
+    // a range's first tile stages its halo columns; a tile reaching before x[0]
+    // or past x[n-1] rewrites its new samples exactly (history / zeros)
+    wave_lds_fence();
+#pragma unroll 1
+    for (int p = (n == 0 ? 0 : 8 * Q) + l; p < 8 * (D::TW + Q); p += 64) {
+      const long long P = porg + p;
+      if (p < 8 * Q || !CLAMP || P < 0 || P >= nx) {
+        const int c = (-p) & 7;
+        U[c * D::LR + (p + c) / 8] = load_hist(xc, nx, hc, hist_len, P);
+      }
+    }
+  }
+  wave_lds_fence();
+  f2 d0 = f2{0.0f, 0.0f}, d1 = f2{0.0f, 0.0f};
+#pragma unroll 1
+  for (int c = 0; c < 8; ++c) {
+    const f4* row = reinterpret_cast<const f4*>(U + c * D::LR + 2 * l);
+    f4 w[D::WIN];
+#pragma unroll
+    for (int h = 0; h < D::WIN; ++h) w[h] = row[h];
+    float t[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) t[q] = g.g[c * Q + q];
+    // window entry m -> output r uses tap q = r + Q - m
+#pragma unroll
+    for (int h = 0; h < D::WIN; ++h) {
+      const f2 w0 = f2{w[h].x, w[h].y}, w1 = f2{w[h].z, w[h].w};
+      const int m0 = 2 * h, m1 = 2 * h + 1;
+      if (Q - m0 >= 0 && Q - m0 < Q) d0 = fma2(splat2(t[Q - m0]), w0, d0);
+      if (Q - m1 >= 0 && Q - m1 < Q) d0 = fma2(splat2(t[Q - m1]), w1, d0);
+      if (1 + Q - m0 >= 0 && 1 + Q - m0 < Q) d1 = fma2(splat2(t[1 + Q - m0]), w0, d1);
+      if (1 + Q - m1 >= 0 && 1 + Q - m1 < Q) d1 = fma2(splat2(t[1 + Q - m1]), w1, d1);
+    }
+  }
+  const long long j = J + 2 * l;
+  if (j + 1 < n_out && (reinterpret_cast<uintptr_t>(outc + j) & 15) == 0) {
+    __builtin_nontemporal_store(f4{d0.x, d0.y, d1.x, d1.y}, reinterpret_cast<f4*>(outc + j));
+  } else {
+    if (j < n_out) outc[j] = d0;
+    if (j + 1 < n_out) outc[j + 1] = d1;
+  }
+}
+
+template <int Q, bool A16, bool CLAMP>
+__global__ __launch_bounds__(64, 3) void k_decim_w(const f2* __restrict__ x, long long x_stride, long long n,
+                                                  const f2* __restrict__ hist, int hist_len, f2* __restrict__ out,
+                                                  long long out_stride, long long n_out, const Taps256 g, int wpc,
+                                                  long long L) {
+  using D = Dw<Q>;
+  __shared__ __attribute__((aligned(16))) f2 U[D::LDS_F2];
+  const int l = threadIdx.x & 63;
+  const int ch = blockIdx.x / wpc;
+  const long long A = static_cast<long long>(blockIdx.x - ch * wpc) * L;
+  const long long B = min(A + L, n_out);
+  if (A >= B) return;
+  // an even tile count: the second tile of a pair always runs (a conditional
+  // one would make the compiler drain the other buffer's prefetch); tiles past
+  // B store nothing
+  const int ntiles = (static_cast<int>((B - A + D::TW - 1) / D::TW) + 1) & ~1;
+  const f2* __restrict__ xc = x + ch * x_stride;
+  const f2* __restrict__ hc = hist + static_cast<long long>(ch) * hist_len;
+  f2* __restrict__ outc = out + ch * out_stride;
+  const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
+  const int s0 = c0 * D::LR + (8 * Q + 2 * l + c0) / 8;
+  const int s1 = c1 * D::LR + (8 * Q + 2 * l + 1 + c1) / 8;
+  long long porg = 8LL * (A - Q);  // x index of staged sample 0 of the first tile
+  f2 va[D::KL][2], vb[D::KL][2];
+  dw_load<Q, A16, CLAMP>(xc, n, porg, l, va);
+  dw_load<Q, A16, CLAMP>(xc, n, porg + D::NEW, l, vb);
+  const long long dummy = -8LL * Q;  // past the range: the channel's first tile (an L2 hit)
+#pragma unroll 1
+  for (int t = 0; t < ntiles; t += 2, porg += 2 * D::NEW) {
+    const long long J = A + static_cast<long long>(t) * D::TW;
+    dw_tile<Q, A16, CLAMP>(U, l, t, porg, J, xc, n, hc, hist_len, va, xc, n,
+                           t + 2 < ntiles ? porg + 2 * D::NEW : dummy, g, s0, s1, outc, B);
+    dw_tile<Q, A16, CLAMP>(U, l, t + 1, porg + D::NEW, J + D::TW, xc, n, hc, hist_len, vb, xc, n,
+                           t + 3 < ntiles ? porg + 3 * D::NEW : dummy, g, s0, s1, outc, B);
   }
 }
 
@@ -263,7 +429,39 @@ void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* 
   const bool a16 = reinterpret_cast<uintptr_t>(x) % 16 == 0 && x_stride % 2 == 0;
   // Fast polyphase path: M = 8 with K <= 128 / 256 taps; grid spread so that the
   // whole launch has >= 2048 workgroups when channels allow.
-  if (M == 8 && K <= 256 && hist_len >= 8 * (K <= 128 ? 16 : 32)) {
+  static const bool legacy = [] {  // experiments: the barrier-form k_decim8
+    const char* e = std::getenv("ORION_DECIM_LEGACY");
+    return e && e[0] == '1';
+  }();
+  if (M == 8 && K <= 256 && hist_len >= 8 * (K <= 128 ? 16 : 32) && !legacy) {
+    static int cap = 0;
+    if (cap == 0) {
+      int per_cu = 0, dev = 0, ncu = 0;
+      ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decim_w<32, true, false>, 64, 0));
+      ORION_HIP(hipGetDevice(&dev));
+      ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      cap = std::max(4, per_cu & ~3) * std::max(1, ncu);  // a multiple of 4 per CU: balanced SIMDs
+    }
+    const long long tiles_ch = (n_out + 127) / 128;
+    long long N = (tiles_ch * nch + cap - 1) / cap;
+    N = (N + 1) & ~1LL;  // tiles per wave, even
+    const long long L = N * 128;
+    const long long wpc = (n_out + L - 1) / L;
+    const long long grid = wpc * nch;
+    if (grid > (1LL << 31) - 1) throw HipError("decimator grid too large");
+    const bool clamp = n < 2 * 1024;
+    const int gi = static_cast<int>(grid), wi = static_cast<int>(wpc);
+#define ORION_DW(QQ)                                                                                        \
+  if (clamp) {                                                                                              \
+    if (a16) k_decim_w<QQ, true, true><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
+    else k_decim_w<QQ, false, true><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
+  } else {                                                                                                  \
+    if (a16) k_decim_w<QQ, true, false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
+    else k_decim_w<QQ, false, false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
+  }
+    if (K <= 128) { ORION_DW(16) } else { ORION_DW(32) }
+#undef ORION_DW
+  } else if (M == 8 && K <= 256 && hist_len >= 8 * (K <= 128 ? 16 : 32)) {
     const long long tiles = (n_out + 511) / 512;
     long long gx = tiles;
     const long long cap = (4 * kMaxGrid) / nch > 0 ? (4 * kMaxGrid) / nch : 1;

@@ -82,7 +82,6 @@ struct Fw {
   static_assert((R % 2) == 0 && NEW <= kWbfmNS, "phasor table covers the tile");
 };
 
-__device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Lane l receives lane l-1's value; lane 0 receives `first` (DPP wave_shr:1).
 __device__ __forceinline__ float wave_shr1(float v, float first) {
