@@ -28,6 +28,7 @@ __all__ = [
     "FmQuadratureDemod", "PmQuadratureDemod", "SsbProductDemod", "AmEnvelopeDemod",
     "CwEnvelopeDemod", "WbfmChain", "fir_lowpass_design", "kaiser_lowpass_taps",
     "kaiser_transition_norm", "kaiser_num_taps", "lp_cascade_design", "lib_path", "OrionError",
+    "AudioToIqChain", "IqToIqChain", "IqToAudioChain", "Graph",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -359,6 +360,76 @@ class WbfmChain(_Block):
         cap on the segmented kernel's waves (include/orion_sdr_amd.h)."""
         _check(_L.orion_wbfm_chain_configure(self._h, self._PATHS[path], int(max_segments)))
         return self
+
+
+# ---- chains (src/core.rs:24-109) and block graphs -------------------------------
+class _Chain:
+    """core.rs:24-109: a chain wraps one block and returns a new array per call.
+    Deliberate divergence from the reference: the reference returns out[..n]
+    (n = input length) even when the block wrote fewer samples (a decimator
+    then leaks stale samples, core.rs:70-77); here the result is
+    out[:out_written]."""
+
+    _in = _out = None
+
+    def __init__(self, block: _Block):
+        if block._in is not self._in or block._out is not self._out:
+            raise TypeError(f"{type(self).__name__} needs a {np.dtype(self._in).name} -> "
+                            f"{np.dtype(self._out).name} block, got {block.name}")
+        self.block = block
+
+    def process(self, x):
+        return self.block.process(x)
+
+    process_ref = process
+
+    def process_into(self, x: np.ndarray, out: np.ndarray) -> WorkReport:
+        return self.block.process_into(x, out)
+
+
+class AudioToIqChain(_Chain):
+    """core.rs:24-53 (f32 -> cf32)."""
+    _in, _out = np.float32, np.complex64
+
+
+class IqToIqChain(_Chain):
+    """core.rs:55-80 (cf32 -> cf32)."""
+    _in, _out = np.complex64, np.complex64
+
+
+class IqToAudioChain(_Chain):
+    """core.rs:82-109 (cf32 -> f32)."""
+    _in, _out = np.complex64, np.float32
+
+
+class Graph:
+    """A linear graph of blocks run back to back on the device: the input is
+    staged to HBM once, every intermediate stays there (each stage's output is
+    the next one's input, honouring out_written), and only the last output
+    returns to the host. The user-composed chains of docs/demodulate.md:128-133
+    (e.g. Rotator -> FirDecimator -> FmQuadratureDemod -> FirLowpass) run this
+    way; blocks keep their streaming state across calls as usual."""
+
+    def __init__(self, *blocks: _Block):
+        if not blocks:
+            raise ValueError("Graph needs at least one block")
+        for a, b in zip(blocks, blocks[1:]):
+            if a._out is not b._in:
+                raise TypeError(f"{a.name} outputs {np.dtype(a._out).name}, {b.name} takes {np.dtype(b._in).name}")
+        self.blocks = list(blocks)
+
+    def process(self, x):
+        import torch
+
+        host = not _is_torch(x)
+        if host:
+            x = self.blocks[0]._validate(x)
+            cur = torch.from_numpy(np.ascontiguousarray(x)).to("cuda")
+        else:
+            cur = x
+        for b in self.blocks:
+            cur = b.process_device(cur)
+        return cur.cpu().numpy() if host else cur
 
 
 # ---- designs (host) ----------------------------------------------------------

@@ -327,6 +327,29 @@ def test_wbfm_configure_errors(gpu_lib):
     assert gpu_lib._L.orion_wbfm_chain_configure(fm._h, 0, 0) == -4  # ORION_E_TYPE: not a WBFM chain
 
 
+# ---- chains and block graphs (core.rs:24-109; BASELINE C1 plumbing) ---------------------
+def test_chains_and_graph(gpu_lib, oracle):
+    """C1 (127-tap FirLowpassIq over 2^20 cf32) through IqToIqChain; the WBFM
+    receiver composed of four separate blocks in a device Graph equals the fused
+    chain; chains return out_written samples (tests/unit/chains.rs:10-33, with
+    the decimator divergence documented in _Chain)."""
+    n = 1 << 20
+    t = np.arange(n, dtype=np.float32)
+    x = (np.exp(2j * np.pi * 0.03 * t).astype(np.complex64) + cnoise(n, 0.07)).astype(np.complex64)
+    ch = gpu_lib.IqToIqChain(gpu_lib.FirLowpassIq.design(127, 0.2, 60.0))
+    ref = oracle.fir_lowpass_iq(x, oracle.kaiser_lowpass_taps(127, 0.2, 60.0))
+    report("C1 IqToIqChain FirLowpassIq(127) nrmse", nrmse(ch.process(x), ref), 1e-6)
+    assert gpu_lib.IqToAudioChain(gpu_lib.FmQuadratureDemod(FS, 2500, 5000)).process(x[:4096]).shape == (4096,)
+    assert gpu_lib.IqToIqChain(gpu_lib.FirDecimator(96e3, 4, 10.8e3, 2.4e3)).process(x[:4096]).shape == (1024,)
+    with pytest.raises(TypeError):
+        gpu_lib.IqToAudioChain(gpu_lib.FirLowpassIq.design(31, 0.2, 60.0))
+    iq = wbfm_input(1 << 18)
+    g = gpu_lib.Graph(gpu_lib.Rotator(-1.5e6, 10e6), gpu_lib.FirDecimator(10e6, 8, 200e3, 79e3),
+                      gpu_lib.FmQuadratureDemod(1.25e6, 75e3, 15e3), gpu_lib.FirLowpass(1.25e6, 15e3, 10e3))
+    got = np.concatenate([g.process(iq[: 1 << 17]), g.process(iq[1 << 17:])])
+    report("WBFM as a 4-block device graph vs oracle nrmse", nrmse(got, oracle.wbfm(iq)), 1e-5)
+
+
 # ---- Python API contract (python/tests/test_unit.py:37-127) ----------------------------
 def test_api_validation(gpu_lib):
     N = 4096
