@@ -84,7 +84,49 @@ __device__ __forceinline__ void stage(const ScanArgs& a, int ch, long long base,
   f2 Swg = f2{1.0f, 0.0f};
   if constexpr (PR == Pre::Ssb || PR == Pre::Fm)
     Swg = phasor_q64(static_cast<uint64_t>(a.k0 + base + 1), a.step);
-  for (int e = threadIdx.x; e < cnt; e += NT) sb[pos(e)] = premap<PR>(a, ch, base + e, base, Swg);
+  if constexpr (PR == Pre::Fm || PR == Pre::Pm) {
+    for (int e = threadIdx.x; e < cnt; e += NT) sb[pos(e)] = premap<PR>(a, ch, base + e, base, Swg);
+  } else {
+    // all of the thread's loads first (fixed trip count, unrolled): one memory
+    // round trip per chunk instead of one per sample
+    constexpr int K = CH / NT;
+    if constexpr (PR == Pre::Real) {
+      const float* __restrict__ x = static_cast<const float*>(a.x) + ch * a.x_stride + base;
+      float v[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int e = threadIdx.x + k * NT;
+        v[k] = e < cnt ? x[e] : 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) sb[pos(threadIdx.x + k * NT)] = v[k];
+    } else {
+      const f2* __restrict__ x = static_cast<const f2*>(a.x) + ch * a.x_stride + base;
+      f2 v[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int e = threadIdx.x + k * NT;
+        v[k] = e < cnt ? x[e] : f2{0.0f, 0.0f};
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int e = threadIdx.x + k * NT;
+        const f2 z = v[k];
+        float o;
+        if constexpr (PR == Pre::Ssb) {
+          const f2 p = cmul(Swg, a.tab[e]);
+          o = __builtin_fmaf(z.x, p.x, z.y * p.y);  // ssb.rs:37
+        } else if constexpr (PR == Pre::AmSqrt) {
+          o = __builtin_fmaf(z.x, z.x, z.y * z.y);  // am.rs:204
+        } else if constexpr (PR == Pre::AmAbs) {
+          o = __builtin_fmaf(a.c.k1, fabsf(z.x), a.c.k2 * fabsf(z.y));  // am.rs:238
+        } else {
+          o = sqrtf(z.x * z.x + z.y * z.y);  // cw.rs:38
+        }
+        sb[pos(e)] = o;
+      }
+    }
+  }
 }
 
 template <Post PO>
@@ -417,7 +459,7 @@ __global__ __launch_bounds__(NT) void k_lpdc_sp(const ScanArgs a, const double* 
     wm = m2;
     wd = d2;
   }
-  if (t == 0) {  // chunk aggregate, look-back, prefix
+  if (wave == 0) {  // chunk aggregate, look-back (one wave, 64 predecessors per step), prefix
     double bm = 1.0, bd = 0.0;
     for (int w = 0; w < 4; ++w) {
       double m2 = dtot[w][0], d2 = dtot[w][1];
@@ -427,31 +469,55 @@ __global__ __launch_bounds__(NT) void k_lpdc_sp(const ScanArgs a, const double* 
     }
     uint32_t* my = rec + (static_cast<long long>(ch) * nchunk + c) * 8;
     if (!last) {
-      sp_st64(my, bd);
-      sp_st64(my + 2, bm);
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the record is visible before its flag
-      sp_st(my + 6, epoch);
-    }
-    double excl = 0.0, mult = 1.0;
-    int k = c - 1;
-    for (; k >= 0; --k) {
-      const uint32_t* pr = rec + (static_cast<long long>(ch) * nchunk + k) * 8;
-      int it = 0;
-      while (sp_ld(pr + 6) != epoch && sp_ld(pr + 7) != epoch && ++it < (1 << 22)) __builtin_amdgcn_s_sleep(2);
-      if (sp_ld(pr + 7) == epoch) {
-        excl = __builtin_fma(mult, sp_ld64(pr + 4), excl);
-        break;
+      if (lane == 0) {
+        sp_st64(my, bd);
+        sp_st64(my + 2, bm);
       }
-      excl = __builtin_fma(mult, sp_ld64(pr), excl);
-      mult *= sp_ld64(pr + 2);
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the record is visible before its flag
+      if (lane == 0) sp_st(my + 6, epoch);
     }
-    if (k < 0) excl = __builtin_fma(mult, static_cast<double>(ci[5]), excl);  // the carried y1
-    if (!last) {
+    // lane i looks at chunk k = base - i; the nearest chunk with a prefix (or
+    // the carried state before chunk 0) closes the walk:
+    //   excl = sum_{i <= first} (prod_{j < i} r^len_j) v_i
+    double excl = 0.0, mult = 1.0;
+    for (int base = c - 1;; base -= 64) {
+      const int k = base - lane;
+      double v = 0.0, mk = 1.0;
+      bool closes = true;
+      if (k >= 0) {
+        const uint32_t* pr = rec + (static_cast<long long>(ch) * nchunk + k) * 8;
+        int it = 0;
+        while (sp_ld(pr + 6) != epoch && sp_ld(pr + 7) != epoch && ++it < (1 << 22)) __builtin_amdgcn_s_sleep(2);
+        closes = sp_ld(pr + 7) == epoch;
+        v = closes ? sp_ld64(pr + 4) : sp_ld64(pr);
+        mk = closes ? 1.0 : sp_ld64(pr + 2);
+      } else {
+        v = static_cast<double>(ci[5]);  // the carried y1
+      }
+      const unsigned long long bal = __ballot(closes);
+      const int first = bal ? __builtin_ctzll(bal) : 64;
+      // exclusive product of the multipliers over lanes (multiplicative scan)
+      double pm = mk;
+#pragma unroll
+      for (int s2 = 0; s2 < 6; ++s2) {
+        const double o = __shfl_up(pm, 1 << s2, 64);
+        if (lane >= (1 << s2)) pm *= o;
+      }
+      double ep = __shfl_up(pm, 1, 64);
+      if (lane == 0) ep = 1.0;
+      double term = lane <= first ? ep * v : 0.0;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) term += __shfl_xor(term, off, 64);
+      excl = __builtin_fma(mult, term, excl);
+      if (first < 64) break;
+      mult *= __shfl(pm, 63, 64);
+    }
+    if (!last && lane == 0) {
       sp_st64(my + 4, __builtin_fma(bm, excl, bd));
       __builtin_amdgcn_s_waitcnt(0x0F70);
       sp_st(my + 7, epoch);
     }
-    excl_sh = excl;
+    if (lane == 0) excl_sh = excl;
   }
   __syncthreads();
   // the state entering this lane: exclusive pair within the block applied to excl
