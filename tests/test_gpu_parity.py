@@ -327,6 +327,48 @@ def test_wbfm_configure_errors(gpu_lib):
     assert gpu_lib._L.orion_wbfm_chain_configure(fm._h, 0, 0) == -4  # ORION_E_TYPE: not a WBFM chain
 
 
+# ---- device-resident path (orion_block_process_device) ---------------------------------
+def test_device_path_alignment_and_capacity(gpu_lib, oracle):
+    """process_device on torch tensors: 16-B aligned and 8-B aligned (x[1:], the
+    non-A16 kernels) inputs, calls chained on the device, and an output capacity
+    below ceil(n/8) (out_written = min(ceil(n/8), cap), decim.rs:66-67)."""
+    import torch
+
+    n = 300_008
+    x = wbfm_input(n + 1)
+    xd = torch.from_numpy(x).cuda()
+    ref = oracle.wbfm(x[1:])
+    for path in ("segmented", "ranges", "split"):
+        W = gpu_lib.WbfmChain().configure(path)
+        got = torch.cat([W.process_device(xd[1 + i: 1 + i + 100_000]) for i in range(0, n, 100_000)])
+        report(f"wbfm device path={path} unaligned chained nrmse", nrmse(got.cpu().numpy(), ref), 1e-5)
+    W = gpu_lib.WbfmChain()
+    got = W.process_device(xd[:n]).cpu().numpy()
+    report("wbfm device aligned nrmse", nrmse(got, oracle.wbfm(x[:n])), 1e-5)
+    W.reset()
+    out = torch.empty(1000, dtype=torch.float32, device="cuda")
+    res = W.process_device(xd[:n], out)
+    assert res.shape == (1000,)
+    report("wbfm device truncated capacity nrmse", nrmse(res.cpu().numpy(), oracle.wbfm(x[:n])[:1000]), 1e-5)
+    D = gpu_lib.FirDecimator(10e6, 8, 200e3, 79e3)
+    got = D.process_device(xd[1:1 + 65_536]).cpu().numpy()
+    report("decimator device unaligned nrmse", nrmse(got, oracle.fir_decimator(x[1:1 + 65_536], 10e6, 8, 200e3, 79e3)),
+           1e-6)
+    a = real_tone(FS, 1200.0, 50_001, 0.4)
+    iq = oracle.ssb_mod(a, FS, 2800.0, 1500.0)
+    iqd = torch.from_numpy(np.concatenate([[0], iq]).astype(np.complex64)).cuda()
+    got = gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0).process_device(iqd[1:]).cpu().numpy()
+    report("ssb device unaligned nrmse", nrmse(got, oracle.ssb_demod(iq, FS, 1500.0, 2800.0)), 1e-4)
+
+
+def test_wbfm_tiny_inputs(gpu_lib, oracle):
+    """Calls shorter than one decimation period, and one sample at a time."""
+    x = wbfm_input(4001)
+    for chunk in (1, 7, 9, 64):
+        got = stream(gpu_lib.WbfmChain(), x[:1200], chunk)
+        report(f"wbfm streamed chunk={chunk} nrmse", nrmse(got, oracle.wbfm(x[:1200], chunk=chunk)), 1e-5)
+
+
 # ---- chains and block graphs (core.rs:24-109; BASELINE C1 plumbing) ---------------------
 def test_chains_and_graph(gpu_lib, oracle):
     """C1 (127-tap FirLowpassIq over 2^20 cf32) through IqToIqChain; the WBFM
