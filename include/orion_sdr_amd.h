@@ -119,6 +119,7 @@ orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float*
 #define ORION_WBFM_RANGES 2     /* one kernel, one wave per 2048-output range */
 #define ORION_WBFM_SPLIT 3      /* two kernels (front, back), any IIR design */
 #define ORION_WBFM_SEGMENTED_V1 4
+#define ORION_WBFM_SPECIALIZED 5  /* one kernel, streaming and back waves per CU */
 int orion_wbfm_chain_configure(orion_block* b, int path, int max_segments);
 
 /* ---- Block contract (core.rs:12-22) ------------------------------------ */

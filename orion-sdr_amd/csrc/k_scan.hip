@@ -8,6 +8,12 @@ constexpr int C = kScanC;
 constexpr int NT = kScanNT;
 constexpr int CH = kScanCH;
 constexpr int PADN = CH + CH / 16 + 16;
+#ifndef ORION_SP_ABL
+#define ORION_SP_ABL 0  // timing experiments only: 1 no phasor table, 2 no look-back, 4 no LP scan
+#endif
+#ifndef ORION_SP_TAB2
+#define ORION_SP_TAB2 0
+#endif
 
 __device__ __forceinline__ int pos(int e) { return e + (e >> 4); }
 
@@ -102,6 +108,10 @@ __device__ __forceinline__ void stage(const ScanArgs& a, int ch, long long base,
       for (int k = 0; k < K; ++k) sb[pos(threadIdx.x + k * NT)] = v[k];
     } else {
       const f2* __restrict__ x = static_cast<const f2*>(a.x) + ch * a.x_stride + base;
+#if ORION_SP_TAB2
+      f2 St = f2{1.0f, 0.0f};
+      if constexpr (PR == Pre::Ssb) St = cmul(Swg, a.tab[threadIdx.x]);
+#endif
       f2 v[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -114,7 +124,13 @@ __device__ __forceinline__ void stage(const ScanArgs& a, int ch, long long base,
         const f2 z = v[k];
         float o;
         if constexpr (PR == Pre::Ssb) {
+#if ORION_SP_ABL & 1
+          const f2 p = Swg;
+#elif ORION_SP_TAB2
+          const f2 p = cmul(St, a.tab[k * NT]);
+#else
           const f2 p = cmul(Swg, a.tab[e]);
+#endif
           o = __builtin_fmaf(z.x, p.x, z.y * p.y);  // ssb.rs:37
         } else if constexpr (PR == Pre::AmSqrt) {
           o = __builtin_fmaf(z.x, z.x, z.y * z.y);  // am.rs:204
@@ -383,9 +399,11 @@ __global__ __launch_bounds__(NT) void k_lpdc_sp(const ScanArgs a, const double* 
 #pragma unroll
   for (int i = 0; i < C; ++i) xs[i] = sb[pos(t * C + i)];
   float s0[S] = {0, 0, 0, 0};
+#if !(ORION_SP_ABL & 4)
 #pragma unroll
   for (int i = 0; i < C; ++i)
     if (t * C + i < cnt) (void)lp.step(s0, xs[i]);
+#endif
   double q[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) q[i] = s0[i];
@@ -480,7 +498,7 @@ __global__ __launch_bounds__(NT) void k_lpdc_sp(const ScanArgs a, const double* 
     // the carried state before chunk 0) closes the walk:
     //   excl = sum_{i <= first} (prod_{j < i} r^len_j) v_i
     double excl = 0.0, mult = 1.0;
-    for (int base = c - 1;; base -= 64) {
+    for (int base = c - 1; !(ORION_SP_ABL & 2); base -= 64) {
       const int k = base - lane;
       double v = 0.0, mk = 1.0;
       bool closes = true;

@@ -23,6 +23,9 @@
 //     1024-output sub-ranges, the IIR between tiles and the audio FIR spread
 //     over the next sub-range's tiles; a segment's first sub-range is handed to
 //     its predecessor (see the comment at the kernel).
+//   k_wbfm_ws    — wave-specialised segments: 8 streaming waves and 4 back
+//     waves per CU, phi through an LDS ring (ORION_WBFM_SPECIALIZED; timing
+//     experiment, slower than k_wbfm_seg2: see DESIGN.md §5).
 //   k_wbfm_seg   — the same segments with each sub-range's whole back run at
 //     once and the first sub-range deferred to the end (ORION_WBFM_SEGMENTED_V1).
 //   k_wbfm_fused — one wave per 2048-output range, two rounds of waves, zero-
@@ -723,8 +726,28 @@ struct FuPrefetch {  // where the tile two ahead starts
 #define ORION_FU_ABL 0  // timing experiments only (separate builds): 2 no decim FIR, 4 no staging
 #endif
 
-template <bool A16, bool CLAMP>
-__device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, long long jd0, const f2 (&ph)[8][2],
+// Per-lane staging phasors of a tile, ph(k, r) = e^{j theta (8Q + 2l + r + 128 k)}:
+// held in 32 registers (PhArr) or formed per tile from the lane's two base
+// phasors and the uniform e^{j theta 128 k} (PhGen: same products, same bits).
+struct PhArr {
+  const f2 (&p)[8][2];
+  __device__ __forceinline__ f2 operator()(int k, int r) const { return p[k][r]; }
+};
+struct PhGen {
+  f2 tb0, tb1;
+  const f2* __restrict__ tabc;
+  __device__ __forceinline__ f2 operator()(int k, int r) const { return cmul(r ? tb1 : tb0, tabc[128 * k]); }
+  // a copy the compiler cannot see through: keeps the products inside the tile
+  // loop (hoisted, they would occupy the 32 registers this form saves)
+  __device__ __forceinline__ PhGen opaque() const {
+    PhGen q = *this;
+    asm volatile("" : "+v"(q.tb0.x), "+v"(q.tb0.y), "+v"(q.tb1.x), "+v"(q.tb1.y));
+    return q;
+  }
+};
+
+template <bool A16, bool CLAMP, class PH>
+__device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, long long jd0, const PH& ph,
                                         f2 (&v)[8][2], const FuPrefetch& pf, f2 Sv, f2& carry, f2& dA,
                                         float* __restrict__ phit, int svi) {
   using G = fu::G;
@@ -752,8 +775,8 @@ __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, 
       if (k == 0) U[T.s1] = v[0][1] + v[1][1] + v[2][1] + v[3][1] + v[4][1] + v[5][1] + v[6][1] + v[7][1];
       continue;
     }
-    U[T.s0 + 16 * k] = cmul_rot_pk(v[k][0], ph[k][0]);
-    U[T.s1 + 16 * k] = cmul_rot_pk(v[k][1], ph[k][1]);
+    U[T.s0 + 16 * k] = cmul_rot_pk(v[k][0], ph(k, 0));
+    U[T.s1 + 16 * k] = cmul_rot_pk(v[k][1], ph(k, 1));
     if (k % 4 == 3) asm volatile("" ::: "memory");
   }
   asm volatile("" ::: "memory");
@@ -918,8 +941,8 @@ __device__ __forceinline__ void fu_front_range(const WbfmArgs& a, const WbfmFron
     const FuPrefetch dummy{org.xl, org.nl, -8LL * Q, true};
     if (n + 2 >= N) p0 = nx.on ? FuPrefetch{nx.xl, nx.nl, nx.porg, true} : dummy;
     if (n + 3 >= N) p1 = nx.on ? FuPrefetch{nx.xl, nx.nl, nx.porg + G::NEW, true} : dummy;
-    fu_tile<A16, CLAMP>(T, n, porg, jd0, ph, va, p0, Sv, carry, dA, T.Phi + G::TW * n, n);
-    fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + G::TW, ph, vb, p1, Sv, carry, dA, T.Phi + G::TW * (n + 1),
+    fu_tile<A16, CLAMP>(T, n, porg, jd0, PhArr{ph}, va, p0, Sv, carry, dA, T.Phi + G::TW * n, n);
+    fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + G::TW, PhArr{ph}, vb, p1, Sv, carry, dA, T.Phi + G::TW * (n + 1),
                         n + 1);
   }
   dlast = carry;
@@ -1565,8 +1588,8 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
       const FuPrefetch p0 = n + 2 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 2 * G::NEW, true} : dummy;
       const FuPrefetch p1 = n + 3 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 3 * G::NEW, true} : dummy;
       float* dst = dst0 + TW * tin;
-      fu_tile<A16, CLAMP>(T, n, porg, jd0, ph, va, p0, Sv, carry, dA, dst, n & 63);
-      fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + TW, ph, vb, p1, Sv, carry, dA, dst + TW, (n + 1) & 63);
+      fu_tile<A16, CLAMP>(T, n, porg, jd0, PhArr{ph}, va, p0, Sv, carry, dA, dst, n & 63);
+      fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + TW, PhArr{ph}, vb, p1, Sv, carry, dA, dst + TW, (n + 1) & 63);
     }
     {  // sub-range `sub` complete: its back, with two tiles in flight
       if (sub == 0) {
@@ -1629,19 +1652,20 @@ namespace sg2 {
 using Y = sg::Y;  // L 1024, NH 512, CH 8
 constexpr int L = Y::L, NH = Y::NH, CH = Y::CH;
 
-// LpCascade states of one sub-range from its exact entering state s_in, with no
+// LpCascade states of one sub-range (phi halves PhA = [0, NH), PhB = [NH, L))
+// from its exact entering state s_in, with no
 // per-lane transition matrices (those are vector loads, which would queue behind
 // the in-flight tile prefetch): s_in is folded into lane 0 of half A's
 // Kogge-Stone scan, half A's end state into lane 0 of half B's. xs = the lane's
 // two chunks (half A, half B); ef = the state entering each (.x A, .y B), f32;
 // end = the state after the sub-range (f64, wave-uniform).
-__device__ __forceinline__ void scan_states(const WbfmFusedConst& Bc, const float* __restrict__ Phi, int l,
-                                            const double (&s_in)[4], f2 (&xs)[CH], f2 (&ef)[4],
-                                            double (&end)[4]) {
+__device__ __forceinline__ void scan_states(const WbfmFusedConst& Bc, const float* __restrict__ PhA,
+                                            const float* __restrict__ PhB, int l, const double (&s_in)[4],
+                                            f2 (&xs)[CH], f2 (&ef)[4], double (&end)[4]) {
 #pragma unroll
   for (int i = 0; i < CH; i += 4) {
-    const f4 u = *reinterpret_cast<const f4*>(Phi + CH * l + i);
-    const f4 w = *reinterpret_cast<const f4*>(Phi + NH + CH * l + i);
+    const f4 u = *reinterpret_cast<const f4*>(PhA + CH * l + i);
+    const f4 w = *reinterpret_cast<const f4*>(PhB + CH * l + i);
     xs[i] = f2{u.x, w.x};
     xs[i + 1] = f2{u.y, w.y};
     xs[i + 2] = f2{u.z, w.z};
@@ -1676,12 +1700,12 @@ __device__ __forceinline__ void scan_states(const WbfmFusedConst& Bc, const floa
 // Zero-state pass of a segment's first sub-range: its zero-state end state sw
 // and zero-state last 128 outputs hist (f[L - 128 + l + 64 r]); tmp: 128 floats
 // of free LDS.
-__device__ __forceinline__ void zs_first(const WbfmFusedConst& Bc, const float* Phi, float* tmp, int l,
-                                         double (&sw)[4], float (&hist)[2]) {
+__device__ __forceinline__ void zs_first(const WbfmFusedConst& Bc, const float* PhA, const float* PhB, float* tmp,
+                                         int l, double (&sw)[4], float (&hist)[2]) {
   constexpr int TL = 64 - fu::PB / CH;  // lanes whose half-B chunk lies in the last 128
   const double zero[4] = {0, 0, 0, 0};
   f2 xs[CH], ef[4];
-  scan_states(Bc, Phi, l, zero, xs, ef, sw);
+  scan_states(Bc, PhA, PhB, l, zero, xs, ef, sw);
   const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
 #pragma unroll
   for (int i = 0; i < CH; ++i) {
@@ -1700,10 +1724,11 @@ __device__ __forceinline__ void zs_first(const WbfmFusedConst& Bc, const float* 
 // f[Lr - 128 + l + 64 r] in hist. chan_last: also the carried IIR state and FIR
 // history of the next call.
 __device__ __forceinline__ void iir(const WbfmArgs& a, const WbfmFusedConst& Bc, int ch, int Lr, bool chan_last,
-                                    const float* Phi, f2* P, int l, double (&sw)[4], float (&hist)[2]) {
+                                    const float* PhA, const float* PhB, f2* P, int l, double (&sw)[4],
+                                    float (&hist)[2]) {
   f2 xs[CH], ef[4];
   double end[4];
-  scan_states(Bc, Phi, l, sw, xs, ef, end);
+  scan_states(Bc, PhA, PhB, l, sw, xs, ef, end);
   const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
   const int jl = Lr - 1;
   const int hl = jl < NH ? jl / CH : (jl - NH) / CH;  // the lane that computes f[jl]
@@ -1890,9 +1915,9 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
       const long long jd0 = g.A + static_cast<long long>(n) * TW;
       const FuPrefetch p0 = n + 2 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 2 * G::NEW, true} : dummy;
       const FuPrefetch p1 = n + 3 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 3 * G::NEW, true} : dummy;
-      fu_tile<A16, CLAMP>(T, n, porg, jd0, ph, va, p0, Sv, carry, dA, Phi + TW * tin, n & 63);
+      fu_tile<A16, CLAMP>(T, n, porg, jd0, PhArr{ph}, va, p0, Sv, carry, dA, Phi + TW * tin, n & 63);
       if (pend && !(ORION_SEG_ABL & 8)) sg2::fir_block(Bc, P, l, tin, acc);
-      fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + TW, ph, vb, p1, Sv, carry, dA, Phi + TW * (tin + 1),
+      fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + TW, PhArr{ph}, vb, p1, Sv, carry, dA, Phi + TW * (tin + 1),
                           (n + 1) & 63);
       if (pend && !(ORION_SEG_ABL & 8)) sg2::fir_block(Bc, P, l, tin + 1, acc);
     }
@@ -1904,13 +1929,13 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
     const int Lr = static_cast<int>(min(static_cast<long long>(sg2::L), g.B - A0));
     if (sub == 0 && !g.first) {
       // zero-state pass only; the phi go to the predecessor, which has the true state
-      sg2::zs_first(Bc, Phi, reinterpret_cast<float*>(P), l, sw, hist);
+      sg2::zs_first(Bc, Phi, Phi + sg2::NH, reinterpret_cast<float*>(P), l, sw, hist);
       uint32_t* slot = a.hand + static_cast<long long>(g.r) * sg2::L;
 #pragma unroll
       for (int i = 0; i < sg2::L / 64; ++i) fu::st_agent(slot + l + 64 * i, __float_as_uint(Phi[l + 64 * i]));
       fu::publish(a.flags + 3LL * g.r, a.epoch, l);
     } else if (!(ORION_SEG_ABL & 1)) {
-      sg2::iir(a, Bc, g.ch, Lr, g.last && sub == nsub - 1, Phi, P, l, sw, hist);
+      sg2::iir(a, Bc, g.ch, Lr, g.last && sub == nsub - 1, Phi, Phi + sg2::NH, P, l, sw, hist);
       pend = true;
       pA0 = A0;
       pLr = Lr;
@@ -1932,7 +1957,7 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
 #pragma unroll
     for (int i = 0; i < sg2::L / 64; ++i) Phi[l + 64 * i] = __uint_as_float(fu::ld_agent(slot + l + 64 * i));
     wave_lds_fence();
-    sg2::iir(a, Bc, g.ch, Lrs, s_last, Phi, P, l, sw, hist);
+    sg2::iir(a, Bc, g.ch, Lrs, s_last, Phi, Phi + sg2::NH, P, l, sw, hist);
 #pragma unroll 1
     for (int kb = 0; kb < 8; ++kb) sg2::fir_block(Bc, P, l, kb, acc);
     sg2::fir_store(a, g.ch, As, Lrs, l, acc);
@@ -1940,6 +1965,353 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
   fu::trace(a, g.r, 3);
 }
 
+// ---- k_wbfm_ws: wave-specialised segments ------------------------------------
+// One 12-wave workgroup per CU (3 waves per SIMD, <= 168 VGPRs each): waves 0-7
+// stream, each the front tiles of its own segment with two tiles of inputs in
+// flight (as many streaming waves per SIMD as k_wbfm_seg2, but none of them
+// stops for IIR or FIR work while it streams, which would let its prefetch run
+// dry); waves 8-11 each run the back (IIR, audio FIR) of two streams' sub-ranges
+// (streams w - 8 and w - 4, alternating), all but the last one of each.
+// Phi travel through a per-stream ring of three 512-float halves in LDS: the
+// front writes sub-range s into halves 2s, 2s+1 (mod 3) and bumps `prod`; the
+// back reads both halves into registers and bumps `cons`; the front re-uses a
+// half only once the sub-range that held it has been consumed, which leaves the
+// back a sub-range and a half of slack. A wave's DS operations complete in
+// order, so the phi land before the counter that announces them.
+// Segment ends: when a stream's tiles are done, its own wave runs the last
+// sub-range (the back parks the IIR state and FIR history in the free ring
+// half, then bumps `done`) and the successor segment's first sub-range, handed
+// over as in k_wbfm_seg2 (a segment's first sub-range goes to its predecessor,
+// which has the true state). Eight streaming waves share that tail work instead
+// of four back waves running four sub-ranges each.
+#ifndef ORION_WS_ABL
+#define ORION_WS_ABL 0  // timing experiments only: 1 back waves only release the ring, 2 fronts never wait
+#endif
+#ifndef ORION_WS_PRIO
+#define ORION_WS_PRIO 1  // 1: streaming waves take s_setprio 1; 2: back waves do; 0: neither
+#endif
+namespace ws {
+#ifndef ORION_WS_NFR
+#define ORION_WS_NFR 8  // streaming waves per workgroup: 8 (3 waves per SIMD) or 4 (2 per SIMD)
+#endif
+constexpr int NFR = ORION_WS_NFR;                 // streaming waves per workgroup
+constexpr int NBK = 4;                            // back waves
+constexpr int SPB = NFR / NBK;                    // streams per back wave (1 or 2)
+static_assert(SPB == 1 || SPB == 2, "geometry");
+#ifndef ORION_WS_D
+#define ORION_WS_D 2  // tiles in flight per streaming wave (2, or 4 with 4 streaming waves)
+#endif
+constexpr int D = ORION_WS_D;
+static_assert(D == 2 || D == 4, "prefetch depth divides the 8 tiles of a sub-range");
+constexpr int HALF = sg2::NH;                     // ring granule (512 phi)
+constexpr int UF = (fu::G::LDS_F2 + 1) & ~1;      // per-stream front image (16-B aligned)
+constexpr int PF = (sg2::Y::PSlots + 1) & ~1;     // per-back-wave FIR pair image
+static_assert(PF <= UF, "a stream's FIR pair image fits its front image");
+constexpr int kThreads = 64 * (NFR + NBK);
+__device__ __forceinline__ int lds_ld(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// bounded: a wait that never ends sets *err and lets the wave finish
+__device__ __forceinline__ void wait_ge(const int* p, int v, int* err) {
+  for (int it = 0; lds_ld(p) < v; ++it) {
+    if (it == (1 << 24)) {
+      __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+}
+
+// One sub-range's back from phi halves PhA, PhB: a segment's first sub-range
+// (not the channel's) is the zero-state pass and the hand-off to the
+// predecessor; any other runs the IIR, releases the phi (*rel = sub + 1, when
+// rel) and the audio FIR.
+__device__ __forceinline__ void job(const WbfmArgs& a, const WbfmFusedConst& Bc, const FuRange& g, int sub,
+                                    bool chan_last, const float* PhA, const float* PhB, f2* P, int l,
+                                    double (&sw)[4], float (&hist)[2], int* rel) {
+  const long long A0 = g.A + static_cast<long long>(sub) * sg2::L;
+  const int Lr = static_cast<int>(min(static_cast<long long>(sg2::L), g.B - A0));
+  if (sub == 0 && !g.first) {
+    sg2::zs_first(Bc, PhA, PhB, reinterpret_cast<float*>(P), l, sw, hist);
+    uint32_t* slot = a.hand + static_cast<long long>(g.r) * sg2::L;
+#pragma unroll
+    for (int i = 0; i < sg2::L / 64; ++i)
+      fu::st_agent(slot + l + 64 * i, __float_as_uint((i < 8 ? PhA : PhB - sg2::NH)[l + 64 * i]));
+    wave_lds_fence();
+    if (rel && l == 0) lds_st(rel, sub + 1);
+    fu::publish(a.flags + 3LL * g.r, a.epoch, l);
+  } else {
+    sg2::iir(a, Bc, g.ch, Lr, chan_last, PhA, PhB, P, l, sw, hist);
+    if (rel && l == 0) lds_st(rel, sub + 1);  // iir read the phi first (scan_states)
+    f2 acc[sg2::CH];
+#pragma unroll
+    for (int i = 0; i < sg2::CH; ++i) acc[i] = f2{0.0f, 0.0f};
+#pragma unroll 1
+    for (int kb = 0; kb < 8; ++kb) sg2::fir_block(Bc, P, l, kb, acc);
+    sg2::fir_store(a, g.ch, A0, Lr, l, acc);
+  }
+}
+}  // namespace ws
+
+template <bool A16, bool CLAMP>
+__global__ __launch_bounds__(ws::kThreads, 1) void k_wbfm_ws(const WbfmArgs a, const WbfmFrontConst C,
+                                                            const WbfmFusedConst Bk, int spc, int S, int nseg) {
+  using G = fu::G;
+  constexpr int TW = G::TW;
+  __shared__ __attribute__((aligned(16))) f2 Us[ws::NFR * ws::UF];
+  __shared__ __attribute__((aligned(16))) float Ring[ws::NFR][3][ws::HALF];
+  __shared__ __attribute__((aligned(16))) f2 Ps[ws::NBK * ws::PF];
+  __shared__ __attribute__((aligned(16))) float Gt[128];        // decimator taps (phase-major)
+  __shared__ __attribute__((aligned(16))) f2 SvL[ws::NFR][64];  // common phasors of 64 tiles
+  __shared__ __attribute__((aligned(16))) f4 TbL[ws::NFR][64];  // lane base phasors
+  __shared__ double SwL[ws::NBK][8];                            // back: parked IIR states
+  __shared__ int Sync[ws::NFR][3];  // [prod, cons, done] per stream
+  // the back's constants in LDS (read through a kernel-argument reference in two
+  // roles, the compiler copied them to scratch)
+  __shared__ __attribute__((aligned(16))) WbfmFusedConst Bc;
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x < 3 * ws::NFR) Sync[threadIdx.x / 3][threadIdx.x % 3] = 0;
+  if (threadIdx.x < 128) Gt[threadIdx.x] = C.g[threadIdx.x];
+  static_assert(sizeof(WbfmFusedConst) % 4 == 0 && sizeof(WbfmFusedConst) / 4 <= ws::kThreads, "one word per lane");
+  if (threadIdx.x < sizeof(WbfmFusedConst) / 4)
+    reinterpret_cast<uint32_t*>(&Bc)[threadIdx.x] = reinterpret_cast<const uint32_t*>(&Bk)[threadIdx.x];
+  __syncthreads();  // the only barrier: before any load is in flight
+  auto seg = [&](int f) {
+    FuRange g;
+    g.r = blockIdx.x * ws::NFR + f;
+    g.ch = g.r / spc;
+    g.wl = g.r - g.ch * spc;
+    g.A = static_cast<long long>(g.wl) * S;
+    g.B = min(g.A + S, a.n_dec);
+    g.Lr = static_cast<int>(g.B - g.A);
+    g.first = g.wl == 0;
+    g.last = g.B == a.n_dec;
+    return g;
+  };
+
+  if (w < ws::NFR) {  // ---- streaming wave ----
+    const int f = w;
+    if (blockIdx.x * ws::NFR + f >= nseg) return;
+    if (ORION_WS_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+    const FuRange g = seg(f);
+    fu::trace(a, g.r, 0);
+    int* prod = &Sync[f][0];
+    const int* cons = &Sync[f][1];
+    f2* U = Us + f * ws::UF;
+    const int nsub = (g.Lr + sg2::L - 1) / sg2::L;
+    const int ntiles = nsub * sg::NS;
+    const FuPrefetch org = fu_origin(a, g);
+    f2 v[ws::D][G::KL][2];
+#pragma unroll
+    for (int j = 0; j < ws::D; ++j) front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + j * G::NEW, l, v[j]);
+    const f2* __restrict__ tabc = a.tab + static_cast<long long>(g.ch) * kWbfmNS;
+    const f2* __restrict__ xc = a.x + g.ch * a.x_stride;
+    const f2* __restrict__ hc = a.hist_in + g.ch * kWbfmHist;
+    const f2 cn = tabc[G::NEW];
+    const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
+    // the tile's scatter slots, re-derived per tile from an opaque lane index
+    // (registers are the streaming wave's limit: a hoisted copy would spill)
+    auto tile = [&]() {
+      int lo = l;
+      asm volatile("" : "+v"(lo));
+      const int d0 = (-2 * lo) & 7, d1 = (-2 * lo - 1) & 7;
+      return FuTile{a, C, U, Ring[f][0], Gt, xc, hc, tabc, g.ch, lo, d0 * G::LR + (8 * Q + 2 * lo + d0) / 8,
+                    d1 * G::LR + (8 * Q + 2 * lo + 1 + d1) / 8, f2{cn.x, -cn.y}, g.first};
+    };
+    long long porg = org.porg;
+    {  // halo rows of the first tile (clamped here, exact via the boundary fixup)
+      const long long P0 = porg + 2 * l;
+      const long long hi = (org.nl & ~1LL) - 2;
+      const long long Pc = P0 < 0 ? 0 : (P0 > hi ? hi : P0);
+      const f2 x0 = org.xl[Pc], x1 = org.xl[Pc + 1];
+      const f4 th = *reinterpret_cast<const f4*>(tabc + 2 * l);
+      U[c0 * G::LR + (2 * l + c0) / 8] = cmul_rot(x0, f2{th.x, th.y});
+      U[c1 * G::LR + (2 * l + 1 + c1) / 8] = cmul_rot(x1, f2{th.z, th.w});
+    }
+    {  // p = -l (row c = l, i = 0), l = 1..7: used only by d[A-1]
+      const long long Pm = max(porg - (l & 7), 0LL);
+      const f2 xm = xc[Pm];
+      const f2 tc = tabc[l & 7];
+      if (!g.first && l >= 1 && l < 8) U[l * G::LR] = cmul_rot(xm, f2{tc.x, -tc.y});
+    }
+    // staging phasors formed per tile from the lane's two base phasors, parked
+    // in LDS (registers are the streaming wave's limit)
+    TbL[f][l] = *reinterpret_cast<const f4*>(tabc + 8 * Q + 2 * l);
+    auto ph = [&]() {
+      const f4 tv = TbL[f][l];
+      return PhGen{f2{tv.x, tv.y}, f2{tv.z, tv.w}, tabc};
+    };
+    f2 carry = f2{0.0f, 0.0f}, dA = f2{0, 0};
+    if (g.first) {  // d[-1]: the previous call's last decimated sample (fm.rs:29 on reset)
+      const float* __restrict__ ci = a.carry_in + g.ch * kWbfmCarry;
+      carry = f2{ci[4], ci[5]};
+    }
+    const FuPrefetch dummy{org.xl, org.nl, -8LL * Q, true};  // past the segment: an L2-resident tile
+#pragma unroll 1
+    for (int n = 0; n < ntiles; n += ws::D, porg += ws::D * G::NEW) {
+      if ((n & 63) == 0) {  // lane l: the common phasor of tile n + l (kept in LDS)
+        SvL[f][l] = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1 + static_cast<long long>(l) * G::NEW),
+                               a.step[g.ch]);
+        wave_lds_fence();
+      }
+#pragma unroll
+      for (int j = 0; j < ws::D; ++j) {
+        const int nj = n + j, sub = nj >> 3, tin = nj & 7;
+        // ring half 2 sub + (tin >= 4) re-uses the half of sub-range sub - 2 + (tin >= 4)
+        if (!(ORION_WS_ABL & 2) && tin == 0 && sub >= 2) ws::wait_ge(cons, sub - 1, a.err);
+        if (!(ORION_WS_ABL & 2) && tin == 4 && sub >= 1) ws::wait_ge(cons, sub, a.err);
+        float* phj = Ring[f][(2 * sub + (tin >> 2)) % 3] + TW * (tin & 3);
+        const long long pj = porg + j * G::NEW;
+        const FuPrefetch pf = nj + ws::D < ntiles ? FuPrefetch{org.xl, org.nl, pj + ws::D * G::NEW, true} : dummy;
+        fu_tile<A16, CLAMP>(tile(), nj, pj, g.A + static_cast<long long>(nj) * TW, ph(), v[j], pf,
+                            SvL[f][nj & 63], carry, dA, phj, 0);
+        if (tin == 7) {
+          wave_lds_fence();
+          if (l == 0) ws::lds_st(prod, sub + 1);
+        }
+      }
+    }
+    fu::trace(a, g.r, 1);
+    if (ORION_WS_ABL & 1) return;
+    // ---- the segment's last sub-range, then the successor's first ----
+    // (geometry re-derived from an opaque stream index: nothing stays live
+    // across the tile loop for this part)
+    int fo = __builtin_amdgcn_readfirstlane(f);
+    asm volatile("" : "+s"(fo));
+    const FuRange gt = seg(fo);
+    const int s = (gt.Lr + sg2::L - 1) / sg2::L - 1;
+    f2* P = reinterpret_cast<f2*>(Us + fo * ws::UF);  // the front image is free now
+    double sw[4] = {0, 0, 0, 0};
+    float hist[2] = {0, 0};
+    if (s > 0) {  // the back parked the state after sub-range s - 1
+      ws::wait_ge(&Sync[fo][2], 1, a.err);
+      const float* park = Ring[fo][(2 * s + 2) % 3];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sw[k] = sg::uni(reinterpret_cast<const double*>(park + 128)[k]);
+      hist[0] = park[l];
+      hist[1] = park[64 + l];
+    } else if (gt.first) {
+      const float* __restrict__ ci = a.carry_in + gt.ch * kWbfmCarry;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sw[k] = ci[k];
+      hist[0] = ci[8 + l];
+      hist[1] = ci[8 + 64 + l];
+    }
+    {
+      const float* PhA = Ring[fo][(2 * s) % 3];
+      const float* PhB = Ring[fo][(2 * s + 1) % 3];
+      const long long A0 = gt.A + static_cast<long long>(s) * sg2::L;
+      const int Lr = static_cast<int>(min(static_cast<long long>(sg2::L), gt.B - A0));
+      if (s == 0 && !gt.first) {
+        sg2::zs_first(Bc, PhA, PhB, reinterpret_cast<float*>(P), l, sw, hist);
+        uint32_t* slot = a.hand + static_cast<long long>(gt.r) * sg2::L;
+#pragma unroll
+        for (int i = 0; i < sg2::L / 64; ++i)
+          fu::st_agent(slot + l + 64 * i, __float_as_uint((i < 8 ? PhA : PhB - sg2::NH)[l + 64 * i]));
+        fu::publish(a.flags + 3LL * gt.r, a.epoch, l);
+      } else {
+        sg2::iir(a, Bc, gt.ch, Lr, gt.last, PhA, PhB, P, l, sw, hist);
+        f2 acc[sg2::CH];
+#pragma unroll
+        for (int i = 0; i < sg2::CH; ++i) acc[i] = f2{0.0f, 0.0f};
+#pragma unroll 1
+        for (int kb = 0; kb < 8; ++kb) sg2::fir_block(Bc, P, l, kb, acc);
+        sg2::fir_store(a, gt.ch, A0, Lr, l, acc);
+      }
+    }
+    fu::trace(a, gt.r, 2);
+    if (!gt.last) {
+      const long long As = gt.B, Bs = min(As + S, a.n_dec);
+      const int Lrs = static_cast<int>(min(static_cast<long long>(sg2::L), Bs - As));
+      const bool s_last = Bs == a.n_dec && Bs - As <= sg2::L;
+      float* Ph = Ring[fo][0];  // halves 0, 1: the ring is free
+      fu::wait_for(a.flags + 3LL * (gt.r + 1), a.epoch, a.err);
+      const uint32_t* slot = a.hand + static_cast<long long>(gt.r + 1) * sg2::L;
+      wave_lds_fence();  // the last job's LDS reads are done before the ring is overwritten
+#pragma unroll
+      for (int i = 0; i < sg2::L / 64; ++i) Ph[l + 64 * i] = __uint_as_float(fu::ld_agent(slot + l + 64 * i));
+      wave_lds_fence();
+      sg2::iir(a, Bc, gt.ch, Lrs, s_last, Ph, Ph + sg2::NH, P, l, sw, hist);
+      f2 acc[sg2::CH];
+#pragma unroll
+      for (int i = 0; i < sg2::CH; ++i) acc[i] = f2{0.0f, 0.0f};
+#pragma unroll 1
+      for (int kb = 0; kb < 8; ++kb) sg2::fir_block(Bc, P, l, kb, acc);
+      sg2::fir_store(a, gt.ch, As, Lrs, l, acc);
+    }
+    fu::trace(a, g.r, 3);
+    return;
+  }
+
+  // ---- back wave: sub-ranges 0 .. nsub-2 of streams b and b + NBK, alternating ----
+  const int b = w - ws::NFR;
+  if (ORION_WS_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+  f2* P = Ps + b * ws::PF;
+  auto nsub_of = [&](int q) {
+    const int f = b + ws::NBK * q;
+    return blockIdx.x * ws::NFR + f < nseg ? (seg(f).Lr + sg2::L - 1) / sg2::L : 0;
+  };
+  const int nsub0 = nsub_of(0), nsub1 = ws::SPB > 1 ? nsub_of(1) : 0;
+  if (nsub0 == 0) return;  // stream b + NBK exists only if stream b does
+  // per stream: the IIR state entering its next sub-range (parked in LDS: SGPRs
+  // are short here) and its FIR history (registers)
+  double* swL = SwL[b];
+  float hi0[2] = {0, 0}, hi1[2] = {0, 0};
+#pragma unroll
+  for (int q = 0; q < ws::SPB; ++q) {
+    const FuRange g = seg(b + ws::NBK * q);
+    const bool carried = (q ? nsub1 : nsub0) > 0 && g.first;
+    const float* __restrict__ ci = a.carry_in + g.ch * kWbfmCarry;
+    if (l < 4) swL[4 * q + l] = carried ? static_cast<double>(ci[l]) : 0.0;
+    float* hi = q ? hi1 : hi0;
+    hi[0] = carried ? ci[8 + l] : 0.0f;
+    hi[1] = carried ? ci[8 + 64 + l] : 0.0f;
+  }
+  wave_lds_fence();
+  const int nmax = max(nsub0, nsub1) - 1;
+#pragma unroll 1
+  for (int it = 0; it < ws::SPB * nmax; ++it) {
+    const int sub = ws::SPB > 1 ? it >> 1 : it, q = ws::SPB > 1 ? it & 1 : 0;
+    const int nsq = q ? nsub1 : nsub0;
+    if (sub >= nsq - 1) continue;
+    const int f = b + ws::NBK * q;
+    const FuRange g = seg(f);
+    double sw[4];
+    float hist[2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sw[k] = sg::uni(swL[4 * q + k]);
+    hist[0] = q ? hi1[0] : hi0[0];
+    hist[1] = q ? hi1[1] : hi0[1];
+    ws::wait_ge(&Sync[f][0], sub + 1, a.err);
+    const float* PhA = Ring[f][(2 * sub) % 3];
+    const float* PhB = Ring[f][(2 * sub + 1) % 3];
+    if (ORION_WS_ABL & 1) {
+      if (l == 0) ws::lds_st(&Sync[f][1], sub + 1);
+    } else {
+      ws::job(a, Bc, g, sub, false, PhA, PhB, P, l, sw, hist, &Sync[f][1]);
+    }
+    if (sub == nsq - 2) {  // the stream's last sub-range is its own wave's: park the state
+      float* park = Ring[f][(2 * sub + 4) % 3];
+      park[l] = hist[0];
+      park[64 + l] = hist[1];
+      if (l < 4) reinterpret_cast<double*>(park + 128)[l] = sw[l & 3];
+      wave_lds_fence();
+      if (l == 0) ws::lds_st(&Sync[f][2], 1);
+    } else {
+      if (l < 4) swL[4 * q + l] = sw[l & 3];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        hi0[k] = q ? hi0[k] : hist[k];
+        hi1[k] = q ? hist[k] : hi1[k];
+      }
+      wave_lds_fence();
+    }
+  }
+}
 }  // namespace
 
 namespace {
@@ -2029,6 +2401,43 @@ void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFused
   }
   if (spread) { ORION_SEG(k_wbfm_seg2) } else { ORION_SEG(k_wbfm_seg) }
 #undef ORION_SEG
+  ORION_LAUNCH_CHECK();
+}
+
+// k_wbfm_ws: one workgroup of 8 streaming + 4 back waves per CU, one round; the
+// segments as in launch_wbfm_seg with 8 per workgroup.
+void launch_wbfm_ws(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
+                    int max_segments, hipStream_t s) {
+  if (a.n_dec <= 0 || nch <= 0) return;
+  constexpr int kThreads = ws::kThreads;
+  static int cap = 0;
+  if (cap == 0) {
+    int per_cu = 0, dev = 0, ncu = 0;
+    ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_ws<true, false>, kThreads, 0));
+    ORION_HIP(hipGetDevice(&dev));
+    ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    cap = std::max(1, per_cu) * std::max(1, ncu) * ws::NFR;
+  }
+  const long long capx = max_segments > 0 ? std::min<long long>(max_segments, cap) : cap;
+  const long long nsub_ch = (a.n_dec + kSgL - 1) / kSgL;
+  long long spc = std::max<long long>(1, std::min<long long>(capx / nch, nsub_ch));
+  const long long S = (nsub_ch + spc - 1) / spc * kSgL;
+  spc = (a.n_dec + S - 1) / S;
+  const long long nseg = spc * nch;
+  // every segment's workgroup is resident at once (a back wave waits on its successor)
+  if (nseg > cap) throw HipError("WBFM: more segments than resident waves (too many channels)");
+  if (S > (1LL << 30)) throw HipError("WBFM segment geometry out of range");
+  const int grid = static_cast<int>((nseg + ws::NFR - 1) / ws::NFR);
+  const bool a16 = (reinterpret_cast<uintptr_t>(a.x) % 16 == 0) && (a.x_stride % 2 == 0);
+  const bool clamp = a.n < 2LL * Fw<2>::NEW;
+  const int sp = static_cast<int>(spc), Si = static_cast<int>(S), ns = static_cast<int>(nseg);
+  if (clamp) {
+    if (a16) k_wbfm_ws<true, true><<<grid, kThreads, 0, s>>>(a, f, b, sp, Si, ns);
+    else k_wbfm_ws<false, true><<<grid, kThreads, 0, s>>>(a, f, b, sp, Si, ns);
+  } else {
+    if (a16) k_wbfm_ws<true, false><<<grid, kThreads, 0, s>>>(a, f, b, sp, Si, ns);
+    else k_wbfm_ws<false, false><<<grid, kThreads, 0, s>>>(a, f, b, sp, Si, ns);
+  }
   ORION_LAUNCH_CHECK();
 }
 

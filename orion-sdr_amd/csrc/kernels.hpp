@@ -129,6 +129,10 @@ long long wbfm_seg_slots(long long n_dec, int nch);
 // handed to the predecessor); else k_wbfm_seg. max_segments > 0 caps the waves.
 void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
                      int max_segments, bool spread, hipStream_t s);
+// Wave-specialised segments (k_wbfm_ws): streaming and back waves in one
+// workgroup per CU; same geometry requirement and hand-off slots as k_wbfm_seg2.
+void launch_wbfm_ws(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
+                    int max_segments, hipStream_t s);
 void launch_wbfm_fused(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
                        hipStream_t s);
 

@@ -353,7 +353,7 @@ class WbfmChain(_Block):
             h = _L.orion_wbfm_chain_batch_new(C.byref(p), _fptr(offs), offs.size)
         super().__init__(h)
 
-    _PATHS = {"auto": 0, "segmented": 1, "ranges": 2, "split": 3, "segmented_v1": 4}
+    _PATHS = {"auto": 0, "segmented": 1, "ranges": 2, "split": 3, "segmented_v1": 4, "specialized": 5}
 
     def configure(self, path: str = "auto", max_segments: int = 0):
         """Engine tuning / tests (no reference counterpart): the kernel path and a

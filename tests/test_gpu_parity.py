@@ -297,6 +297,12 @@ def test_wbfm_full_size_windowed(gpu_lib, oracle):
     ("segmented", 7, 4097 * 8 + 5),  # one sub-range per segment, 2-output last segment
     ("segmented", 2, 8 * 1024 + 8),  # second segment of one output
     ("segmented_v1", 3, 1 << 20),
+    ("specialized", 3, 1 << 20),
+    ("specialized", 1, 600_000),
+    ("specialized", 7, 4097 * 8 + 5),
+    ("specialized", 2, 8 * 1024 + 8),
+    ("specialized", 6, 1 << 16),     # 6 segments in two workgroups, the second part-filled
+    ("specialized", 0, 1 << 20),     # the resident capacity: one sub-range per segment
     ("ranges", 0, 1 << 20),
     ("split", 0, 1 << 20)])
 def test_wbfm_kernel_paths(gpu_lib, oracle, path, max_seg, n):
@@ -306,18 +312,18 @@ def test_wbfm_kernel_paths(gpu_lib, oracle, path, max_seg, n):
     report(f"wbfm path={path} max_segments={max_seg} n={n} nrmse", nrmse(got, oracle.wbfm(x)), 1e-5)
 
 
-@pytest.mark.parametrize("max_seg", [2, 5])
-def test_wbfm_segmented_streaming_and_channels(gpu_lib, oracle, max_seg):
+@pytest.mark.parametrize("path,max_seg", [("segmented", 2), ("segmented", 5), ("specialized", 2), ("specialized", 5)])
+def test_wbfm_segmented_streaming_and_channels(gpu_lib, oracle, path, max_seg):
     """Carried state across calls and independent channels with several
     multi-sub-range segments per channel."""
     x = wbfm_input(700_000)
     for chunk in (300_003, 131_072):
-        got = stream(gpu_lib.WbfmChain().configure("segmented", max_seg), x, chunk)
-        report(f"wbfm segmented max_segments={max_seg} chunk={chunk} nrmse", nrmse(got, oracle.wbfm(x, chunk=chunk)), 1e-5)
+        got = stream(gpu_lib.WbfmChain().configure(path, max_seg), x, chunk)
+        report(f"wbfm {path} max_segments={max_seg} chunk={chunk} nrmse", nrmse(got, oracle.wbfm(x, chunk=chunk)), 1e-5)
     offs = np.array([1.5e6, -2.2e6, 0.7e6], np.float32)
     xc = np.stack([wbfm_input(1 << 18, f_off=float(f), seed=0x55 ^ c) for c, f in enumerate(offs)])
-    got = gpu_lib.WbfmChain(f_off=offs).configure("segmented", 3 * max_seg).process(xc)
-    report(f"wbfm segmented 3 ch max_segments={3 * max_seg} nrmse", nrmse(got, oracle.wbfm_channels(xc, offs, 3)), 1e-5)
+    got = gpu_lib.WbfmChain(f_off=offs).configure(path, 3 * max_seg).process(xc)
+    report(f"wbfm {path} 3 ch max_segments={3 * max_seg} nrmse", nrmse(got, oracle.wbfm_channels(xc, offs, 3)), 1e-5)
 
 
 def test_wbfm_configure_errors(gpu_lib):
