@@ -12,7 +12,7 @@ constexpr int PADN = CH + CH / 16 + 16;
 #define ORION_SP_ABL 0  // timing experiments only: 1 no phasor table, 2 no look-back, 4 no LP scan
 #endif
 #ifndef ORION_SP_TAB2
-#define ORION_SP_TAB2 0
+#define ORION_SP_TAB2 1  // SSB mixing phasor = (Swg tab[t]) tab[k NT]: one uniform table load per sample, not a per-lane one
 #endif
 
 __device__ __forceinline__ int pos(int e) { return e + (e >> 4); }
