@@ -11,6 +11,9 @@ constexpr int PADN = CH + CH / 16 + 16;
 #ifndef ORION_SP_ABL
 #define ORION_SP_ABL 0  // timing experiments only: 1 no phasor table, 2 no look-back, 4 no LP scan
 #endif
+#ifndef ORION_SP_WAVES
+#define ORION_SP_WAVES 1  // occupancy hint for k_lpdc_sp (experiments: 6)
+#endif
 #ifndef ORION_SP_TAB2
 #define ORION_SP_TAB2 1  // SSB mixing phasor = (Swg tab[t]) tab[k NT]: one uniform table load per sample, not a per-lane one
 #endif
@@ -372,7 +375,7 @@ __device__ __forceinline__ void dc_combine(double m1, double d1, double& m2, dou
 }
 
 template <Pre PR>
-__global__ __launch_bounds__(NT) void k_lpdc_sp(const ScanArgs a, const double* __restrict__ mlp, int nch,
+__global__ __launch_bounds__(NT, ORION_SP_WAVES) void k_lpdc_sp(const ScanArgs a, const double* __restrict__ mlp, int nch,
                                                uint32_t* __restrict__ rec, uint32_t epoch) {
   constexpr int S = 4;
   __shared__ float sb[PADN];
@@ -423,13 +426,18 @@ __global__ __launch_bounds__(NT) void k_lpdc_sp(const ScanArgs a, const double* 
 #pragma unroll
     for (int i = 0; i < S; ++i) cw[i] = v[i];
   }
+  // the wave's entering state folded into lane 0 and the wave re-scanned (a
+  // per-lane transition matrix would be 128 B of global reads per lane)
   double e[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) q[i] = s0[i];
+  if (lane == 0) matvec_acc<S>(mlp + ScanMatsLayout::kPwc * S * S, cw, q);  // pw[0] = A^C
+  wave_scan_inclusive<S>(q, mlp + ScanMatsLayout::kPwc * S * S, lane);
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     const double o = __shfl_up(q[i], 1, 64);
-    e[i] = lane == 0 ? 0.0 : o;
+    e[i] = lane == 0 ? cw[i] : o;
   }
-  matvec_acc<S>(mlp + (ScanMatsLayout::kLane + lane) * S * S, cw, e);
   float ef[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) ef[i] = static_cast<float>(e[i]);
