@@ -35,7 +35,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
            IFS=';' read -ra SETS <<< "${PMC_SETS:-$DEFAULT_PMC}"
            for set in "${SETS[@]}"; do
              i=$((i+1))
-             step pmc$i 600 rocprofv3 --pmc $set -d "$OUT/pmc$i" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ${BARGS:-} || exit $?
+             step pmc$i 600 rocprofv3 --pmc $set -f csv -d "$OUT/pmc$i" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ${BARGS:-} || exit $?
            done ;;
     list)  step list 120 rocprofv3 -L || exit $? ;;
     abl)   for v in ${ABLS:-0 1 2 4 8 3 14 15 16 32 48}; do  # timing ablations (k_wbfm.hip ABL)
