@@ -41,18 +41,28 @@ METRICS = {  # the non-default configs name what they measure
 }
 
 
-def wbfm_iq(n, f_off, dev, seed, fs=10e6):
+def _sum_sin(w, k):
+    """sum_{j < k} sin(w j), closed form (float64)."""
+    return np.sin(w * (k - 1) / 2) * np.sin(w * k / 2) / np.sin(w / 2) if k > 0 else 0.0
+
+
+def wbfm_iq(n, f_off, dev, seed, fs=10e6, t0=0, noise=0.0025):
     """C2 synthetic IQ generated on the device: FM (dev 75 kHz) of
-    0.5 sin(1 kHz) + 0.3 sin(7 kHz) at +f_off, plus complex AWGN (P = 0.0025)."""
-    t = torch.arange(n, device=dev, dtype=torch.float64) / fs
+    0.5 sin(1 kHz) + 0.3 sin(7 kHz) at +f_off, plus complex AWGN (P = 0.0025).
+    t0: index of the first sample within the stream (a time shard of it; the
+    FM phase accumulated before t0 is added in closed form)."""
+    t = (torch.arange(n, device=dev, dtype=torch.float64) + t0) / fs
     aud = 0.5 * torch.sin(2 * np.pi * 1e3 * t) + 0.3 * torch.sin(2 * np.pi * 7e3 * t)
-    ph = torch.cumsum(2 * np.pi * 75e3 / fs * aud, 0) + 2 * np.pi * f_off * t
+    k = 2 * np.pi * 75e3 / fs
+    ph0 = k * (0.5 * _sum_sin(2 * np.pi * 1e3 / fs, t0) + 0.3 * _sum_sin(2 * np.pi * 7e3 / fs, t0))
+    ph = torch.cumsum(k * aud, 0) + ph0 + 2 * np.pi * f_off * t
     del aud
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
     x = torch.polar(torch.ones_like(ph), ph).to(torch.complex64)
     del ph, t
-    x += (torch.randn(n, dtype=torch.complex64, device=dev, generator=g) * np.sqrt(0.0025)).to(torch.complex64)
+    if noise > 0:
+        x += (torch.randn(n, dtype=torch.complex64, device=dev, generator=g) * np.sqrt(noise)).to(torch.complex64)
     return x
 
 
@@ -78,8 +88,21 @@ def max_over_ranks(elapsed, dist, device):
     return float(tt.item())
 
 
-def make_workload(cfg, rank, dev, n_override=None, world=1):
-    """Returns (block, x, out, samples_per_step, bytes_per_sample, description)."""
+def make_workload(cfg, rank, dev, n_override=None, world=1, shard="stream"):
+    """Returns (block, x, samples_per_step, bytes_per_sample, description).
+    C2 on several ranks: shard="stream" cuts ONE stream of world x n samples in
+    time (rank r runs [start, stop) from a STREAM_HALO-sample halo,
+    sought to the halo start); shard="channels" gives each rank its own channel."""
+    if cfg == "c2" and world > 1 and shard == "stream":
+        n = n_override or (1 << 26)
+        start, stop, h = orion_sdr.stream_shard(world * n, rank, world)
+        blk = orion_sdr.WbfmChain(f_off=OFFSETS[0]).seek(h)
+        x = wbfm_iq(stop - h, OFFSETS[0], dev, 0x1234 + rank, t0=h)
+        desc = dict(workload="C2 WBFM chain on ONE stream cut in time: Rotator(-f_off) -> FirDecimator(10e6, 8, "
+                    "200e3, 79e3; 127 taps) -> FmQuadratureDemod(1.25e6, 75e3, 15e3) -> FirLowpass(1.25e6, 15e3, "
+                    "10e3; 125 taps)", fs_hz=10e6, stream_samples=world * n, samples_per_step_per_gpu=stop - start,
+                    halo_samples=start - h, channels_per_gpu=1)
+        return blk, x, stop - start, 8.5, desc
     if cfg == "c2":
         n = n_override or (1 << 26)
         (f_off, seed), = channel_plan(cfg, rank, world)
@@ -154,6 +177,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-max-samples", type=int, default=1 << 24)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--shard", default="stream", choices=["stream", "channels"],
+                    help="C2 on several GPUs: one stream cut in time (with a halo), or a channel per GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -170,7 +195,7 @@ def main():
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream(dev)
 
-    blk, x, samples, bps, desc = make_workload(args.config, rank, dev, args.n or None, world)
+    blk, x, samples, bps, desc = make_workload(args.config, rank, dev, args.n or None, world, args.shard)
     nout = blk.out_len(x.shape[-1])
     out_shape = (nout,) if x.dim() == 1 else (x.shape[0], nout)
     out_dtype = torch.float32 if args.config != "c3" else torch.complex64
@@ -207,7 +232,9 @@ def main():
         "metric": METRICS.get(args.config, METRIC), "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": dict(desc, parallelism=f"channel-sharded x{world}, no data-path collective"),
+        "config": dict(desc, parallelism=(f"stream time-sharded x{world} (halo {orion_sdr.STREAM_HALO} samples), no "
+                                          "data-path collective" if "halo_samples" in desc
+                                          else f"channel-sharded x{world}, no data-path collective")),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": "k_wbfm" if args.config in ("c2", "c4") else ("k_decim8" if args.config == "c3"

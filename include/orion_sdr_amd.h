@@ -121,6 +121,12 @@ orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float*
 #define ORION_WBFM_SEGMENTED_V1 4
 #define ORION_WBFM_SPECIALIZED 5  /* one kernel, streaming and back waves per CU */
 int orion_wbfm_chain_configure(orion_block* b, int path, int max_segments);
+/* Time-sharded streams (no reference counterpart): the absolute
+ * index of the next input sample, i.e. the NCO phase origin (rotator.rs:44-62
+ * advances the phase once per sample from index 0). A shard of one stream is
+ * processed by a fresh handle sought to its halo start, fed the halo and then
+ * the shard (orion_sdr.stream_shard). ORION_E_TYPE if b is not a WBFM chain. */
+int orion_wbfm_chain_seek(orion_block* b, uint64_t index);
 
 /* ---- Block contract (core.rs:12-22) ------------------------------------ */
 /* Host buffers (synchronous). */

@@ -495,6 +495,7 @@ class WbfmBlock final : public Block {
     k0_ = 0;
   }
   std::vector<float> taps(int which) const override { return which == 0 ? h_dec_ : h_aud_; }
+  void seek(uint64_t index) { k0_ = index; }
   int configure(int path, int max_seg) {
     if (path < kPathAuto || path > kPathWs || max_seg < 0) return -3;
     if ((path == kPathSeg2 || path == kPathSeg || path == kPathWs) && !seg_ok_) return -3;
@@ -552,6 +553,13 @@ int wbfm_chain_configure(Block* b, int path, int max_segments) {
   auto* w = dynamic_cast<WbfmBlock*>(b);
   if (!w) return -4;
   return w->configure(path, max_segments);
+}
+
+int wbfm_chain_seek(Block* b, unsigned long long index) {
+  auto* w = dynamic_cast<WbfmBlock*>(b);
+  if (!w) return -4;
+  w->seek(index);
+  return 0;
 }
 
 }  // namespace orion

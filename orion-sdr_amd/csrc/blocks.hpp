@@ -104,5 +104,9 @@ std::unique_ptr<Block> make_wbfm_chain(const WbfmParams& p, const std::vector<fl
 // -3 if this design cannot run on that path.
 enum : int { kPathAuto = 0, kPathSeg2 = 1, kPathRange = 2, kPathSplit = 3, kPathSeg = 4, kPathWs = 5 };
 int wbfm_chain_configure(Block* b, int path, int max_segments);
+// Absolute index of the next input sample (the NCO phase origin) of a WBFM
+// chain: a time-sharded stream starts each shard's handle at its halo start
+// (include/orion_sdr_amd.h orion_wbfm_chain_seek). -4 if b is not a WBFM chain.
+int wbfm_chain_seek(Block* b, unsigned long long index);
 
 }  // namespace orion

@@ -163,6 +163,14 @@ int orion_wbfm_chain_configure(orion_block* b, int path, int max_segments) {
   });
 }
 
+int orion_wbfm_chain_seek(orion_block* b, uint64_t index) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    if (orion::wbfm_chain_seek(b->impl.get(), index) == -4) return fail(ORION_E_TYPE, "not a WBFM chain");
+    return ORION_OK;
+  });
+}
+
 int orion_block_process(orion_block* b, const void* in, size_t n_in, void* out, size_t out_cap,
                         orion_work_report* wr) {
   if (!b) return fail(ORION_E_NULL, "null handle");

@@ -28,7 +28,7 @@ __all__ = [
     "FmQuadratureDemod", "PmQuadratureDemod", "SsbProductDemod", "AmEnvelopeDemod",
     "CwEnvelopeDemod", "WbfmChain", "fir_lowpass_design", "kaiser_lowpass_taps",
     "kaiser_transition_norm", "kaiser_num_taps", "lp_cascade_design", "lib_path", "OrionError",
-    "AudioToIqChain", "IqToIqChain", "IqToAudioChain", "Graph",
+    "AudioToIqChain", "IqToIqChain", "IqToAudioChain", "Graph", "stream_shard", "STREAM_HALO",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -87,6 +87,7 @@ def _load():
         "orion_wbfm_chain_new": (vp, [C.POINTER(WbfmParams)]),
         "orion_wbfm_chain_batch_new": (vp, [C.POINTER(WbfmParams), fp, sz]),
         "orion_wbfm_chain_configure": (i, [vp, i, i]),
+        "orion_wbfm_chain_seek": (i, [vp, C.c_uint64]),
         "orion_block_process": (i, [vp, vp, sz, vp, sz, C.POINTER(WorkReport)]),
         "orion_block_process_device": (i, [vp, vp, sz, vp, sz, vp, C.POINTER(WorkReport)]),
         "orion_block_reset": (i, [vp]), "orion_block_free": (None, [vp]),
@@ -151,7 +152,7 @@ class _Block:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h:
+        if h and _L is not None:  # at interpreter exit the module globals may already be gone
             _L.orion_block_free(h)
             self._h = None
 
@@ -352,6 +353,7 @@ class WbfmChain(_Block):
             offs = np.ascontiguousarray(offs)
             h = _L.orion_wbfm_chain_batch_new(C.byref(p), _fptr(offs), offs.size)
         super().__init__(h)
+        self.m = int(m)
 
     _PATHS = {"auto": 0, "segmented": 1, "ranges": 2, "split": 3, "segmented_v1": 4, "specialized": 5}
 
@@ -360,6 +362,45 @@ class WbfmChain(_Block):
         cap on the segmented kernel's waves (include/orion_sdr_amd.h)."""
         _check(_L.orion_wbfm_chain_configure(self._h, self._PATHS[path], int(max_segments)))
         return self
+
+    def seek(self, index: int):
+        """Absolute index of the next input sample (the NCO phase origin);
+        no reference counterpart (include/orion_sdr_amd.h orion_wbfm_chain_seek)."""
+        _check(_L.orion_wbfm_chain_seek(self._h, int(index)))
+        return self
+
+    def process_shard(self, x_halo, start: int, halo_start: int):
+        """One time shard of a stream (stream_shard): x_halo holds input
+        samples [halo_start, stop). The handle is reset and sought to halo_start,
+        runs the halo (which settles the decimator history, the discriminator's
+        previous sample, the LpCascade state and the audio FIR history), and the
+        audio of [start, stop) is returned: the same samples a single handle
+        produces for the whole stream, up to the halo's settling residual."""
+        self.reset()
+        self.seek(halo_start)
+        y = self.process(x_halo)
+        return y[(start - halo_start) // self.m:]
+
+
+# ---- time-sharded streams (SURVEY §8e) ----------------------------------------------
+# Halo before a shard: 1024 audio samples at M = 8. The LpCascade forgets its
+# zero start state within ~560 samples (||A^560|| < 1e-10 at 1.25 MHz, the host's
+# own check uses ||A^896|| ~ 1e-16), the audio FIR then needs 124 settled
+# samples, and the decimator 126 raw inputs; the rest is margin.
+STREAM_HALO = 8192
+
+
+def stream_shard(n: int, rank: int, world: int, m: int = 8, halo: int = STREAM_HALO):
+    """Rank `rank` of `world`'s time slice of ONE n-sample stream: (start, stop,
+    halo_start). Cuts fall on multiples of m (the decimator keeps inputs 0, m,
+    2m, ... of every call, decim.rs:66-71), so the shards' outputs concatenate
+    to the single-stream output; halo_start = max(0, start - halo)."""
+    if not (0 <= rank < world) or n < 0 or halo % m:
+        raise ValueError("stream_shard: bad rank/world/n/halo")
+    units = n // m
+    start = (units * rank // world) * m
+    stop = n if rank == world - 1 else (units * (rank + 1) // world) * m
+    return start, stop, max(0, start - halo)
 
 
 # ---- chains (src/core.rs:24-109) and block graphs -------------------------------

@@ -53,6 +53,12 @@ def tail(x, fraction=0.75):
     return x[int(len(x) * (1.0 - fraction)):]
 
 
+def report(name, v, tol):
+    """Print a measured parity figure and assert it is within tol."""
+    print(f"[parity] {name}: {v:.3e} (tol {tol:.1e})")
+    assert v <= tol, f"{name}: {v:.3e} > {tol:.1e}"
+
+
 def nrmse(got, ref):
     got = np.asarray(got, np.complex128 if np.iscomplexobj(got) else np.float64)
     ref = np.asarray(ref, got.dtype)

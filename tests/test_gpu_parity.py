@@ -13,7 +13,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import FS, complex_tone, nrmse, real_tone, snr_db, tail, wbfm_input
+from conftest import FS, complex_tone, nrmse, real_tone, report, snr_db, tail, wbfm_input
 
 pytestmark = pytest.mark.gpu
 GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden.npz"))
@@ -27,11 +27,6 @@ def cnoise(n, scale=1.0):
 def stream(blk, x, chunk):
     outs = [blk.process(x[..., i:i + chunk]) for i in range(0, x.shape[-1], chunk)]
     return np.concatenate(outs, axis=-1)
-
-
-def report(name, v, tol):
-    print(f"[parity] {name}: {v:.3e} (tol {tol:.1e})")
-    assert v <= tol, f"{name}: {v:.3e} > {tol:.1e}"
 
 
 def ulp_floor(fn, x):
@@ -324,6 +319,24 @@ def test_wbfm_segmented_streaming_and_channels(gpu_lib, oracle, path, max_seg):
     xc = np.stack([wbfm_input(1 << 18, f_off=float(f), seed=0x55 ^ c) for c, f in enumerate(offs)])
     got = gpu_lib.WbfmChain(f_off=offs).configure(path, 3 * max_seg).process(xc)
     report(f"wbfm {path} 3 ch max_segments={3 * max_seg} nrmse", nrmse(got, oracle.wbfm_channels(xc, offs, 3)), 1e-5)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_wbfm_stream_shards(gpu_lib, oracle, world):
+    """one stream cut into `world` time shards, each run by its own
+    handle from STREAM_HALO earlier samples (sought to the halo start, so its NCO
+    phasors are the single call's); concatenated, the single-stream output."""
+    n = (1 << 20) + 44
+    x = wbfm_input(n)
+    full = gpu_lib.WbfmChain().process(x)
+    parts = []
+    for r in range(world):
+        start, stop, h = gpu_lib.stream_shard(n, r, world)
+        parts.append(gpu_lib.WbfmChain().process_shard(x[h:stop], start, h))
+    got = np.concatenate(parts)
+    assert len(got) == len(full)
+    report(f"wbfm stream shards world={world} vs one call nrmse", nrmse(got, full), 1e-5)
+    report(f"wbfm stream shards world={world} vs oracle nrmse", nrmse(got, oracle.wbfm(x)), 1e-5)
 
 
 def test_wbfm_configure_errors(gpu_lib):
