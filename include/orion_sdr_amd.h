@@ -95,6 +95,21 @@ int orion_am_envelope_demod_with_abs_approx(orion_block* b, float k1, float k2);
 orion_block* orion_cw_envelope_demod_new(float fs, float tone_hz, float env_bw_hz);
 int orion_cw_envelope_demod_set_gain(orion_block* b, float g);
 
+/* ---- analog modulators: f32 audio -> cf32 IQ ---- */
+/* modulate/am.rs:20-30 AmDsbMod::new(fs, rf_hz, carrier_level, modulation_index);
+ * set_gain :31-33, set_clamp :34-36 (ORION_E_TYPE on another block). */
+orion_block* orion_am_dsb_mod_new(float fs, float rf_hz, float carrier_level, float modulation_index);
+int orion_am_dsb_mod_set_gain(orion_block* b, float g);
+int orion_am_dsb_mod_set_clamp(orion_block* b, int on);
+/* modulate/fm.rs:21-32 FmPhaseAccumMod::new(sample_rate, deviation_hz, rf_hz);
+ * set_deviation :33-35, set_gain :36-38. The phase is summed in f64 on the
+ * device (the reference multiplies f32 phasors, renormalised every 1024). */
+orion_block* orion_fm_phase_accum_mod_new(float fs, float deviation_hz, float rf_hz);
+int orion_fm_phase_accum_mod_set_deviation(orion_block* b, float deviation_hz);
+int orion_fm_phase_accum_mod_set_gain(orion_block* b, float g);
+/* modulate/ssb.rs:22-35 SsbPhasingMod::new(fs, audio_bw_hz, audio_if_hz, rf_hz, usb). */
+orion_block* orion_ssb_phasing_mod_new(float fs, float audio_bw_hz, float audio_if_hz, float rf_hz, int usb);
+
 /* The WBFM chain composed per docs/demodulate.md:128-133 (no single reference
  * type): Rotator(-f_off, fs) -> FirDecimator(fs, m, dec_cutoff, dec_trans) ->
  * FmQuadratureDemod(fs/m, dev_hz, audio_bw) -> FirLowpass(fs/m, audio_pass,

@@ -110,6 +110,74 @@ class RotatorBlock final : public Block {
   uint64_t k_ = 0;
 };
 
+// ------------------------------------------------------ analog modulators --
+constexpr float kTauF = 6.28318530717958647692f;  // core::f32::consts::TAU
+// modulate/am.rs:9-120. F32 audio -> C32 IQ.
+class AmModBlock final : public Block {
+ public:
+  AmModBlock(float fs, float rf_hz, float cl, float mi) : osc_(oscillator(rf_hz, fs)), cl_(cl), mi_(mi) {}
+  const char* name() const override { return "AmDsbMod"; }
+  Dt in_type() const override { return Dt::F32; }
+  Dt out_type() const override { return Dt::C32; }
+  WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
+    const size_t n = std::min(n_in, out_cap);  // am.rs:45
+    launch_am_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), k_, osc_.step_q64,
+                  cl_, mi_, g_, clamp_, s);
+    k_ += n;
+    return {n, n};
+  }
+  void reset() override { k_ = 0; }
+  void set_gain(float g) { g_ = g; }        // am.rs:31-33
+  void set_clamp(bool on) { clamp_ = on; }  // am.rs:34-36
+  std::vector<float> taps(int) const override { return {osc_.w_re, osc_.w_im}; }
+
+ private:
+  Oscillator osc_;
+  float cl_, mi_, g_ = 1.0f;
+  bool clamp_ = false;
+  uint64_t k_ = 0;
+};
+
+// modulate/fm.rs:11-74. F32 audio -> C32 IQ; the running phase is carried on the
+// device (f64, reduced mod 2 pi) so consecutive calls chain without a host sync.
+class FmModBlock final : public Block {
+ public:
+  FmModBlock(float fs, float dev_hz, float rf_hz) : fs_(fs), dev_(dev_hz), osc_(oscillator(rf_hz, fs)) {
+    for (auto& c : carry_) c.resize(sizeof(double));
+    reset();
+  }
+  const char* name() const override { return "FmPhaseAccumMod"; }
+  Dt in_type() const override { return Dt::F32; }
+  Dt out_type() const override { return Dt::C32; }
+  WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
+    const size_t n = std::min(n_in, out_cap);  // fm.rs:47
+    if (n == 0) return {0, 0};
+    const float kf = kTauF * dev_ / fs_;  // fm.rs:48, f32 as in the reference
+    sums_.resize(static_cast<size_t>(fm_mod_chunks(static_cast<long long>(n))) * sizeof(double));
+    launch_fm_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), kf, g_,
+                  sums_.as<double>(), carry_[cur_].as<double>(), carry_[cur_ ^ 1].as<double>(), k_, osc_.step_q64, s);
+    cur_ ^= 1;
+    k_ += n;
+    return {n, n};
+  }
+  void reset() override {
+    for (auto& c : carry_) c.zero();
+    ORION_HIP(hipDeviceSynchronize());
+    cur_ = 0;
+    k_ = 0;
+  }
+  void set_gain(float g) { g_ = g; }           // fm.rs:37-39
+  void set_deviation(float d) { dev_ = d; }    // fm.rs:34-36
+  std::vector<float> taps(int) const override { return {kTauF * dev_ / fs_, osc_.w_re, osc_.w_im}; }
+
+ private:
+  float fs_, dev_, g_ = 1.0f;
+  Oscillator osc_;
+  DevBuf carry_[2], sums_;
+  int cur_ = 0;
+  uint64_t k_ = 0;
+};
+
 // --------------------------------------------------------- FirDecimator ----
 class DecimBlock final : public Block {
  public:
@@ -531,6 +599,29 @@ class WbfmBlock final : public Block {
 }  // namespace
 
 std::unique_ptr<Block> make_rotator(float f, float fs) { return std::make_unique<RotatorBlock>(f, fs); }
+std::unique_ptr<Block> make_am_mod(float fs, float rf_hz, float cl, float mi) {
+  return std::make_unique<AmModBlock>(fs, rf_hz, cl, mi);
+}
+std::unique_ptr<Block> make_fm_mod(float fs, float dev_hz, float rf_hz) {
+  return std::make_unique<FmModBlock>(fs, dev_hz, rf_hz);
+}
+int mod_set_gain(Block* b, float g) {
+  if (auto* a = dynamic_cast<AmModBlock*>(b)) { a->set_gain(g); return 0; }
+  if (auto* f = dynamic_cast<FmModBlock*>(b)) { f->set_gain(g); return 0; }
+  return -4;
+}
+int am_mod_set_clamp(Block* b, bool on) {
+  auto* a = dynamic_cast<AmModBlock*>(b);
+  if (!a) return -4;
+  a->set_clamp(on);
+  return 0;
+}
+int fm_mod_set_deviation(Block* b, float d) {
+  auto* f = dynamic_cast<FmModBlock*>(b);
+  if (!f) return -4;
+  f->set_deviation(d);
+  return 0;
+}
 std::unique_ptr<Block> make_fir_decimator(float fs, size_t m, float cutoff, float trans, int nch) {
   return std::make_unique<DecimBlock>(fs, m, cutoff, trans, nch);
 }

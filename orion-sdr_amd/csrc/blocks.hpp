@@ -90,6 +90,13 @@ std::unique_ptr<Block> make_fir_lowpass_iq(const std::vector<float>& taps);
 // via a scratch copy. Resets the block's streaming state first, like the reference.
 int fir_lowpass_iq_filter_aligned(Block* b, void* io_dev, size_t n, hipStream_t s);
 
+// Analog modulators. F32 audio -> C32 IQ.
+std::unique_ptr<Block> make_am_mod(float fs, float rf_hz, float carrier_level, float modulation_index);  // am.rs
+std::unique_ptr<Block> make_fm_mod(float fs, float deviation_hz, float rf_hz);                         // fm.rs
+int mod_set_gain(Block* b, float g);             // AmDsbMod / FmPhaseAccumMod set_gain; -4 other blocks
+int am_mod_set_clamp(Block* b, bool on);         // -4 if not an AmDsbMod
+int fm_mod_set_deviation(Block* b, float d);     // -4 if not an FmPhaseAccumMod
+
 // The WBFM chain (docs/demodulate.md:128-133): Rotator(-f_off) -> FirDecimator
 // (fs, m=8, dec_cutoff, dec_trans) -> FmQuadratureDemod(fs/8, dev, audio_bw) ->
 // FirLowpass(fs/8, audio_pass, audio_trans). C32 -> F32, out = ceil(n/8).

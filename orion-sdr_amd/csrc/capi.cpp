@@ -104,6 +104,39 @@ int orion_fir_lowpass_iq_filter_aligned(orion_block* b, void* io, size_t n) {
     return ORION_OK;
   });
 }
+orion_block* orion_am_dsb_mod_new(float fs, float rf_hz, float carrier_level, float modulation_index) {
+  return make([&] { return orion::make_am_mod(fs, rf_hz, carrier_level, modulation_index); });
+}
+int orion_am_dsb_mod_set_gain(orion_block* b, float g) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  if (std::strcmp(b->impl->name(), "AmDsbMod") != 0) return fail(ORION_E_TYPE, "not an AmDsbMod");
+  return guarded([&] { return orion::mod_set_gain(b->impl.get(), g); });
+}
+int orion_am_dsb_mod_set_clamp(orion_block* b, int on) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    if (orion::am_mod_set_clamp(b->impl.get(), on != 0)) return fail(ORION_E_TYPE, "not an AmDsbMod");
+    return ORION_OK;
+  });
+}
+orion_block* orion_fm_phase_accum_mod_new(float fs, float deviation_hz, float rf_hz) {
+  return make([&] { return orion::make_fm_mod(fs, deviation_hz, rf_hz); });
+}
+int orion_fm_phase_accum_mod_set_deviation(orion_block* b, float deviation_hz) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    if (orion::fm_mod_set_deviation(b->impl.get(), deviation_hz)) return fail(ORION_E_TYPE, "not an FmPhaseAccumMod");
+    return ORION_OK;
+  });
+}
+int orion_fm_phase_accum_mod_set_gain(orion_block* b, float g) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  if (std::strcmp(b->impl->name(), "FmPhaseAccumMod") != 0) return fail(ORION_E_TYPE, "not an FmPhaseAccumMod");
+  return guarded([&] { return orion::mod_set_gain(b->impl.get(), g); });
+}
+orion_block* orion_ssb_phasing_mod_new(float fs, float audio_bw_hz, float audio_if_hz, float rf_hz, int usb) {
+  return make([&] { return orion::make_ssb_mod(fs, audio_bw_hz, audio_if_hz, rf_hz, usb != 0); });
+}
 orion_block* orion_lp_cascade_new(float fs, float fc) {
   return make([&] { return orion::make_lp_cascade(fs, fc); });
 }

@@ -1,0 +1,217 @@
+// k_mod.hip — on-device analog modulators for gfx950.
+//   AmDsbMod::process          modulate/am.rs:44-120
+//   FmPhaseAccumMod::process   modulate/fm.rs:45-74 (+ mix_with_nco, dsp/nco.rs:62-66)
+//   SsbPhasingMod::process     modulate/ssb.rs:43-114 (front and back of the two
+//                              LpCascade scans, which run on the k_scan kernels)
+// Every oscillator is the closed form of the reference's phasor recurrence:
+// sample i of a call uses w^(k0 + i + 1) (Rotator::next / Nco::next_cs advance
+// before returning), evaluated by phasor_q64 from the stream index, so a call
+// never depends on its predecessor's rounding. Streaming, memory-bound kernels:
+// grid-stride over the samples, at most 8 workgroups per CU.
+#include <algorithm>
+
+#include "kernels.hpp"
+
+namespace orion {
+namespace {
+
+constexpr int NT = 256;
+constexpr int kMaxGrid = 2048;
+constexpr int kFmC = 16;             // FM phase scan: samples per thread
+constexpr int kFmCH = kFmC * NT;     // samples per workgroup chunk (4096)
+
+int grid_for(long long n) { return static_cast<int>(std::min<long long>(kMaxGrid, std::max(1LL, (n + NT - 1) / NT))); }
+
+// am.rs:87-89 (clamp: :56): m = (cl + mi x) [clamped to +-1] * g; out = m * r.
+__global__ __launch_bounds__(NT) void k_am_mod(const float* __restrict__ x, f2* __restrict__ y, long long n,
+                                               uint64_t k0, uint64_t step, float cl, float mi, float g, int clamp) {
+  for (long long i = blockIdx.x * static_cast<long long>(NT) + threadIdx.x; i < n;
+       i += static_cast<long long>(gridDim.x) * NT) {
+    float v = cl + mi * x[i];
+    if (clamp) v = fminf(fmaxf(v, -1.0f), 1.0f);
+    const float m = v * g;
+    const f2 r = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
+    y[i] = f2{m * r.x, m * r.y};
+  }
+}
+
+// ssb.rs:52-54: the two LpCascade inputs x p.re, x p.im (p = audio NCO), planar.
+__global__ __launch_bounds__(NT) void k_ssb_mod_front(const float* __restrict__ x, float* __restrict__ u,
+                                                      long long n, uint64_t k0, uint64_t step) {
+  for (long long i = blockIdx.x * static_cast<long long>(NT) + threadIdx.x; i < n;
+       i += static_cast<long long>(gridDim.x) * NT) {
+    const f2 p = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
+    const float xi = x[i];
+    u[i] = xi * p.x;
+    u[n + i] = xi * p.y;
+  }
+}
+
+// ssb.rs:55-60: z = (I, side Q); out = z * r (rf NCO), FMA form of rotate_block.
+__global__ __launch_bounds__(NT) void k_ssb_mod_back(const float* __restrict__ v, f2* __restrict__ y, long long n,
+                                                     uint64_t k0, uint64_t step, float side) {
+  for (long long i = blockIdx.x * static_cast<long long>(NT) + threadIdx.x; i < n;
+       i += static_cast<long long>(gridDim.x) * NT) {
+    const f2 r = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
+    const f2 z = f2{v[i], side * v[n + i]};
+    y[i] = cmul_rot(z, r);
+  }
+}
+
+// ---- FmPhaseAccumMod: phi_i = phi_carry + sum_{j <= i} inc_j (f64), z = e^{j phi} ----
+// fm.rs:48-56 multiplies the running phasor by (cos dphi, sin dphi) rounded to
+// f32, dphi = kf x_i, renormalising every 1024 samples. The angle of that f32
+// pair, not dphi itself, is what the recurrence adds per sample, and its bias
+// is systematic (it drifted 1.2e-2 rad from the exact sum over 2^20 samples of
+// the C2 input): so the increment is atan2 of the same f32 pair, summed in f64.
+// What remains is the recurrence's own multiply rounding (a random walk) and
+// sincosf/sin_cos last-bit differences.
+__device__ __forceinline__ double fm_inc(float kf, float x) {
+  const float dphi = kf * x;  // fm.rs:50
+  float s, c;
+  sincosf(dphi, &s, &c);  // fm.rs:51
+  return atan2(static_cast<double>(s), static_cast<double>(c));
+}
+
+// Pass 1: the f64 sum of each chunk's phase increments.
+__global__ __launch_bounds__(NT) void k_fm_mod_sum(const float* __restrict__ x, long long n, float kf,
+                                                   double* __restrict__ sums) {
+  __shared__ double part[NT / 64];
+  const long long base = static_cast<long long>(blockIdx.x) * kFmCH;
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < kFmC; ++k) {
+    const long long i = base + threadIdx.x + static_cast<long long>(k) * NT;
+    if (i < n) s += fm_inc(kf, x[i]);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < NT / 64; ++w) t += part[w];
+    sums[blockIdx.x] = t;
+  }
+}
+
+// Pass 2 (one workgroup): exclusive prefix of the chunk sums from the carried
+// phase; the carried phase of the next call (reduced mod 2 pi).
+__global__ __launch_bounds__(NT) void k_fm_mod_carry(double* __restrict__ sums, int nchunk,
+                                                     const double* __restrict__ carry_in,
+                                                     double* __restrict__ carry_out) {
+  __shared__ double tot[NT / 64];
+  __shared__ double run;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) run = carry_in[0];
+  __syncthreads();
+  for (int c0 = 0; c0 < nchunk; c0 += NT) {
+    const int c = c0 + t;
+    const double v = c < nchunk ? sums[c] : 0.0;
+    double inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const double o = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += o;
+    }
+    if (lane == 63) tot[w] = inc;
+    __syncthreads();
+    double before = run;
+    for (int k = 0; k < w; ++k) before += tot[k];
+    if (c < nchunk) sums[c] = before + inc - v;  // exclusive
+    __syncthreads();
+    if (t == NT - 1) run = before + inc;
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double r = run;
+    carry_out[0] = r - 6.283185307179586 * rint(r * 0.15915494309189535);
+  }
+}
+
+// Pass 3: per chunk, the inclusive prefix of the increments (thread-local runs,
+// then a workgroup scan of the run totals), z = e^{j phi} * gain, and
+// mix_with_nco's non-FMA complex product with the RF phasor (nco.rs:62-66).
+__global__ __launch_bounds__(NT) void k_fm_mod_apply(const float* __restrict__ x, f2* __restrict__ y, long long n,
+                                                     float kf, float gain, const double* __restrict__ offs,
+                                                     uint64_t k0, uint64_t step) {
+  __shared__ double tot[NT / 64];
+  __shared__ float xs[kFmCH + kFmCH / 16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const long long base = static_cast<long long>(blockIdx.x) * kFmCH;
+  // coalesced load, then each thread owns kFmC consecutive samples
+  for (int k = 0; k < kFmC; ++k) {
+    const int e = t + k * NT;
+    const long long i = base + e;
+    xs[e + (e >> 4)] = i < n ? x[i] : 0.0f;
+  }
+  __syncthreads();
+  double d[kFmC];
+  double run = 0.0;
+#pragma unroll
+  for (int k = 0; k < kFmC; ++k) {
+    const int e = t * kFmC + k;
+    d[k] = fm_inc(kf, xs[e + (e >> 4)]);
+    run += d[k];
+  }
+  double inc = run;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const double o = __shfl_up(inc, dd, 64);
+    if (lane >= dd) inc += o;
+  }
+  if (lane == 63) tot[w] = inc;
+  __syncthreads();
+  double phi = offs[blockIdx.x] + inc - run;
+  for (int k = 0; k < w; ++k) phi += tot[k];
+#pragma unroll
+  for (int k = 0; k < kFmC; ++k) {
+    const long long i = base + t * kFmC + k;
+    phi += d[k];
+    if (i < n) {
+      const double red = phi - 6.283185307179586 * rint(phi * 0.15915494309189535);
+      float s, c;
+      sincosf(static_cast<float>(red), &s, &c);
+      const f2 b = f2{c * gain, s * gain};  // fm.rs:66 base = z * gain
+      const f2 r = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
+      y[i] = f2{b.x * r.x - b.y * r.y, b.x * r.y + b.y * r.x};  // nco.rs:65 (no FMA)
+    }
+  }
+}
+
+}  // namespace
+
+void launch_am_mod(const float* x, f2* y, long long n, uint64_t k0, uint64_t step, float cl, float mi, float g,
+                   bool clamp, hipStream_t s) {
+  if (n <= 0) return;
+  k_am_mod<<<grid_for(n), NT, 0, s>>>(x, y, n, k0, step, cl, mi, g, clamp ? 1 : 0);
+  ORION_LAUNCH_CHECK();
+}
+
+void launch_ssb_mod_front(const float* x, float* u, long long n, uint64_t k0, uint64_t step, hipStream_t s) {
+  if (n <= 0) return;
+  k_ssb_mod_front<<<grid_for(n), NT, 0, s>>>(x, u, n, k0, step);
+  ORION_LAUNCH_CHECK();
+}
+
+void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, uint64_t step, float side, hipStream_t s) {
+  if (n <= 0) return;
+  k_ssb_mod_back<<<grid_for(n), NT, 0, s>>>(v, y, n, k0, step, side);
+  ORION_LAUNCH_CHECK();
+}
+
+long long fm_mod_chunks(long long n) { return (n + kFmCH - 1) / kFmCH; }
+
+void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, double* sums,
+                   const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, hipStream_t s) {
+  if (n <= 0) return;
+  const long long nchunk = fm_mod_chunks(n);
+  if (nchunk > (1LL << 30)) throw HipError("FM modulator: input too long");
+  const int g = static_cast<int>(nchunk);
+  k_fm_mod_sum<<<g, NT, 0, s>>>(x, n, kf, sums);
+  k_fm_mod_carry<<<1, NT, 0, s>>>(sums, g, carry_in, carry_out);
+  k_fm_mod_apply<<<g, NT, 0, s>>>(x, y, n, kf, gain, sums, k0, step);
+  ORION_LAUNCH_CHECK();
+}
+
+}  // namespace orion

@@ -15,6 +15,18 @@ namespace orion {
 // phasor after k0+i+1 steps, e^{j theta (k0+i+1)}. tab_dev = e^{j theta p},
 // p < kRotTile.
 constexpr int kRotTile = 4096;
+// ---- analog modulators (k_mod.hip; modulate/am.rs, fm.rs, ssb.rs) ----
+void launch_am_mod(const float* x, f2* y, long long n, uint64_t k0, uint64_t step, float cl, float mi, float g,
+                   bool clamp, hipStream_t s);
+// u = [x p.re | x p.im] (planar, 2n floats), p = audio NCO phasor k0 + i + 1
+void launch_ssb_mod_front(const float* x, float* u, long long n, uint64_t k0, uint64_t step, hipStream_t s);
+// y = (v[i], side v[n + i]) * rf phasor k0 + i + 1
+void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, uint64_t step, float side, hipStream_t s);
+// FM phase accumulator: sums = fm_mod_chunks(n) doubles of workspace; carry_in /
+// carry_out: the running phase (one double each, ping-pong between calls)
+long long fm_mod_chunks(long long n);
+void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, double* sums,
+                   const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, hipStream_t s);
 void launch_rotator(const f2* x_dev, f2* y_dev, long long n, uint64_t k0, uint64_t step_q64,
                     const f2* tab_dev, hipStream_t s);
 // SsbProductDemod front end helper / Rotator::mix_usb_block (rotator.rs:88-94):

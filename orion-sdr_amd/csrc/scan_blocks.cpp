@@ -233,7 +233,52 @@ class AmBlock final : public ScanBlock {
   DevBuf tmp_;
 };
 
+// modulate/ssb.rs:9-114. F32 audio -> C32 IQ: the audio-NCO products (k_mod), both
+// LpCascades as one 2-channel LP4 scan (I, Q planar), then (I, side Q) x RF NCO.
+class SsbModBlock final : public Block {
+ public:
+  SsbModBlock(float fs, float bw, float if_hz, float rf_hz, bool usb)
+      : aud_(oscillator(if_hz, fs)), rf_(oscillator(rf_hz, fs)), side_(usb ? 1.0f : -1.0f) {
+    b_ = lp_cascade_design(fs, bw * 0.9f);  // ssb.rs:25
+    st_ = std::make_unique<ScanStage>(RecK::LP4, Pre::Real, Post::Id, lp_cascade_ss(b_), coef_lp(b_), 2);
+    st_->set_carry(carry_zero());
+  }
+  const char* name() const override { return "SsbPhasingMod"; }
+  Dt in_type() const override { return Dt::F32; }
+  Dt out_type() const override { return Dt::C32; }
+  WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
+    const size_t n = std::min(n_in, out_cap);  // ssb.rs:44
+    if (n == 0) return {0, 0};
+    const long long nn = static_cast<long long>(n);
+    u_.resize(2 * n * sizeof(float));
+    v_.resize(2 * n * sizeof(float));
+    launch_ssb_mod_front(static_cast<const float*>(in), u_.as<float>(), nn, k_, aud_.step_q64, s);
+    st_->run(u_.as<void>(), nn, nn, v_.as<void>(), nn, static_cast<long long>(k_), s);
+    launch_ssb_mod_back(v_.as<float>(), static_cast<f2*>(out), nn, k_, rf_.step_q64, side_, s);
+    k_ += n;
+    return {n, n};
+  }
+  void reset() override {
+    k_ = 0;
+    st_->set_carry(carry_zero());
+    ORION_HIP(hipDeviceSynchronize());
+  }
+  std::vector<float> taps(int) const override { return {b_.b0, b_.b1, b_.b2, b_.a1, b_.a2}; }
+
+ private:
+  Oscillator aud_, rf_;
+  float side_;
+  BiquadCoeffs b_;
+  std::unique_ptr<ScanStage> st_;
+  DevBuf u_, v_;
+  uint64_t k_ = 0;
+};
+
 }  // namespace
+
+std::unique_ptr<Block> make_ssb_mod(float fs, float audio_bw, float audio_if_hz, float rf_hz, bool usb) {
+  return std::make_unique<SsbModBlock>(fs, audio_bw, audio_if_hz, rf_hz, usb);
+}
 
 std::unique_ptr<Block> make_lp_cascade(float fs, float fc) {
   const BiquadCoeffs b = lp_cascade_design(fs, fc);

@@ -6,7 +6,9 @@
 
 namespace orion {
 
-std::unique_ptr<Block> make_lp_cascade(float fs, float fc);                  // dsp/iir.rs:49-83
+std::unique_ptr<Block> make_lp_cascade(float fs, float fc);
+// modulate/ssb.rs:9-114 (SsbPhasingMod::new(fs, audio_bw, audio_if, rf, usb)). F32 -> C32.
+std::unique_ptr<Block> make_ssb_mod(float fs, float audio_bw, float audio_if_hz, float rf_hz, bool usb);                  // dsp/iir.rs:49-83
 std::unique_ptr<Block> make_dc_blocker(float fs, float cut_hz);              // dsp/dc.rs:8-59
 std::unique_ptr<Block> make_fm_demod(float fs, float dev_hz, float audio_bw);  // demodulate/fm.rs
 int fm_demod_with_translate(Block* b, float freq_hz);                        // fm.rs:34-37

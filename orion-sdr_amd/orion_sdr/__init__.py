@@ -26,7 +26,8 @@ import numpy as np
 __all__ = [
     "Rotator", "FirDecimator", "FirLowpass", "FirLowpassIq", "LpCascade", "DcBlocker",
     "FmQuadratureDemod", "PmQuadratureDemod", "SsbProductDemod", "AmEnvelopeDemod",
-    "CwEnvelopeDemod", "WbfmChain", "fir_lowpass_design", "kaiser_lowpass_taps",
+    "CwEnvelopeDemod", "WbfmChain", "AmDsbMod", "FmPhaseAccumMod", "SsbPhasingMod",
+    "fir_lowpass_design", "kaiser_lowpass_taps",
     "kaiser_transition_norm", "kaiser_num_taps", "lp_cascade_design", "lib_path", "OrionError",
     "AudioToIqChain", "IqToIqChain", "IqToAudioChain", "Graph", "stream_shard", "STREAM_HALO",
 ]
@@ -84,6 +85,13 @@ def _load():
         "orion_am_envelope_demod_with_abs_approx": (i, [vp, f, f]),
         "orion_cw_envelope_demod_new": (vp, [f, f, f]),
         "orion_cw_envelope_demod_set_gain": (i, [vp, f]),
+        "orion_am_dsb_mod_new": (vp, [f, f, f, f]),
+        "orion_am_dsb_mod_set_gain": (i, [vp, f]),
+        "orion_am_dsb_mod_set_clamp": (i, [vp, i]),
+        "orion_fm_phase_accum_mod_new": (vp, [f, f, f]),
+        "orion_fm_phase_accum_mod_set_deviation": (i, [vp, f]),
+        "orion_fm_phase_accum_mod_set_gain": (i, [vp, f]),
+        "orion_ssb_phasing_mod_new": (vp, [f, f, f, f, i]),
         "orion_wbfm_chain_new": (vp, [C.POINTER(WbfmParams)]),
         "orion_wbfm_chain_batch_new": (vp, [C.POINTER(WbfmParams), fp, sz]),
         "orion_wbfm_chain_configure": (i, [vp, i, i]),
@@ -336,6 +344,40 @@ class FmQuadratureDemod(_Block):
 class PmQuadratureDemod(_Block):
     def __init__(self, fs: float, k: float, audio_bw_hz: float):
         super().__init__(_L.orion_pm_quadrature_demod_new(fs, k, audio_bw_hz))
+
+
+# ---- analog modulators (src/modulate): f32 audio -> complex64 IQ ----
+class AmDsbMod(_Block):
+    """modulate/am.rs:20-36: carrier_level 1 -> full carrier (A3E), 0 -> DSB-SC."""
+
+    def __init__(self, fs: float, rf_hz: float, carrier_level: float, modulation_index: float):
+        super().__init__(_L.orion_am_dsb_mod_new(fs, rf_hz, carrier_level, modulation_index))
+
+    def set_gain(self, g: float):
+        _check(_L.orion_am_dsb_mod_set_gain(self._h, g))
+
+    def set_clamp(self, on: bool):
+        _check(_L.orion_am_dsb_mod_set_clamp(self._h, 1 if on else 0))
+
+
+class FmPhaseAccumMod(_Block):
+    """modulate/fm.rs:21-38 (deviation in Hz per unit input; rf_hz 0 for baseband)."""
+
+    def __init__(self, sample_rate: float, deviation_hz: float, rf_hz: float = 0.0):
+        super().__init__(_L.orion_fm_phase_accum_mod_new(sample_rate, deviation_hz, rf_hz))
+
+    def set_deviation(self, deviation_hz: float):
+        _check(_L.orion_fm_phase_accum_mod_set_deviation(self._h, deviation_hz))
+
+    def set_gain(self, g: float):
+        _check(_L.orion_fm_phase_accum_mod_set_gain(self._h, g))
+
+
+class SsbPhasingMod(_Block):
+    """modulate/ssb.rs:22-35."""
+
+    def __init__(self, fs: float, audio_bw_hz: float, audio_if_hz: float, rf_hz: float = 0.0, usb: bool = True):
+        super().__init__(_L.orion_ssb_phasing_mod_new(fs, audio_bw_hz, audio_if_hz, rf_hz, 1 if usb else 0))
 
 
 class WbfmChain(_Block):

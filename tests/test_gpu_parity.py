@@ -424,3 +424,80 @@ def test_api_validation(gpu_lib):
         gpu_lib.SsbProductDemod(FS, 0.0, 2800).process(np.zeros(2 * N, np.complex64)[::2])
     assert gpu_lib.FirDecimator(96e3, 4, 10.8e3, 2.4e3).process(complex_tone(96e3, 2e3, N)).shape == (N // 4,)
     assert gpu_lib.FmQuadratureDemod(FS, 2500, 5000).process(np.zeros(0, np.complex64)).shape == (0,)
+
+
+# ---- analog modulators (src/modulate) ---------------------------
+def _speech(n, fs=FS):
+    return (real_tone(fs, 700.0, n, 0.4) + real_tone(fs, 1900.0, n, 0.3)).astype(np.float32)
+
+
+@pytest.mark.parametrize("rf,cl,mi,gain,clamp", [(0.0, 1.0, 0.8, 1.0, False), (12e3, 0.0, 1.0, 0.7, False),
+                                                 (-5e3, 0.5, 1.6, 1.3, True)])
+def test_am_dsb_mod(gpu_lib, oracle, rf, cl, mi, gain, clamp):
+    """am.rs:44-120; the RF NCO in closed form against the reference's f32 phasor
+    recurrence: abs error bounded by its drift (|m| <= 1.3 here)."""
+    n = 1 << 18
+    a = _speech(n)
+    m = gpu_lib.AmDsbMod(FS, rf, cl, mi)
+    m.set_gain(gain)
+    m.set_clamp(clamp)
+    got = np.concatenate([m.process(a[:100_001]), m.process(a[100_001:])])  # streamed: the NCO index carries
+    ref = oracle.am_mod(a, FS, rf, cl, mi, gain, clamp)
+    err = float(np.max(np.abs(got - ref)))
+    report(f"am_dsb_mod rf={rf} clamp={clamp} max abs", err, 0.0 if rf == 0.0 else 4e-5)
+
+
+def test_fm_phase_accum_mod(gpu_lib, oracle):
+    """fm.rs:45-74 at the C2 rate (dev 75 kHz). Baseband against the reference
+    directly (the GPU sums the angles of the reference's own f32 step phasors in
+    f64). With the 1.5 MHz RF NCO, as for the Rotator: against the reference's
+    baseband output rotated by the exact phasor of the NCO's f32 step, and
+    against the reference within that NCO recurrence's own drift. Streamed calls
+    against one call (the f64 phase carry); the WBFM chain's audio from the
+    GPU-modulated IQ against the oracle-modulated IQ."""
+    fs, n = 10e6, 1 << 20
+    t = np.arange(n) / fs
+    aud = (0.5 * np.sin(2 * np.pi * 1e3 * t) + 0.3 * np.sin(2 * np.pi * 7e3 * t)).astype(np.float32)
+    base = gpu_lib.FmPhaseAccumMod(fs, 75e3, 0.0).process(aud)
+    base_ref = oracle.fm_mod(aud, fs, 75e3, 0.0)
+    report("fm_mod baseband vs reference max abs", float(np.max(np.abs(base - base_ref))), 2e-5)
+    one = gpu_lib.FmPhaseAccumMod(fs, 75e3, 1.5e6).process(aud)
+    ex = _exact_rotation(base_ref, 1.5e6, fs)
+    report("fm_mod RF 1.5 MHz vs exact NCO max abs", float(np.max(np.abs(one - ex))), 2e-5)
+    ref = oracle.fm_mod(aud, fs, 75e3, 1.5e6)
+    drift = np.abs(ref - ex)
+    print(f"[parity] fm_mod reference RF NCO recurrence drift max {float(drift.max()):.3e}")
+    assert np.all(np.abs(one - ref) <= drift + 2e-5)
+    m = gpu_lib.FmPhaseAccumMod(fs, 75e3, 1.5e6)
+    streamed = np.concatenate([m.process(aud[i:i + 300_007]) for i in range(0, n, 300_007)])
+    report("fm_mod streamed vs one call max abs", float(np.max(np.abs(streamed - one))), 2e-6)
+    report("fm_mod -> wbfm audio nrmse", nrmse(oracle.wbfm(one), oracle.wbfm(ref)), 1e-5)
+    g = gpu_lib.FmPhaseAccumMod(fs, 75e3, 0.0)
+    g.set_deviation(50e3)
+    g.set_gain(0.5)
+    ref2 = oracle.fm_mod(aud[:65536], fs, 50e3, 0.0) * np.float32(0.5)
+    report("fm_mod dev 50k gain 0.5 baseband max abs", float(np.max(np.abs(g.process(aud[:65536]) - ref2))), 2e-5)
+
+
+@pytest.mark.parametrize("usb,rf", [(True, 0.0), (False, 6e3)])
+def test_ssb_phasing_mod(gpu_lib, oracle, usb, rf):
+    """ssb.rs:43-114: audio NCO products, both LpCascades (one 2-channel scan),
+    (I, side Q) x RF NCO; and the mod -> SsbProductDemod round trip."""
+    n = (1 << 18) + 3
+    a = real_tone(FS, 1200.0, n, 0.5)
+    m = gpu_lib.SsbPhasingMod(FS, 2800.0, 1500.0, rf, usb)
+    got = np.concatenate([m.process(a[:70_000]), m.process(a[70_000:])])
+    ref = oracle.ssb_mod(a, FS, 2800.0, 1500.0, rf, usb)
+    # SURVEY §8c: SSB 1e-4 (NCO phase drift is not differential)
+    report(f"ssb_mod usb={usb} rf={rf} nrmse", nrmse(got, ref), 1e-4)
+    if rf == 0.0:
+        d = gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0).process(got)
+        report("ssb mod -> demod round trip vs oracle nrmse", nrmse(d, oracle.ssb_demod(ref, FS, 1500.0, 2800.0)), 1e-4)
+
+
+def test_modulator_setters_reject_other_blocks(gpu_lib):
+    fm = gpu_lib.FmQuadratureDemod(48e3, 2500, 5000)
+    assert gpu_lib._L.orion_am_dsb_mod_set_clamp(fm._h, 1) == -4
+    assert gpu_lib._L.orion_fm_phase_accum_mod_set_deviation(fm._h, 1.0) == -4
+    am = gpu_lib.AmDsbMod(FS, 0.0, 1.0, 0.5)
+    assert gpu_lib._L.orion_fm_phase_accum_mod_set_gain(am._h, 1.0) == -4
