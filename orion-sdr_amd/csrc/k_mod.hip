@@ -66,10 +66,24 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_back(const float* __restrict__ v
 // the C2 input): so the increment is atan2 of the same f32 pair, summed in f64.
 // What remains is the recurrence's own multiply rounding (a random walk) and
 // sincosf/sin_cos last-bit differences.
+// For |dphi| < 1/8 (every WBFM-rate deviation): dphi plus the angle between the
+// f32 pair and the exact (C, S) = (cos, sin) dphi, the latter from f64 Taylor
+// series (truncation < 1e-21), the former to first order (it is < 1e-7 rad).
 __device__ __forceinline__ double fm_inc(float kf, float x) {
   const float dphi = kf * x;  // fm.rs:50
   float s, c;
   sincosf(dphi, &s, &c);  // fm.rs:51
+  const double d = dphi;
+  if (fabs(d) < 0.125) {
+    const double q = d * d;
+    const double S = d * (1.0 - q * (1.0 / 6) * (1.0 - q * (1.0 / 20) * (1.0 - q * (1.0 / 42) *
+                     (1.0 - q * (1.0 / 72) * (1.0 - q * (1.0 / 110))))));
+    const double C = 1.0 - q * 0.5 * (1.0 - q * (1.0 / 12) * (1.0 - q * (1.0 / 30) * (1.0 - q * (1.0 / 56) *
+                     (1.0 - q * (1.0 / 90) * (1.0 - q * (1.0 / 132))))));
+    // sin of the angle between them; |(c, s)| = 1 +- 1e-7, so dividing by their
+    // cosine (1 +- 1e-7) would change the ~1e-8 result by ~1e-15
+    return d + (static_cast<double>(s) * C - static_cast<double>(c) * S);
+  }
   return atan2(static_cast<double>(s), static_cast<double>(c));
 }
 
@@ -96,37 +110,33 @@ __global__ __launch_bounds__(NT) void k_fm_mod_sum(const float* __restrict__ x, 
 }
 
 // Pass 2 (one workgroup): exclusive prefix of the chunk sums from the carried
-// phase; the carried phase of the next call (reduced mod 2 pi).
+// phase (each thread a run of consecutive chunks, one workgroup scan of the run
+// totals); the carried phase of the next call (reduced mod 2 pi).
 __global__ __launch_bounds__(NT) void k_fm_mod_carry(double* __restrict__ sums, int nchunk,
                                                      const double* __restrict__ carry_in,
                                                      double* __restrict__ carry_out) {
   __shared__ double tot[NT / 64];
-  __shared__ double run;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (t == 0) run = carry_in[0];
-  __syncthreads();
-  for (int c0 = 0; c0 < nchunk; c0 += NT) {
-    const int c = c0 + t;
-    const double v = c < nchunk ? sums[c] : 0.0;
-    double inc = v;
+  const int per = (nchunk + NT - 1) / NT;
+  const int c0 = min(nchunk, t * per), c1 = min(nchunk, c0 + per);
+  double run = 0.0;
+  for (int c = c0; c < c1; ++c) run += sums[c];
+  double inc = run;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const double o = __shfl_up(inc, d, 64);
-      if (lane >= d) inc += o;
-    }
-    if (lane == 63) tot[w] = inc;
-    __syncthreads();
-    double before = run;
-    for (int k = 0; k < w; ++k) before += tot[k];
-    if (c < nchunk) sums[c] = before + inc - v;  // exclusive
-    __syncthreads();
-    if (t == NT - 1) run = before + inc;
-    __syncthreads();
+  for (int d = 1; d < 64; d <<= 1) {
+    const double o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
   }
-  if (t == 0) {
-    const double r = run;
-    carry_out[0] = r - 6.283185307179586 * rint(r * 0.15915494309189535);
+  if (lane == 63) tot[w] = inc;
+  __syncthreads();
+  double before = carry_in[0] + inc - run;
+  for (int k = 0; k < w; ++k) before += tot[k];
+  for (int c = c0; c < c1; ++c) {
+    const double v = sums[c];
+    sums[c] = before;
+    before += v;
   }
+  if (t == NT - 1) carry_out[0] = before - 6.283185307179586 * rint(before * 0.15915494309189535);
 }
 
 // Pass 3: per chunk, the inclusive prefix of the increments (thread-local runs,
