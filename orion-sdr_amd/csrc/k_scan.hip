@@ -203,50 +203,102 @@ __global__ __launch_bounds__(NT) void k_scan_agg(const ScanArgs a) {
   }
 }
 
+// 4x4-or-smaller f64 matrix product C = A B (one thread).
+template <int S>
+__device__ void mat_mul_dev(const double* A, const double* B, double* C) {
+  for (int r = 0; r < S; ++r)
+    for (int c = 0; c < S; ++c) {
+      double acc = 0.0;
+      for (int k = 0; k < S; ++k) acc = __builtin_fma(A[r * S + k], B[k * S + c], acc);
+      C[r * S + c] = acc;
+    }
+}
+
+// State entering every block of a channel from the block aggregates. Each thread
+// owns a run of P = ceil(nblk / NT) consecutive blocks: the run's zero-state
+// aggregate (P sequential steps), one workgroup Kogge-Stone over the runs with
+// (A^(CH P))^(2^s), then the run walked again writing each block's entering
+// state. Runs before the last non-empty one are full, which is all the scan
+// needs; later (empty or short) runs write nothing.
 template <RecK RK>
 __global__ __launch_bounds__(NT) void k_scan_carry(const ScanArgs a, int nblk) {
   constexpr int S = RecSel<RK>::T::S;
+  __shared__ double mp[8][S * S];  // (A^(CH P))^(2^s)
   __shared__ double q[2][NT][S];
-  __shared__ double cs[S];
   const int t = threadIdx.x;
   const int ch = blockIdx.x;
-  if (t < S) cs[t] = a.carry_in[ch * kScanCarry + t];
+  const int P = (nblk + NT - 1) / NT;
+  const double* M1 = a.mats + ScanMatsLayout::kPch * S * S;  // A^CH
+  if (t == 0) {  // A^(CH P) by binary powering, then its squarings
+    double R[S * S], B[S * S], T2[S * S];
+    for (int e = 0; e < S * S; ++e) {
+      R[e] = (e / S == e % S) ? 1.0 : 0.0;
+      B[e] = M1[e];
+    }
+    for (int p = P; p > 0; p >>= 1) {
+      if (p & 1) {
+        mat_mul_dev<S>(R, B, T2);
+        for (int e = 0; e < S * S; ++e) R[e] = T2[e];
+      }
+      if (p > 1) {
+        mat_mul_dev<S>(B, B, T2);
+        for (int e = 0; e < S * S; ++e) B[e] = T2[e];
+      }
+    }
+    for (int e = 0; e < S * S; ++e) mp[0][e] = R[e];
+    for (int sq = 1; sq < 8; ++sq) mat_mul_dev<S>(mp[sq - 1], mp[sq - 1], mp[sq]);
+  }
+  const int b0 = min(nblk, t * P), b1 = min(nblk, b0 + P);
+  const double* __restrict__ ag = a.aggs + static_cast<long long>(ch) * nblk * S;
+  double g[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) g[i] = 0.0;
+#pragma unroll 8
+  for (int b = b0; b < b1; ++b) {  // g <- A^CH g + agg_b (unrolled: the loads go out together)
+    double v[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) v[i] = ag[static_cast<long long>(b) * S + i];
+    matvec_acc<S>(M1, g, v);
+#pragma unroll
+    for (int i = 0; i < S; ++i) g[i] = v[i];
+  }
+  double carry[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) carry[i] = a.carry_in[ch * kScanCarry + i];
+  __syncthreads();  // mp ready
+  if (t == 0) matvec_acc<S>(mp[0], carry, g);  // fold the incoming state into run 0 (a full run)
+  int buf = 0;
+  for (int s = 0; s < 8; ++s) {
+    const int d = 1 << s;
+#pragma unroll
+    for (int i = 0; i < S; ++i) q[buf][t][i] = g[i];
+    __syncthreads();
+    if (t >= d) {
+      double o[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) o[i] = q[buf][t - d][i];
+      matvec_acc<S>(mp[s], o, g);
+    }
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i) q[buf][t][i] = g[i];
   __syncthreads();
-  const double* Mch = a.mats + ScanMatsLayout::kPch * S * S;
-  for (int c0 = 0; c0 < nblk; c0 += NT) {
-    const int b = c0 + t;
-    double v[S], carry[S];
+  double st[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) st[i] = t == 0 ? carry[i] : q[buf][t - 1][i];
+  double* __restrict__ out = a.sin + static_cast<long long>(ch) * nblk * S;
+#pragma unroll 8
+  for (int b = b0; b < b1; ++b) {  // entering state of each block of the run
+    double v[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) {
-      carry[i] = cs[i];
-      v[i] = b < nblk ? a.aggs[(static_cast<long long>(ch) * nblk + b) * S + i] : 0.0;
+      out[static_cast<long long>(b) * S + i] = st[i];
+      v[i] = ag[static_cast<long long>(b) * S + i];
     }
-    if (t == 0) matvec_acc<S>(Mch, carry, v);  // fold the incoming state into element 0
-    int buf = 0;
-    for (int s = 0; s < 8; ++s) {
-      const int d = 1 << s;
+    matvec_acc<S>(M1, st, v);
 #pragma unroll
-      for (int i = 0; i < S; ++i) q[buf][t][i] = v[i];
-      __syncthreads();
-      if (t >= d) {
-        double o[S];
-#pragma unroll
-        for (int i = 0; i < S; ++i) o[i] = q[buf][t - d][i];
-        matvec_acc<S>(Mch + s * S * S, o, v);
-      }
-      buf ^= 1;
-    }
-#pragma unroll
-    for (int i = 0; i < S; ++i) q[buf][t][i] = v[i];
-    __syncthreads();
-    if (b < nblk) {
-      double* out = a.sin + (static_cast<long long>(ch) * nblk + b) * S;
-#pragma unroll
-      for (int i = 0; i < S; ++i) out[i] = t == 0 ? carry[i] : q[buf][t - 1][i];
-    }
-    __syncthreads();
-    if (t < S) cs[t] = q[buf][NT - 1][t];
-    __syncthreads();
+    for (int i = 0; i < S; ++i) st[i] = v[i];
   }
 }
 
