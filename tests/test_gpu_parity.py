@@ -9,6 +9,7 @@ of its f32 step); WBFM end to end 1e-5 nrmse; SSB 1e-4 nrmse (BFO drift is
 not differential). Measured values are printed (pytest -s).
 """
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -17,6 +18,7 @@ from conftest import FS, complex_tone, nrmse, real_tone, report, snr_db, tail, w
 
 pytestmark = pytest.mark.gpu
 GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden.npz"))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 RNG = np.random.default_rng(1234)
 
 
@@ -501,3 +503,40 @@ def test_modulator_setters_reject_other_blocks(gpu_lib):
     assert gpu_lib._L.orion_fm_phase_accum_mod_set_deviation(fm._h, 1.0) == -4
     am = gpu_lib.AmDsbMod(FS, 0.0, 1.0, 0.5)
     assert gpu_lib._L.orion_fm_phase_accum_mod_set_gain(am._h, 1.0) == -4
+
+
+def test_bench_stream_shard_workload(gpu_lib):
+    """bench.py's C2 workload on 2 ranks (--shard stream), both ranks run here on
+    one GPU: rank r's slice (generated from its halo start), its handle sought
+    there, one call over halo + shard; concatenated past the halos, the audio of
+    one handle over the ranks' shard inputs."""
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    dev = torch.device("cuda", 0)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    n, world = 1 << 20, 2
+    outs, xs = [], []
+    for r in range(world):
+        blk, x, samples, _, desc = bench.make_workload("c2", r, dev, n, world, "stream")
+        start, stop, h = gpu_lib.stream_shard(world * n, r, world)
+        assert samples == stop - start == n and desc["halo_samples"] == start - h
+        out = torch.empty(blk.out_len(x.shape[-1]), dtype=torch.float32, device=dev)
+        blk.process_device(x, out, sh)
+        torch.cuda.synchronize()
+        outs.append(out[(start - h) // 8:].cpu().numpy())
+        xs.append(x[start - h:])
+    full = gpu_lib.WbfmChain(f_off=bench.OFFSETS[0])
+    xf = torch.cat(xs)
+    of = torch.empty(full.out_len(xf.shape[-1]), dtype=torch.float32, device=dev)
+    full.process_device(xf, of, sh)
+    torch.cuda.synchronize()
+    got, ref = np.concatenate(outs), of.cpu().numpy()
+    assert len(got) == len(ref)
+    # rank 1's halo comes from its own slice generator (a different noise seed than
+    # rank 0's tail), so compare past the settling span after the cut
+    cut = n // 8
+    report("bench stream shards rank 0 nrmse", nrmse(got[:cut], ref[:cut]), 1e-6)
+    report("bench stream shards rank 1 past 2048 nrmse", nrmse(got[cut + 2048:], ref[cut + 2048:]), 1e-6)
