@@ -642,6 +642,104 @@ __global__ __launch_bounds__(NT, ORION_SP_WAVES) void k_lpdc_sp(const ScanArgs a
   for (int e2 = warm + t; e2 < cnt; e2 += NT) yo[e2 - warm] = sb[pos(e2)];
 }
 
+// SsbPhasingMod in one pass (modulate/ssb.rs:43-114): per chunk, the audio-NCO
+// products of both branches staged in LDS, both LpCascades as LP4 block scans
+// (warm-up of kSpWarm samples from a zero state after the first chunk, as in
+// k_lpdc_sp: the host checks ||A^kSpWarm||), and (I, side Q) x RF NCO stored.
+// carry: [I state 4][Q state 4] floats.
+__global__ __launch_bounds__(NT) void k_ssb_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
+                                                   uint64_t k0, uint64_t step_aud, uint64_t step_rf, float side,
+                                                   ScanCoef cf, const double* __restrict__ mlp,
+                                                   const float* __restrict__ carry_in, float* __restrict__ carry_out) {
+  constexpr int S = 4;
+  __shared__ float sb[2][PADN];
+  __shared__ double tot[2][4][S];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c = static_cast<int>(blockIdx.x);
+  const int warm = c == 0 ? 0 : kSpWarm;
+  const long long o0 = c == 0 ? 0 : CH + static_cast<long long>(c - 1) * (CH - kSpWarm);
+  const long long base = o0 - warm;
+  const int cnt = static_cast<int>(min(static_cast<long long>(CH), n - base));
+  const bool last = o0 + (cnt - warm) >= n;
+  const RecLP4 lp{{cf.b0, cf.b1, cf.b2, cf.a1, cf.a2}};
+  {  // stage: x p.re, x p.im (ssb.rs:53-54), coalesced loads first
+    float v[C];
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+      const int e = t + k * NT;
+      v[k] = e < cnt ? x[base + e] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+      const int e = t + k * NT;
+      const f2 p = phasor_q64(k0 + static_cast<uint64_t>(base + e) + 1, step_aud);
+      sb[0][pos(e)] = v[k] * p.x;
+      sb[1][pos(e)] = v[k] * p.y;
+    }
+  }
+  __syncthreads();
+  float xs[2][C];
+  float s0[2][S];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+#pragma unroll
+    for (int i = 0; i < C; ++i) xs[b][i] = sb[b][pos(t * C + i)];
+#pragma unroll
+    for (int k = 0; k < S; ++k) s0[b][k] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < C; ++i)
+      if (t * C + i < cnt) (void)lp.step(s0[b], xs[b][i]);
+    double q[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) q[k] = s0[b][k];
+    wave_scan_inclusive<S>(q, mlp + ScanMatsLayout::kPwc * S * S, lane);
+    if (lane == 63)
+#pragma unroll
+      for (int k = 0; k < S; ++k) tot[b][wave][k] = q[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    double cw[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) cw[k] = c == 0 ? static_cast<double>(carry_in[4 * b + k]) : 0.0;
+    for (int w = 0; w < wave; ++w) {
+      double v[S];
+#pragma unroll
+      for (int k = 0; k < S; ++k) v[k] = tot[b][w][k];
+      matvec_acc<S>(mlp + ScanMatsLayout::kM64 * S * S, cw, v);
+#pragma unroll
+      for (int k = 0; k < S; ++k) cw[k] = v[k];
+    }
+    // the wave's entering state folded into lane 0, the wave re-scanned
+    double q[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) q[k] = s0[b][k];
+    if (lane == 0) matvec_acc<S>(mlp + ScanMatsLayout::kPwc * S * S, cw, q);
+    wave_scan_inclusive<S>(q, mlp + ScanMatsLayout::kPwc * S * S, lane);
+    float ef[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const double o = __shfl_up(q[k], 1, 64);
+      ef[k] = static_cast<float>(lane == 0 ? cw[k] : o);
+    }
+#pragma unroll
+    for (int i = 0; i < C; ++i)
+      if (t * C + i < cnt) xs[b][i] = lp.step(ef, xs[b][i]);  // ssb.rs:53-54 LpCascade outputs
+    if (last && t * C <= cnt - 1 && cnt - 1 < t * C + C)  // the next call's state
+#pragma unroll
+      for (int k = 0; k < S; ++k) carry_out[4 * b + k] = ef[k];
+  }
+#pragma unroll
+  for (int i = 0; i < C; ++i) {  // ssb.rs:55-60
+    const int e = t * C + i;
+    if (e >= warm && e < cnt) {
+      const f2 r = phasor_q64(k0 + static_cast<uint64_t>(base + e) + 1, step_rf);
+      y[base + e] = cmul_rot(f2{xs[0][i], side * xs[1][i]}, r);
+    }
+  }
+}
+
 template <RecK RK, Pre PR, Post PO>
 void run3(const ScanArgs& a, int nch, hipStream_t s) {
   const int nblk = div_up(a.n, CH);
@@ -661,6 +759,17 @@ int scan_state_dim(RecK rec) {
     case RecK::DC: return 2;
     default: return 1;
   }
+}
+
+void launch_ssb_mod_sp(const float* x, f2* y, long long n, uint64_t k0, uint64_t step_aud, uint64_t step_rf,
+                       float side, const ScanCoef& c, const double* mats_lp, const float* carry_in, float* carry_out,
+                       hipStream_t s) {
+  if (n <= 0) return;
+  const long long grid = lpdc_sp_chunks(n);
+  if (grid > (1LL << 31) - 1) throw HipError("single-pass SSB modulator grid too large");
+  k_ssb_mod_sp<<<static_cast<int>(grid), NT, 0, s>>>(x, y, n, k0, step_aud, step_rf, side, c, mats_lp, carry_in,
+                                                     carry_out);
+  ORION_LAUNCH_CHECK();
 }
 
 long long lpdc_sp_chunks(long long n) {

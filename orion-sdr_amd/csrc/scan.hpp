@@ -81,6 +81,11 @@ void launch_scan(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, hipSt
 // lpdc_sp_chunks(n) * nch * 8 u32 look-back records; epoch: this launch's tag.
 constexpr int kSpWarm = 256;
 long long lpdc_sp_chunks(long long n);
+// SsbPhasingMod in one pass (k_ssb_mod_sp): valid when ||A_lp^kSpWarm|| is
+// negligible; mats_lp = the LP4 scan matrices; carry = [I 4][Q 4] floats.
+void launch_ssb_mod_sp(const float* x, f2* y, long long n, uint64_t k0, uint64_t step_aud, uint64_t step_rf,
+                       float side, const ScanCoef& c, const double* mats_lp, const float* carry_in, float* carry_out,
+                       hipStream_t s);
 void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, uint32_t* rec, uint32_t epoch,
                     hipStream_t s);
 int scan_state_dim(RecK rec);

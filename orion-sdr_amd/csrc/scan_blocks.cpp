@@ -240,8 +240,20 @@ class SsbModBlock final : public Block {
   SsbModBlock(float fs, float bw, float if_hz, float rf_hz, bool usb)
       : aud_(oscillator(if_hz, fs)), rf_(oscillator(rf_hz, fs)), side_(usb ? 1.0f : -1.0f) {
     b_ = lp_cascade_design(fs, bw * 0.9f);  // ssb.rs:25
-    st_ = std::make_unique<ScanStage>(RecK::LP4, Pre::Real, Post::Id, lp_cascade_ss(b_), coef_lp(b_), 2);
+    const StateSpace ss = lp_cascade_ss(b_);
+    st_ = std::make_unique<ScanStage>(RecK::LP4, Pre::Real, Post::Id, ss, coef_lp(b_), 2);
     st_->set_carry(carry_zero());
+    // one pass when the LP4 forgets its state within the kSpWarm-sample warm-up
+    const auto m = mat_pow(ss.A, 4, kSpWarm);
+    double fro = 0.0;
+    for (double v : m) fro += v * v;
+    sp_ok_ = std::sqrt(fro) < 1e-10;
+    if (sp_ok_) {
+      const auto ml = ScanStage::build_mats(ss);
+      mats_.upload(ml.data(), ml.size() * sizeof(double));
+      for (auto& c : carry_) c.resize(8 * sizeof(float));
+    }
+    reset_sp();
   }
   const char* name() const override { return "SsbPhasingMod"; }
   Dt in_type() const override { return Dt::F32; }
@@ -250,27 +262,45 @@ class SsbModBlock final : public Block {
     const size_t n = std::min(n_in, out_cap);  // ssb.rs:44
     if (n == 0) return {0, 0};
     const long long nn = static_cast<long long>(n);
-    u_.resize(2 * n * sizeof(float));
-    v_.resize(2 * n * sizeof(float));
-    launch_ssb_mod_front(static_cast<const float*>(in), u_.as<float>(), nn, k_, aud_.step_q64, s);
-    st_->run(u_.as<void>(), nn, nn, v_.as<void>(), nn, static_cast<long long>(k_), s);
-    launch_ssb_mod_back(v_.as<float>(), static_cast<f2*>(out), nn, k_, rf_.step_q64, side_, s);
+    if (sp_ok_ && mode_ == 0) {
+      launch_ssb_mod_sp(static_cast<const float*>(in), static_cast<f2*>(out), nn, k_, aud_.step_q64, rf_.step_q64,
+                        side_, coef_lp(b_), mats_.as<double>(), carry_[cur_].as<float>(), carry_[cur_ ^ 1].as<float>(),
+                        s);
+      cur_ ^= 1;
+    } else {
+      u_.resize(2 * n * sizeof(float));
+      v_.resize(2 * n * sizeof(float));
+      launch_ssb_mod_front(static_cast<const float*>(in), u_.as<float>(), nn, k_, aud_.step_q64, s);
+      st_->run(u_.as<void>(), nn, nn, v_.as<void>(), nn, static_cast<long long>(k_), s);
+      launch_ssb_mod_back(v_.as<float>(), static_cast<f2*>(out), nn, k_, rf_.step_q64, side_, s);
+    }
     k_ += n;
     return {n, n};
   }
   void reset() override {
     k_ = 0;
     st_->set_carry(carry_zero());
+    reset_sp();
     ORION_HIP(hipDeviceSynchronize());
   }
+  // 0 auto (single pass where valid), 1 the three-pass form (tests)
+  void set_mode(int m) { mode_ = m; }
   std::vector<float> taps(int) const override { return {b_.b0, b_.b1, b_.b2, b_.a1, b_.a2}; }
 
  private:
+  void reset_sp() {
+    if (!sp_ok_) return;
+    const std::vector<float> z(8, 0.0f);
+    for (auto& c : carry_) c.upload(z.data(), z.size() * sizeof(float));
+    cur_ = 0;
+  }
   Oscillator aud_, rf_;
   float side_;
   BiquadCoeffs b_;
   std::unique_ptr<ScanStage> st_;
-  DevBuf u_, v_;
+  DevBuf u_, v_, mats_, carry_[2];
+  bool sp_ok_ = false;
+  int mode_ = 0, cur_ = 0;
   uint64_t k_ = 0;
 };
 

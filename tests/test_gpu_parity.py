@@ -481,17 +481,19 @@ def test_fm_phase_accum_mod(gpu_lib, oracle):
     report("fm_mod dev 50k gain 0.5 baseband max abs", float(np.max(np.abs(g.process(aud[:65536]) - ref2))), 2e-5)
 
 
-@pytest.mark.parametrize("usb,rf", [(True, 0.0), (False, 6e3)])
-def test_ssb_phasing_mod(gpu_lib, oracle, usb, rf):
-    """ssb.rs:43-114: audio NCO products, both LpCascades (one 2-channel scan),
-    (I, side Q) x RF NCO; and the mod -> SsbProductDemod round trip."""
+@pytest.mark.parametrize("usb,rf,fs", [(True, 0.0, FS), (False, 6e3, FS), (True, 20e3, 1e6)])
+def test_ssb_phasing_mod(gpu_lib, oracle, usb, rf, fs):
+    """ssb.rs:43-114: audio NCO products, both LpCascades, (I, side Q) x RF NCO;
+    at 48 kHz the one-pass kernel (the LP4 forgets within its 256-sample
+    warm-up), at 1 MHz the three-pass form (2-channel scan); streamed calls with
+    ragged cuts; and the mod -> SsbProductDemod round trip."""
     n = (1 << 18) + 3
-    a = real_tone(FS, 1200.0, n, 0.5)
-    m = gpu_lib.SsbPhasingMod(FS, 2800.0, 1500.0, rf, usb)
-    got = np.concatenate([m.process(a[:70_000]), m.process(a[70_000:])])
-    ref = oracle.ssb_mod(a, FS, 2800.0, 1500.0, rf, usb)
+    a = real_tone(fs, 1200.0, n, 0.5)
+    m = gpu_lib.SsbPhasingMod(fs, 2800.0, 1500.0, rf, usb)
+    got = np.concatenate([m.process(a[:70_000]), m.process(a[70_000:70_001]), m.process(a[70_001:])])
+    ref = oracle.ssb_mod(a, fs, 2800.0, 1500.0, rf, usb)
     # SURVEY §8c: SSB 1e-4 (NCO phase drift is not differential)
-    report(f"ssb_mod usb={usb} rf={rf} nrmse", nrmse(got, ref), 1e-4)
+    report(f"ssb_mod usb={usb} rf={rf} fs={fs} nrmse", nrmse(got, ref), 1e-4)
     if rf == 0.0:
         d = gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0).process(got)
         report("ssb mod -> demod round trip vs oracle nrmse", nrmse(d, oracle.ssb_demod(ref, FS, 1500.0, 2800.0)), 1e-4)
