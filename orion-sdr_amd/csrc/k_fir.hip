@@ -14,6 +14,10 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int kMaxGrid = 2048;  // memory-bound: cap and grid-stride (2048 = 8 WG per CU)
+#ifndef ORION_FIR_HT
+#define ORION_FIR_HT 4
+#endif
+constexpr int kFirHT = ORION_FIR_HT;  // 512-output halves per complex-FIR tile
 
 // ------------------------------------------------------------------ NCO --
 template <bool A16, bool USB>
@@ -338,31 +342,51 @@ __global__ __launch_bounds__(NT) void k_fir_real_generic(const float* __restrict
 }
 
 // ------------------------------------------------------ complex FIR -------
-template <int KP>
+// HT halves of 512 outputs per tile: one load round trip (behind one barrier)
+// feeds HT x 512 outputs, so a workgroup keeps HT times the bytes in flight.
+template <int KP, int HT>
 __global__ __launch_bounds__(NT) void k_fir_iq(const f2* __restrict__ x, long long n,
                                                const f2* __restrict__ hist, int hist_len,
                                                f2* __restrict__ y, long long n_out, long long off,
                                                const Taps256 g) {
-  constexpr int TT = 512;
+  constexpr int TH = 512, TT = TH * HT;
   __shared__ __attribute__((aligned(16))) f2 L[TT + KP + 2];
   const int t = threadIdx.x;
   for (long long J = static_cast<long long>(blockIdx.x) * TT; J < n_out;
        J += static_cast<long long>(gridDim.x) * TT) {
     const long long org = J + off - KP;
-    for (int p = t; p < TT + KP + 2; p += NT) L[p] = load_hist(x, n, hist, hist_len, org + p);
+    constexpr int W = TT + KP + 2, PER = (W + NT - 1) / NT;
+    if (org >= 0 && org + W <= n) {  // interior tile: every load issued before any is used
+      f2 v[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int p = t + k * NT;
+        v[k] = p < W ? x[org + p] : f2{0.0f, 0.0f};
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int p = t + k * NT;
+        if (p < W) L[p] = v[k];
+      }
+    } else {
+      for (int p = t; p < W; p += NT) L[p] = load_hist(x, n, hist, hist_len, org + p);
+    }
     __syncthreads();
-    f2 acc0 = f2{0.0f, 0.0f}, acc1 = f2{0.0f, 0.0f};
-    // element e (= input index i + off) <-> L[e - org]
-    fir2_blocked<KP>(
-        [&](long long i, f2& w0, f2& w1) {
-          const f4 v = *reinterpret_cast<const f4*>(L + (i - org));
-          w0 = f2{v.x, v.y};
-          w1 = f2{v.z, v.w};
-        },
-        J + off + 2 * t, [&](int k) { return g.g[k]; }, acc0, acc1);
-    const long long j = J + 2 * t;
-    if (j < n_out) y[j] = acc0;
-    if (j + 1 < n_out) y[j + 1] = acc1;
+#pragma unroll
+    for (int h = 0; h < HT; ++h) {
+      f2 acc0 = f2{0.0f, 0.0f}, acc1 = f2{0.0f, 0.0f};
+      // element e (= input index i + off) <-> L[e - org]
+      fir2_blocked<KP>(
+          [&](long long i, f2& w0, f2& w1) {
+            const f4 v = *reinterpret_cast<const f4*>(L + (i - org));
+            w0 = f2{v.x, v.y};
+            w1 = f2{v.z, v.w};
+          },
+          J + h * TH + off + 2 * t, [&](int k) { return g.g[k]; }, acc0, acc1);
+      const long long j = J + h * TH + 2 * t;
+      if (j < n_out) y[j] = acc0;
+      if (j + 1 < n_out) y[j + 1] = acc1;
+    }
     __syncthreads();
   }
 }
@@ -501,9 +525,9 @@ void launch_fir_iq(const f2* x, long long n, const f2* hist, int hist_len, f2* y
                    long long off, int K, const Taps256& g, const float* g_dev, hipStream_t s) {
   if (n_out <= 0) return;
   const int grid = grid_for(n_out, 512);
-  if (K <= 64 && hist_len >= 64) k_fir_iq<64><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
-  else if (K <= 128 && hist_len >= 128) k_fir_iq<128><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
-  else if (K <= 256 && hist_len >= 256) k_fir_iq<256><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
+  if (K <= 64 && hist_len >= 64) k_fir_iq<64, kFirHT><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
+  else if (K <= 128 && hist_len >= 128) k_fir_iq<128, kFirHT><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
+  else if (K <= 256 && hist_len >= 256) k_fir_iq<256, kFirHT><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
   else k_fir_iq_generic<<<grid_for(n_out, NT), NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, K, g_dev);
   ORION_LAUNCH_CHECK();
 }
