@@ -144,6 +144,8 @@ class FmModBlock final : public Block {
  public:
   FmModBlock(float fs, float dev_hz, float rf_hz) : fs_(fs), dev_(dev_hz), osc_(oscillator(rf_hz, fs)) {
     for (auto& c : carry_) c.resize(sizeof(double));
+    const auto t = phasor_table(osc_.theta, static_cast<size_t>(fm_mod_rtab_len()));
+    rtab_.upload(t.data(), t.size() * sizeof(float));
     reset();
   }
   const char* name() const override { return "FmPhaseAccumMod"; }
@@ -155,7 +157,8 @@ class FmModBlock final : public Block {
     const float kf = kTauF * dev_ / fs_;  // fm.rs:48, f32 as in the reference
     sums_.resize(static_cast<size_t>(fm_mod_chunks(static_cast<long long>(n))) * sizeof(double));
     launch_fm_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), kf, g_,
-                  sums_.as<double>(), carry_[cur_].as<double>(), carry_[cur_ ^ 1].as<double>(), k_, osc_.step_q64, s);
+                  sums_.as<double>(), carry_[cur_].as<double>(), carry_[cur_ ^ 1].as<double>(), k_, osc_.step_q64,
+                  rtab_.as<f2>(), s);
     cur_ ^= 1;
     k_ += n;
     return {n, n};
@@ -173,7 +176,7 @@ class FmModBlock final : public Block {
  private:
   float fs_, dev_, g_ = 1.0f;
   Oscillator osc_;
-  DevBuf carry_[2], sums_;
+  DevBuf carry_[2], sums_, rtab_;
   int cur_ = 0;
   uint64_t k_ = 0;
 };

@@ -144,7 +144,7 @@ __global__ __launch_bounds__(NT) void k_fm_mod_carry(double* __restrict__ sums, 
 // mix_with_nco's non-FMA complex product with the RF phasor (nco.rs:62-66).
 __global__ __launch_bounds__(NT) void k_fm_mod_apply(const float* __restrict__ x, f2* __restrict__ y, long long n,
                                                      float kf, float gain, const double* __restrict__ offs,
-                                                     uint64_t k0, uint64_t step) {
+                                                     uint64_t k0, uint64_t step, const f2* __restrict__ rtab) {
   __shared__ double tot[NT / 64];
   __shared__ float xs[kFmCH + kFmCH / 16];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -174,16 +174,19 @@ __global__ __launch_bounds__(NT) void k_fm_mod_apply(const float* __restrict__ x
   __syncthreads();
   double phi = offs[blockIdx.x] + inc - run;
   for (int k = 0; k < w; ++k) phi += tot[k];
+  // RF phasor of sample i0 + k = (phasor of i0) x e^{j theta k} (rtab: k < kFmC)
+  const long long i0 = base + t * kFmC;
+  const f2 R0 = phasor_q64(k0 + static_cast<uint64_t>(i0) + 1, step);
 #pragma unroll
   for (int k = 0; k < kFmC; ++k) {
-    const long long i = base + t * kFmC + k;
+    const long long i = i0 + k;
     phi += d[k];
     if (i < n) {
       const double red = phi - 6.283185307179586 * rint(phi * 0.15915494309189535);
       float s, c;
       sincosf(static_cast<float>(red), &s, &c);
       const f2 b = f2{c * gain, s * gain};  // fm.rs:66 base = z * gain
-      const f2 r = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
+      const f2 r = cmul(R0, rtab[k]);
       y[i] = f2{b.x * r.x - b.y * r.y, b.x * r.y + b.y * r.x};  // nco.rs:65 (no FMA)
     }
   }
@@ -211,16 +214,18 @@ void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, uint64
 }
 
 long long fm_mod_chunks(long long n) { return (n + kFmCH - 1) / kFmCH; }
+int fm_mod_rtab_len() { return kFmC; }
 
 void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, double* sums,
-                   const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, hipStream_t s) {
+                   const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
+                   hipStream_t s) {
   if (n <= 0) return;
   const long long nchunk = fm_mod_chunks(n);
   if (nchunk > (1LL << 30)) throw HipError("FM modulator: input too long");
   const int g = static_cast<int>(nchunk);
   k_fm_mod_sum<<<g, NT, 0, s>>>(x, n, kf, sums);
   k_fm_mod_carry<<<1, NT, 0, s>>>(sums, g, carry_in, carry_out);
-  k_fm_mod_apply<<<g, NT, 0, s>>>(x, y, n, kf, gain, sums, k0, step);
+  k_fm_mod_apply<<<g, NT, 0, s>>>(x, y, n, kf, gain, sums, k0, step, rtab);
   ORION_LAUNCH_CHECK();
 }
 

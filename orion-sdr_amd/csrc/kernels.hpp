@@ -24,9 +24,12 @@ void launch_ssb_mod_front(const float* x, float* u, long long n, uint64_t k0, ui
 void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, uint64_t step, float side, hipStream_t s);
 // FM phase accumulator: sums = fm_mod_chunks(n) doubles of workspace; carry_in /
 // carry_out: the running phase (one double each, ping-pong between calls)
+// rtab: e^{j theta k}, k < fm_mod_rtab_len(), of the RF oscillator
 long long fm_mod_chunks(long long n);
+int fm_mod_rtab_len();
 void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, double* sums,
-                   const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, hipStream_t s);
+                   const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
+                   hipStream_t s);
 void launch_rotator(const f2* x_dev, f2* y_dev, long long n, uint64_t k0, uint64_t step_q64,
                     const f2* tab_dev, hipStream_t s);
 // SsbProductDemod front end helper / Rotator::mix_usb_block (rotator.rs:88-94):
