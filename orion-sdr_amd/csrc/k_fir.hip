@@ -391,6 +391,78 @@ __global__ __launch_bounds__(NT) void k_fir_iq(const f2* __restrict__ x, long lo
   }
 }
 
+// Eight consecutive outputs per lane (2048 per workgroup tile): per 16-tap block
+// a lane reads a 24-sample window (12 ds_read_b128) for 128 packed FMAs, 3.6x
+// the FMAs per LDS read of two outputs per lane. The staged tile is padded by 2
+// samples per 8 (lane stride 80 B: the 16-lane b128 groups hit distinct bank
+// slots).
+template <int KP>
+__global__ __launch_bounds__(NT) void k_fir_iq8(const f2* __restrict__ x, long long n,
+                                                const f2* __restrict__ hist, int hist_len,
+                                                f2* __restrict__ y, long long n_out, long long off,
+                                                const Taps256 g) {
+  constexpr int TT = 8 * NT;
+  constexpr int W = TT + KP + 2, PER = (W + NT - 1) / NT;
+  constexpr int WP = W + 2 * (W / 8) + 2;
+  static_assert(KP % 16 == 0, "taps padded to 16");
+  __shared__ __attribute__((aligned(16))) f2 L[WP];
+  auto pidx = [](int p) { return p + 2 * (p >> 3); };
+  const int t = threadIdx.x;
+  for (long long J = static_cast<long long>(blockIdx.x) * TT; J < n_out;
+       J += static_cast<long long>(gridDim.x) * TT) {
+    const long long org = J + off - KP;  // staged sample p <-> element org + p
+    if (org >= 0 && org + W <= n) {
+      f2 v[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int p = t + k * NT;
+        v[k] = p < W ? x[org + p] : f2{0.0f, 0.0f};
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int p = t + k * NT;
+        if (p < W) L[pidx(p)] = v[k];
+      }
+    } else {
+      for (int p = t; p < W; p += NT) L[pidx(p)] = load_hist(x, n, hist, hist_len, org + p);
+    }
+    __syncthreads();
+    f2 acc[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = f2{0.0f, 0.0f};
+#pragma unroll 1
+    for (int kb = 0; kb < KP / 16; ++kb) {
+      // output j0 + r, tap 16 kb + kk reads element j0 + off + r - 16 kb - kk =
+      // staged p = pb + 16 + r - kk, pb = 8 t + KP - 16 kb - 16 (even, >= 0)
+      const int pb = 8 * t + KP - 16 * kb - 16;
+      f2 w[24];
+#pragma unroll
+      for (int h = 0; h < 12; ++h) {
+        const f4 v = *reinterpret_cast<const f4*>(L + pidx(pb + 2 * h));
+        w[2 * h] = f2{v.x, v.y};
+        w[2 * h + 1] = f2{v.z, v.w};
+      }
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const f2 tap = splat2(g.g[16 * kb + kk]);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc[r] = fma2(tap, w[16 + r - kk], acc[r]);
+      }
+    }
+    const long long j0 = J + 8 * t;
+    if (j0 + 8 <= n_out && (reinterpret_cast<uintptr_t>(y + j0) & 15) == 0) {
+      f4* yo = reinterpret_cast<f4*>(y + j0);
+#pragma unroll
+      for (int r = 0; r < 8; r += 2) yo[r / 2] = f4{acc[r].x, acc[r].y, acc[r + 1].x, acc[r + 1].y};
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (j0 + r < n_out) y[j0 + r] = acc[r];
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(NT) void k_fir_iq_generic(const f2* __restrict__ x, long long n,
                                                        const f2* __restrict__ hist, int hist_len,
                                                        f2* __restrict__ y, long long n_out,
@@ -525,7 +597,16 @@ void launch_fir_iq(const f2* x, long long n, const f2* hist, int hist_len, f2* y
                    long long off, int K, const Taps256& g, const float* g_dev, hipStream_t s) {
   if (n_out <= 0) return;
   const int grid = grid_for(n_out, 512);
-  if (K <= 64 && hist_len >= 64) k_fir_iq<64, kFirHT><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
+  static const bool legacy = [] {  // timing comparisons only: two outputs per lane
+    const char* e = std::getenv("ORION_FIR_IQ2");
+    return e && std::atoi(e) != 0;
+  }();
+  if (!legacy && K <= 256 && hist_len >= (K <= 64 ? 64 : K <= 128 ? 128 : 256)) {
+    const int g8 = grid_for(n_out, 8 * NT);
+    if (K <= 64) k_fir_iq8<64><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
+    else if (K <= 128) k_fir_iq8<128><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
+    else k_fir_iq8<256><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
+  } else if (K <= 64 && hist_len >= 64) k_fir_iq<64, kFirHT><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
   else if (K <= 128 && hist_len >= 128) k_fir_iq<128, kFirHT><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
   else if (K <= 256 && hist_len >= 256) k_fir_iq<256, kFirHT><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
   else k_fir_iq_generic<<<grid_for(n_out, NT), NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, K, g_dev);
