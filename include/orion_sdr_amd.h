@@ -99,6 +99,10 @@ int orion_cw_envelope_demod_set_gain(orion_block* b, float g);
 /* modulate/am.rs:20-30 AmDsbMod::new(fs, rf_hz, carrier_level, modulation_index);
  * set_gain :31-33, set_clamp :34-36 (ORION_E_TYPE on another block). */
 orion_block* orion_am_dsb_mod_new(float fs, float rf_hz, float carrier_level, float modulation_index);
+/* dsp/agc.rs:20-31 AgcRms::new(fs, attack_ms, release_ms, target_rms); process :48-75. f32->f32 */
+orion_block* orion_agc_rms_new(float fs, float attack_ms, float release_ms, float target_rms);
+/* dsp/agc.rs:93-106 AgcRmsIq::new(fs, attack_ms, release_ms, target_rms); process :124-150. cf32->cf32 */
+orion_block* orion_agc_rms_iq_new(float fs, float attack_ms, float release_ms, float target_rms);
 int orion_am_dsb_mod_set_gain(orion_block* b, float g);
 int orion_am_dsb_mod_set_clamp(orion_block* b, int on);
 /* modulate/fm.rs:21-32 FmPhaseAccumMod::new(sample_rate, deviation_hz, rf_hz);

@@ -77,6 +77,7 @@ def lib():
         "o_run_ssb_demod_channels": (_sz, [_f, _f, _f, _sz, _c64p, _sz, _f32p, _sz]),
         "o_run_decim_channels": (_sz, [_f, _sz, _f, _f, _sz, _c64p, _sz, _c64p, _sz]),
         "o_add_awgn": (None, [_c64p, _sz, _f, C.c_uint64]),
+        "o_run_agc": (_f, [C.c_int, _f, _f, _f, _f, C.c_void_p, C.c_void_p, _sz, _sz]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -183,6 +184,16 @@ def dc_blocker(x, fs, cut_hz, chunk=0):
     y = np.empty_like(x)
     lib().o_run_dc(fs, cut_hz, x, y, len(x), chunk)
     return y
+
+
+def agc(x, fs, attack_ms, release_ms, target_rms, chunk=0):
+    """dsp/agc.rs AgcRms (real input) / AgcRmsIq (complex input). Returns (out, end env)."""
+    iq = np.iscomplexobj(x)
+    x = _c64(x) if iq else _f32(x)
+    y = np.empty_like(x)
+    env = lib().o_run_agc(int(iq), fs, attack_ms, release_ms, target_rms,
+                          x.ctypes.data, y.ctypes.data, len(x), chunk)
+    return y, env
 
 
 def fm_demod(x, fs, dev_hz, audio_bw_hz, translate_hz=None, chunk=0):

@@ -847,3 +847,44 @@ size_t o_run_decim_channels(float fs, size_t m, float cutoff_hz, float trans_hz,
     o_pool_run(&P, nthreads);
     return nch * ((n + m - 1) / m);
 }
+
+/* ------------------------------------------------------------------ */
+/* dsp/agc.rs:20-31 AgcRms::new / :93-106 AgcRmsIq::new; update_env    */
+/* :32-41 / :108-116; process :48-75 / :124-150. iq != 0: cf32 input.  */
+/* Rust's f32 ops: no FMA contraction (-ffp-contract=off), expf/sqrtf. */
+typedef struct { float attack_a, release_a, target_rms, min_gain, max_gain, env; } o_agc;
+static void o_agc_init(o_agc *a, float fs, float attack_ms, float release_ms, float target_rms) {
+    a->attack_a = expf(-1.0f / (fs * (o_maxf(attack_ms, 1e-3f) / 1000.0f)));
+    a->release_a = expf(-1.0f / (fs * (o_maxf(release_ms, 1e-3f) / 1000.0f)));
+    a->target_rms = o_maxf(target_rms, 1e-6f);
+    a->min_gain = 0.05f;
+    a->max_gain = 20.0f;
+    a->env = 0.0f;
+}
+static void o_agc_process(o_agc *a, int iq, const float *in, float *out, size_t n) {
+    if (n == 0) return;
+    if (a->env == 0.0f) {  /* agc.rs:57-60 / :133-136 seed */
+        float x2 = iq ? in[0] * in[0] + in[1] * in[1] : in[0] * in[0];
+        a->env = o_maxf(x2, 1e-12f);
+    }
+    float env = a->env;
+    for (size_t i = 0; i < n; i++) {
+        float re = iq ? in[2 * i] : in[i], im = iq ? in[2 * i + 1] : 0.0f;
+        float x2 = iq ? re * re + im * im : re * re;
+        float k = x2 > env ? a->attack_a : a->release_a;
+        env = k * env + (1.0f - k) * x2;
+        float rms = o_maxf(sqrtf(env), 1e-6f);
+        float g = a->target_rms / rms;
+        g = g < a->min_gain ? a->min_gain : (g > a->max_gain ? a->max_gain : g);
+        if (iq) { out[2 * i] = g * re; out[2 * i + 1] = g * im; } else out[i] = g * re;
+    }
+    a->env = env;
+}
+/* Streams n samples through one AGC in calls of `chunk` (0 = one call); returns the end env. */
+float o_run_agc(int iq, float fs, float attack_ms, float release_ms, float target_rms,
+                const float *in, float *out, size_t n, size_t chunk) {
+    o_agc a; o_agc_init(&a, fs, attack_ms, release_ms, target_rms);
+    const size_t w = iq ? 2 : 1;
+    for (size_t i = 0; i < n;) { size_t c = o_step(chunk, n - i); o_agc_process(&a, iq, in + w * i, out + w * i, c); i += c; }
+    return a.env;
+}

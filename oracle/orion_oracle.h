@@ -201,6 +201,9 @@ size_t o_run_ssb_demod_channels(float fs, float bfo_hz, float audio_bw_hz, size_
                                 size_t n, float *out, size_t nthreads);
 size_t o_run_decim_channels(float fs, size_t m, float cutoff_hz, float trans_hz, size_t nch,
                             const oc32 *in, size_t n, oc32 *out, size_t nthreads);
+/* dsp/agc.rs AgcRms (iq = 0, f32) / AgcRmsIq (iq = 1, cf32 interleaved); returns the end env. */
+float o_run_agc(int iq, float fs, float attack_ms, float release_ms, float target_rms,
+                const float *in, float *out, size_t n, size_t chunk);
 
 #ifdef __cplusplus
 }

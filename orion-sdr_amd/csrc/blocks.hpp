@@ -96,6 +96,7 @@ std::unique_ptr<Block> make_fm_mod(float fs, float deviation_hz, float rf_hz);  
 int mod_set_gain(Block* b, float g);             // AmDsbMod / FmPhaseAccumMod set_gain; -4 other blocks
 int am_mod_set_clamp(Block* b, bool on);         // -4 if not an AmDsbMod
 int fm_mod_set_deviation(Block* b, float d);     // -4 if not an FmPhaseAccumMod
+std::unique_ptr<Block> make_agc(bool iq, float fs, float attack_ms, float release_ms, float target_rms);  // agc.rs
 
 // The WBFM chain (docs/demodulate.md:128-133): Rotator(-f_off) -> FirDecimator
 // (fs, m=8, dec_cutoff, dec_trans) -> FmQuadratureDemod(fs/8, dev, audio_bw) ->

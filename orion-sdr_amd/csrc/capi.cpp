@@ -104,6 +104,12 @@ int orion_fir_lowpass_iq_filter_aligned(orion_block* b, void* io, size_t n) {
     return ORION_OK;
   });
 }
+orion_block* orion_agc_rms_new(float fs, float attack_ms, float release_ms, float target_rms) {
+  return make([&] { return orion::make_agc(false, fs, attack_ms, release_ms, target_rms); });
+}
+orion_block* orion_agc_rms_iq_new(float fs, float attack_ms, float release_ms, float target_rms) {
+  return make([&] { return orion::make_agc(true, fs, attack_ms, release_ms, target_rms); });
+}
 orion_block* orion_am_dsb_mod_new(float fs, float rf_hz, float carrier_level, float modulation_index) {
   return make([&] { return orion::make_am_mod(fs, rf_hz, carrier_level, modulation_index); });
 }

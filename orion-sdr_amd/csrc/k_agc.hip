@@ -1,0 +1,150 @@
+// k_agc.hip — AgcRms / AgcRmsIq (dsp/agc.rs:7-150) on the device.
+//
+// The reference's envelope is a data-dependent recurrence
+//   env <- a(x2 > env) * env + (1 - a) * x2,  a in {attack_a, release_a}
+// (agc.rs:33-41). As a map of env it is continuous at env = x2 (both branches give
+// x2) and piecewise linear with slopes attack_a and release_a, so two trajectories
+// over the same input approach each other by at least amax = max(attack_a,
+// release_a) per sample. Each lane owns a chunk of L samples and starts W samples
+// early from a guess (the seed rule of agc.rs:57-60 applied at that sample); the
+// host picks W with amax^W < 1e-9, so the entering envelope of every chunk is the
+// sequential one to |env error| <= 1e-9 * max x2 (in practice the f32 trajectories
+// meet exactly). Chunk 0 starts from the carried state, as the reference does.
+// Per sample: the reference's f32 ops in its order, no FMA contraction
+// (-ffp-contract=off), correctly rounded sqrt and divide.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <stdexcept>
+
+#include "blocks.hpp"
+#include "hip_common.hpp"
+
+namespace orion {
+namespace {
+
+struct AgcK {
+  float att, rel, tgt, gmin, gmax;
+};
+
+template <bool IQ>
+__device__ __forceinline__ float agc_x2(const float* in, long long i) {
+  if constexpr (IQ) {
+    const float2 v = reinterpret_cast<const float2*>(in)[i];
+    return v.x * v.x + v.y * v.y;
+  } else {
+    const float v = in[i];
+    return v * v;
+  }
+}
+
+template <bool IQ>
+__global__ __launch_bounds__(256) void k_agc(const float* __restrict__ in, float* __restrict__ out,
+                                             long long n, long long L, long long W, AgcK k,
+                                             const float* __restrict__ env_in, float* __restrict__ env_out) {
+  const long long c = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const long long b = c * L;
+  if (b >= n) return;
+  const long long e = b + L < n ? b + L : n;
+  float env;
+  long long i;
+  if (c == 0) {
+    env = env_in[0];
+    if (env == 0.0f) env = fmaxf(agc_x2<IQ>(in, 0), 1e-12f);  // agc.rs:57-60
+    i = 0;
+  } else {
+    i = b - W > 0 ? b - W : 0;
+    env = fmaxf(agc_x2<IQ>(in, i), 1e-12f);
+  }
+  for (; i < b; ++i) {  // warm-up: envelope only
+    const float x2 = agc_x2<IQ>(in, i);
+    const float a = x2 > env ? k.att : k.rel;
+    env = a * env + (1.0f - a) * x2;
+  }
+  for (; i < e; ++i) {
+    float re, im = 0.0f, x2;
+    if constexpr (IQ) {
+      const float2 v = reinterpret_cast<const float2*>(in)[i];
+      re = v.x; im = v.y;
+      x2 = re * re + im * im;
+    } else {
+      re = in[i];
+      x2 = re * re;
+    }
+    const float a = x2 > env ? k.att : k.rel;
+    env = a * env + (1.0f - a) * x2;
+    const float rms = fmaxf(sqrtf(env), 1e-6f);
+    const float g = fminf(fmaxf(k.tgt / rms, k.gmin), k.gmax);
+    if constexpr (IQ) {
+      reinterpret_cast<float2*>(out)[i] = make_float2(g * re, g * im);
+    } else {
+      out[i] = g * re;
+    }
+  }
+  if (e == n) env_out[0] = env;
+}
+
+class AgcBlock final : public Block {
+ public:
+  AgcBlock(bool iq, float fs, float attack_ms, float release_ms, float target_rms) : iq_(iq) {
+    // agc.rs:21 / :97: a(ms) = exp(-1 / (fs * (max(ms, 1e-3) / 1000)))
+    auto coef = [fs](float ms) { return std::exp(-1.0f / (fs * (std::max(ms, 1e-3f) / 1000.0f))); };
+    k_.att = coef(attack_ms);
+    k_.rel = coef(release_ms);
+    k_.tgt = std::max(target_rms, 1e-6f);
+    k_.gmin = 0.05f;
+    k_.gmax = 20.0f;
+    const double amax = std::max(k_.att, k_.rel);
+    // amax^W < 1e-9; amax == 1 (or NaN) never forgets: one sequential lane.
+    warm_ = amax < 1.0 ? static_cast<long long>(std::ceil(std::log(1e-9) / std::log(amax))) : -1;
+    env_.resize(2 * sizeof(float));
+    env_.zero();
+  }
+  const char* name() const override { return iq_ ? "AgcRmsIq" : "AgcRms"; }
+  Dt in_type() const override { return iq_ ? Dt::C32 : Dt::F32; }
+  Dt out_type() const override { return iq_ ? Dt::C32 : Dt::F32; }
+  WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
+    const long long n = static_cast<long long>(std::min(n_in, out_cap));  // agc.rs:49
+    if (n == 0) return {0, 0};
+    // Chunk length: at least the warm-up (<= 2x envelope work), at least 1024.
+    const long long L = warm_ < 0 ? n : std::max<long long>(1024, warm_);
+    const long long chunks = (n + L - 1) / L;
+    float* e = env_.as<float>();
+    float* ein = e + cur_;
+    float* eout = e + (cur_ ^ 1);
+    const unsigned grid = static_cast<unsigned>((chunks + 255) / 256);
+    const float* x = static_cast<const float*>(in);
+    float* y = static_cast<float*>(out);
+    if (iq_) {
+      hipLaunchKernelGGL(k_agc<true>, dim3(grid), dim3(256), 0, s, x, y, n, L, warm_ < 0 ? 0 : warm_, k_, ein, eout);
+    } else {
+      hipLaunchKernelGGL(k_agc<false>, dim3(grid), dim3(256), 0, s, x, y, n, L, warm_ < 0 ? 0 : warm_, k_, ein, eout);
+    }
+    ORION_HIP(hipGetLastError());
+    cur_ ^= 1;
+    return {static_cast<size_t>(n), static_cast<size_t>(n)};
+  }
+  void reset() override {
+    env_.zero();
+    cur_ = 0;
+  }
+  std::vector<float> taps(int) const override {
+    return {k_.att, k_.rel, k_.tgt, static_cast<float>(warm_)};
+  }
+
+ private:
+  bool iq_;
+  AgcK k_{};
+  long long warm_ = 0;
+  DevBuf env_;  // two floats: the carried envelope, ping-ponged per call
+  int cur_ = 0;
+};
+
+}  // namespace
+
+std::unique_ptr<Block> make_agc(bool iq, float fs, float attack_ms, float release_ms, float target_rms) {
+  return std::make_unique<AgcBlock>(iq, fs, attack_ms, release_ms, target_rms);
+}
+
+}  // namespace orion

@@ -26,7 +26,7 @@ import numpy as np
 __all__ = [
     "Rotator", "FirDecimator", "FirLowpass", "FirLowpassIq", "LpCascade", "DcBlocker",
     "FmQuadratureDemod", "PmQuadratureDemod", "SsbProductDemod", "AmEnvelopeDemod",
-    "CwEnvelopeDemod", "WbfmChain", "AmDsbMod", "FmPhaseAccumMod", "SsbPhasingMod",
+    "CwEnvelopeDemod", "WbfmChain", "AgcRms", "AgcRmsIq", "AmDsbMod", "FmPhaseAccumMod", "SsbPhasingMod",
     "fir_lowpass_design", "kaiser_lowpass_taps",
     "kaiser_transition_norm", "kaiser_num_taps", "lp_cascade_design", "lib_path", "OrionError",
     "AudioToIqChain", "IqToIqChain", "IqToAudioChain", "Graph", "stream_shard", "STREAM_HALO",
@@ -86,6 +86,8 @@ def _load():
         "orion_cw_envelope_demod_new": (vp, [f, f, f]),
         "orion_cw_envelope_demod_set_gain": (i, [vp, f]),
         "orion_am_dsb_mod_new": (vp, [f, f, f, f]),
+        "orion_agc_rms_new": (vp, [f, f, f, f]),
+        "orion_agc_rms_iq_new": (vp, [f, f, f, f]),
         "orion_am_dsb_mod_set_gain": (i, [vp, f]),
         "orion_am_dsb_mod_set_clamp": (i, [vp, i]),
         "orion_fm_phase_accum_mod_new": (vp, [f, f, f]),
@@ -347,6 +349,20 @@ class PmQuadratureDemod(_Block):
 
 
 # ---- analog modulators (src/modulate): f32 audio -> complex64 IQ ----
+class AgcRms(_Block):
+    """dsp/agc.rs:20-31 AgcRms::new(fs, attack_ms, release_ms, target_rms): real audio AGC."""
+
+    def __init__(self, fs: float, attack_ms: float, release_ms: float, target_rms: float):
+        super().__init__(_L.orion_agc_rms_new(fs, attack_ms, release_ms, target_rms))
+
+
+class AgcRmsIq(_Block):
+    """dsp/agc.rs:93-106 AgcRmsIq::new(fs, attack_ms, release_ms, target_rms): one gain on I and Q."""
+
+    def __init__(self, fs: float, attack_ms: float, release_ms: float, target_rms: float):
+        super().__init__(_L.orion_agc_rms_iq_new(fs, attack_ms, release_ms, target_rms))
+
+
 class AmDsbMod(_Block):
     """modulate/am.rs:20-36: carrier_level 1 -> full carrier (A3E), 0 -> DSB-SC."""
 

@@ -3,6 +3,7 @@ property / threshold test the reference holds for this path.
 
 These pin the oracle before any GPU result is compared with it.
 """
+import math
 import os
 
 import numpy as np
@@ -228,3 +229,44 @@ def test_wbfm_chain_recovers_audio(oracle):
     assert len(y) == (1 << 20) // 8
     assert snr_db(tail(y), 1.25e6, 1000.0) > 30.0
     assert 5e-7 < float(np.sqrt(np.mean(tail(y) ** 2))) < 5e-6
+
+
+# ---- AGC (dsp/agc.rs) ---------------------------------------------
+def _agc_py(x, fs, attack_ms, release_ms, target):
+    """Pure-Python f32 restatement of agc.rs:20-75 / :93-150 (small n only)."""
+    f = np.float32
+    coef = lambda ms: f(math.exp(float(f(-1.0) / (f(fs) * (f(max(ms, 1e-3)) / f(1000.0))))))  # expf, rounded once
+    att, rel, tgt = coef(attack_ms), coef(release_ms), f(max(target, 1e-6))
+    iq = np.iscomplexobj(x)
+    x2s = [(f(v.real) * f(v.real) + f(v.imag) * f(v.imag)) if iq else f(v) * f(v) for v in x]
+    env = max(x2s[0], f(1e-12))
+    out = np.empty_like(x)
+    for i, (v, x2) in enumerate(zip(x, x2s)):
+        a = att if x2 > env else rel
+        env = f(f(a * env) + f(f(f(1.0) - a) * x2))
+        g = min(max(f(tgt / max(f(np.sqrt(env)), f(1e-6))), f(0.05)), f(20.0))
+        out[i] = (f(g * f(v.real)) + 1j * f(g * f(v.imag))) if iq else f(g * v)
+    return out
+
+
+def test_agc_reference_threshold(oracle):
+    """tests/unit/agc.rs:9-32: AgcRmsIq(48k, 0.2, 5.0, 0.2), steps 0.02 -> 1.0, tail RMS 0.2 +- 0.03."""
+    n = 8000
+    x = np.where(np.arange(n) < n // 2, 0.02, 1.0).astype(np.complex64)
+    y, _ = oracle.agc(x, 48e3, 0.2, 5.0, 0.2)
+    rms = float(np.sqrt(np.mean(np.abs(y[-1000:]) ** 2)))
+    assert abs(rms - 0.2) < 0.03, rms
+
+
+@pytest.mark.parametrize("iq", [False, True])
+def test_agc_oracle_vs_python(oracle, iq):
+    rng = np.random.default_rng(7)
+    n = 3000
+    a = np.where(np.arange(n) < 1500, 0.05, 0.8)
+    x = (a * rng.standard_normal(n)).astype(np.float32)
+    if iq:
+        x = (x + 1j * a * rng.standard_normal(n)).astype(np.complex64)
+    y, _ = oracle.agc(x, 48e3, 1.0, 20.0, 0.3)
+    _eq(y.view(np.float32), _agc_py(x, 48e3, 1.0, 20.0, 0.3).view(np.float32))
+    ys, _ = oracle.agc(x, 48e3, 1.0, 20.0, 0.3, chunk=777)
+    _eq(ys.view(np.float32), y.view(np.float32))
