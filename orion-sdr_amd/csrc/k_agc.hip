@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <stdexcept>
+#include <type_traits>
 
 #include "blocks.hpp"
 #include "hip_common.hpp"
@@ -40,47 +41,69 @@ __device__ __forceinline__ float agc_x2(const float* in, long long i) {
 }
 
 template <bool IQ>
+struct AgcSample {
+  using T = typename std::conditional<IQ, float2, float>::type;
+};
+
+// A lane's samples are walked in batches of kB: the next batch's loads are issued
+// before the current batch's recurrence runs, so the serial chain never waits on HBM.
+constexpr int kB = 16;
+
+template <bool IQ>
 __global__ __launch_bounds__(256) void k_agc(const float* __restrict__ in, float* __restrict__ out,
                                              long long n, long long L, long long W, AgcK k,
                                              const float* __restrict__ env_in, float* __restrict__ env_out) {
+  using T = typename AgcSample<IQ>::T;
+  const T* x = reinterpret_cast<const T*>(in);
+  T* y = reinterpret_cast<T*>(out);
   const long long c = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
   const long long b = c * L;
   if (b >= n) return;
   const long long e = b + L < n ? b + L : n;
+  const long long s0 = c == 0 ? 0 : (b - W > 0 ? b - W : 0);
   float env;
-  long long i;
   if (c == 0) {
     env = env_in[0];
     if (env == 0.0f) env = fmaxf(agc_x2<IQ>(in, 0), 1e-12f);  // agc.rs:57-60
-    i = 0;
   } else {
-    i = b - W > 0 ? b - W : 0;
-    env = fmaxf(agc_x2<IQ>(in, i), 1e-12f);
+    env = fmaxf(agc_x2<IQ>(in, s0), 1e-12f);
   }
-  for (; i < b; ++i) {  // warm-up: envelope only
-    const float x2 = agc_x2<IQ>(in, i);
-    const float a = x2 > env ? k.att : k.rel;
-    env = a * env + (1.0f - a) * x2;
-  }
-  for (; i < e; ++i) {
-    float re, im = 0.0f, x2;
-    if constexpr (IQ) {
-      const float2 v = reinterpret_cast<const float2*>(in)[i];
-      re = v.x; im = v.y;
-      x2 = re * re + im * im;
-    } else {
-      re = in[i];
-      x2 = re * re;
+  const float oma = 1.0f - k.att, omr = 1.0f - k.rel;  // (1 - a) as agc.rs:40 forms it
+  T cur[kB], nxt[kB];
+#pragma unroll
+  for (int j = 0; j < kB; ++j) cur[j] = s0 + j < e ? x[s0 + j] : T{};
+  for (long long base = s0; base < e; base += kB) {
+    const long long nb = base + kB;
+#pragma unroll
+    for (int j = 0; j < kB; ++j) nxt[j] = nb + j < e ? x[nb + j] : T{};
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const long long i = base + j;
+      float re, im = 0.0f, x2;
+      if constexpr (IQ) {
+        re = cur[j].x; im = cur[j].y;
+        x2 = re * re + im * im;
+      } else {
+        re = cur[j];
+        x2 = re * re;
+      }
+      const bool up = x2 > env;
+      const float a = up ? k.att : k.rel;
+      const float om = up ? oma : omr;
+      const float ne = a * env + om * x2;
+      if (i < e) env = ne;
+      if (i >= b && i < e) {
+        const float rms = fmaxf(sqrtf(env), 1e-6f);
+        const float g = fminf(fmaxf(k.tgt / rms, k.gmin), k.gmax);
+        if constexpr (IQ) {
+          y[i] = make_float2(g * re, g * im);
+        } else {
+          y[i] = g * re;
+        }
+      }
     }
-    const float a = x2 > env ? k.att : k.rel;
-    env = a * env + (1.0f - a) * x2;
-    const float rms = fmaxf(sqrtf(env), 1e-6f);
-    const float g = fminf(fmaxf(k.tgt / rms, k.gmin), k.gmax);
-    if constexpr (IQ) {
-      reinterpret_cast<float2*>(out)[i] = make_float2(g * re, g * im);
-    } else {
-      out[i] = g * re;
-    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) cur[j] = nxt[j];
   }
   if (e == n) env_out[0] = env;
 }
@@ -107,8 +130,8 @@ class AgcBlock final : public Block {
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const long long n = static_cast<long long>(std::min(n_in, out_cap));  // agc.rs:49
     if (n == 0) return {0, 0};
-    // Chunk length: at least the warm-up (<= 2x envelope work), at least 1024.
-    const long long L = warm_ < 0 ? n : std::max<long long>(1024, warm_);
+    // Chunk length W/2 (at least 1024): a lane walks 1.5 W samples in series, 3x the envelope work.
+    const long long L = warm_ < 0 ? n : std::max<long long>(1024, warm_ / 2);
     const long long chunks = (n + L - 1) / L;
     float* e = env_.as<float>();
     float* ein = e + cur_;

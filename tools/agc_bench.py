@@ -15,7 +15,7 @@ def run(iq, fs, at, rl, tg, n, reps=10):
     dt = torch.complex64 if iq else torch.float32
     x = torch.randn(n, device="cuda", dtype=dt, generator=g)
     blk = (orion_sdr.AgcRmsIq if iq else orion_sdr.AgcRms)(fs, at, rl, tg)
-    out, _ = blk.process_device(x)
+    out = blk.process_device(x)
     for _ in range(3):
         blk.process_device(x, out)
     torch.cuda.synchronize()
