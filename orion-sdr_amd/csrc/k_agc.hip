@@ -45,34 +45,19 @@ struct AgcSample {
   using T = typename std::conditional<IQ, float2, float>::type;
 };
 
-// A lane's samples are walked in batches of kB: the next batch's loads are issued
-// before the current batch's recurrence runs, so the serial chain never waits on HBM.
 constexpr int kB = 16;
 
-template <bool IQ>
-__global__ __launch_bounds__(256) void k_agc(const float* __restrict__ in, float* __restrict__ out,
-                                             long long n, long long L, long long W, AgcK k,
-                                             const float* __restrict__ env_in, float* __restrict__ env_out) {
+// Walks samples [s, e) of one lane in batches of kB, the next batch's loads issued
+// before the current batch's recurrence. OUT = false: envelope only (the warm-up).
+template <bool IQ, bool OUT>
+__device__ __forceinline__ float agc_walk(const typename AgcSample<IQ>::T* __restrict__ x,
+                                          typename AgcSample<IQ>::T* __restrict__ y, long long s, long long e,
+                                          float env, const AgcK& k, float oma, float omr) {
   using T = typename AgcSample<IQ>::T;
-  const T* x = reinterpret_cast<const T*>(in);
-  T* y = reinterpret_cast<T*>(out);
-  const long long c = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const long long b = c * L;
-  if (b >= n) return;
-  const long long e = b + L < n ? b + L : n;
-  const long long s0 = c == 0 ? 0 : (b - W > 0 ? b - W : 0);
-  float env;
-  if (c == 0) {
-    env = env_in[0];
-    if (env == 0.0f) env = fmaxf(agc_x2<IQ>(in, 0), 1e-12f);  // agc.rs:57-60
-  } else {
-    env = fmaxf(agc_x2<IQ>(in, s0), 1e-12f);
-  }
-  const float oma = 1.0f - k.att, omr = 1.0f - k.rel;  // (1 - a) as agc.rs:40 forms it
   T cur[kB], nxt[kB];
 #pragma unroll
-  for (int j = 0; j < kB; ++j) cur[j] = s0 + j < e ? x[s0 + j] : T{};
-  for (long long base = s0; base < e; base += kB) {
+  for (int j = 0; j < kB; ++j) cur[j] = s + j < e ? x[s + j] : T{};
+  for (long long base = s; base < e; base += kB) {
     const long long nb = base + kB;
 #pragma unroll
     for (int j = 0; j < kB; ++j) nxt[j] = nb + j < e ? x[nb + j] : T{};
@@ -90,21 +75,50 @@ __global__ __launch_bounds__(256) void k_agc(const float* __restrict__ in, float
       const bool up = x2 > env;
       const float a = up ? k.att : k.rel;
       const float om = up ? oma : omr;
-      const float ne = a * env + om * x2;
-      if (i < e) env = ne;
-      if (i >= b && i < e) {
-        const float rms = fmaxf(sqrtf(env), 1e-6f);
-        const float g = fminf(fmaxf(k.tgt / rms, k.gmin), k.gmax);
-        if constexpr (IQ) {
-          y[i] = make_float2(g * re, g * im);
-        } else {
-          y[i] = g * re;
+      const float ne = a * env + om * x2;  // agc.rs:40
+      if (i < e) {
+        env = ne;
+        if constexpr (OUT) {
+          const float rms = fmaxf(sqrtf(env), 1e-6f);
+          const float g = fminf(fmaxf(k.tgt / rms, k.gmin), k.gmax);
+          if constexpr (IQ) {
+            y[i] = make_float2(g * re, g * im);
+          } else {
+            y[i] = g * re;
+          }
         }
       }
     }
 #pragma unroll
     for (int j = 0; j < kB; ++j) cur[j] = nxt[j];
   }
+  return env;
+}
+
+template <bool IQ>
+__global__ __launch_bounds__(256) void k_agc(const float* __restrict__ in, float* __restrict__ out,
+                                             long long n, long long L, long long W, AgcK k,
+                                             const float* __restrict__ env_in, float* __restrict__ env_out) {
+  using T = typename AgcSample<IQ>::T;
+  const T* x = reinterpret_cast<const T*>(in);
+  T* y = reinterpret_cast<T*>(out);
+  const long long c = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const long long b = c * L;
+  if (b >= n) return;
+  const long long e = b + L < n ? b + L : n;
+  // A warm-up that would reach back past the call's first sample starts there, from
+  // the carried envelope, exactly as chunk 0 does.
+  const long long s0 = b - W > 0 ? b - W : 0;
+  float env;
+  if (s0 == 0) {
+    env = env_in[0];
+    if (env == 0.0f) env = fmaxf(agc_x2<IQ>(in, 0), 1e-12f);  // agc.rs:57-60
+  } else {
+    env = fmaxf(agc_x2<IQ>(in, s0), 1e-12f);
+  }
+  const float oma = 1.0f - k.att, omr = 1.0f - k.rel;  // (1 - a) as agc.rs:40 forms it
+  env = agc_walk<IQ, false>(x, y, s0, b, env, k, oma, omr);
+  env = agc_walk<IQ, true>(x, y, b, e, env, k, oma, omr);
   if (e == n) env_out[0] = env;
 }
 
@@ -130,8 +144,8 @@ class AgcBlock final : public Block {
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const long long n = static_cast<long long>(std::min(n_in, out_cap));  // agc.rs:49
     if (n == 0) return {0, 0};
-    // Chunk length W/2 (at least 1024): a lane walks 1.5 W samples in series, 3x the envelope work.
-    const long long L = warm_ < 0 ? n : std::max<long long>(1024, warm_ / 2);
+    // Chunk length 256: >> 1024 waves share the serial W-sample warm-up (envelope only).
+    const long long L = warm_ < 0 ? n : 256;
     const long long chunks = (n + L - 1) / L;
     float* e = env_.as<float>();
     float* ein = e + cur_;
