@@ -151,7 +151,9 @@ int orion_wbfm_chain_seek(orion_block* b, uint64_t index);
 /* Host buffers (synchronous). */
 int orion_block_process(orion_block* b, const void* in, size_t n_in, void* out, size_t out_cap,
                         orion_work_report* wr);
-/* Device buffers (asynchronous on `stream`). */
+/* Device buffers (asynchronous on `stream`). Overlapping in/out ranges are
+ * ORION_E_ARG, except for AgcRms / AgcRmsIq, which work in place (through an
+ * internal copy of the input). */
 int orion_block_process_device(orion_block* b, const void* in_dev, size_t n_in, void* out_dev,
                                size_t out_cap, void* stream, orion_work_report* wr);
 int orion_block_reset(orion_block* b);

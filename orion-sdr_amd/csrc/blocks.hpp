@@ -65,6 +65,9 @@ class Block {
   virtual void check_device_errors() {}
   virtual void reset() = 0;
   virtual int channels() const { return 1; }
+  // process_device may be given overlapping in/out ranges (the block stages its
+  // input itself); the C ABI rejects overlap for every other block.
+  virtual bool alias_ok() const { return false; }
   // Designed coefficients (for tests): which = 0 primary taps, 1 secondary.
   virtual std::vector<float> taps(int which) const { (void)which; return {}; }
 

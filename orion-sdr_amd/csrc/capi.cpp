@@ -225,6 +225,12 @@ int orion_block_process_device(orion_block* b, const void* in, size_t n_in, void
   if (!b) return fail(ORION_E_NULL, "null handle");
   if ((!in && n_in) || (!out && out_cap)) return fail(ORION_E_NULL, "null buffer");
   return guarded([&] {
+    const orion::Block& blk = *b->impl;
+    const size_t nch = static_cast<size_t>(blk.channels());
+    const size_t ib = nch * n_in * orion::dt_size(blk.in_type()), ob = nch * out_cap * orion::dt_size(blk.out_type());
+    const char *ip = static_cast<const char*>(in), *op = static_cast<const char*>(out);
+    if (ib && ob && ip < op + ob && op < ip + ib && !blk.alias_ok())
+      return fail(ORION_E_ARG, "input and output device ranges overlap (not supported by this block)");
     const orion::WorkReport w = b->impl->process_device(in, n_in, out, out_cap, static_cast<hipStream_t>(stream));
     if (wr) { wr->in_read = w.in_read; wr->out_written = w.out_written; }
     return ORION_OK;
