@@ -139,6 +139,7 @@ orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float*
 #define ORION_WBFM_SPLIT 3      /* two kernels (front, back), any IIR design */
 #define ORION_WBFM_SEGMENTED_V1 4
 #define ORION_WBFM_SPECIALIZED 5  /* one kernel, streaming and back waves per CU */
+#define ORION_WBFM_SEGMENTED3 6   /* one kernel, three waves per SIMD, burst back */
 int orion_wbfm_chain_configure(orion_block* b, int path, int max_segments);
 /* Time-sharded streams (no reference counterpart): the absolute
  * index of the next input sample, i.e. the NCO phase origin (rotator.rs:44-62

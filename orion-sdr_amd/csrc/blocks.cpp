@@ -501,13 +501,14 @@ class WbfmBlock final : public Block {
         if (env && std::strcmp(env, "fused") == 0 && fused_ok_) path = kPathRange;
         if (env && std::strcmp(env, "seg") == 0 && seg_ok_) path = kPathSeg;
         if (env && std::strcmp(env, "ws") == 0 && seg_ok_) path = kPathWs;
+        if (env && std::strcmp(env, "seg3") == 0 && seg_ok_) path = kPathSeg3;
       }
-      const bool seg = path == kPathSeg || path == kPathSeg2 || path == kPathWs;
+      const bool seg = path == kPathSeg || path == kPathSeg2 || path == kPathSeg3 || path == kPathWs;
       const bool fused = seg || path == kPathRange;
       if (fused) {
         const long long slots = seg ? wbfm_seg_slots(static_cast<long long>(n_dec), nch_)
                                     : wbfm_fused_slots(static_cast<long long>(n_dec), nch_);
-        const size_t words = (path == kPathSeg2 || path == kPathWs) ? kSg2Slot : kFuSlot;
+        const size_t words = (path == kPathSeg2 || path == kPathSeg3 || path == kPathWs) ? kSg2Slot : kFuSlot;
         if (static_cast<size_t>(slots) * words * 4 > hand_.size()) hand_.resize(static_cast<size_t>(slots) * words * 4);
         if (static_cast<size_t>(slots) * 3 * 4 > flags_.size()) {
           flags_.resize(static_cast<size_t>(slots) * 3 * 4);
@@ -535,7 +536,7 @@ class WbfmBlock final : public Block {
           epoch_ = 0;
         }
         if (path == kPathWs) launch_wbfm_ws(a, cf_, cs_, nch_, max_seg_, s);
-        else if (seg) launch_wbfm_seg(a, cf_, cs_, nch_, max_seg_, path == kPathSeg2, s);
+        else if (seg) launch_wbfm_seg(a, cf_, cs_, nch_, max_seg_, path == kPathSeg3 ? 2 : path == kPathSeg2 ? 1 : 0, s);
         else launch_wbfm_fused(a, cf_, cu_, nch_, s);
         if (trace_path) {  // debug: dump this launch's timestamps (overwrites: last launch wins)
           std::vector<long long> h(static_cast<size_t>(slots) * kFuTracePoints);
@@ -568,8 +569,8 @@ class WbfmBlock final : public Block {
   std::vector<float> taps(int which) const override { return which == 0 ? h_dec_ : h_aud_; }
   void seek(uint64_t index) { k0_ = index; }
   int configure(int path, int max_seg) {
-    if (path < kPathAuto || path > kPathWs || max_seg < 0) return -3;
-    if ((path == kPathSeg2 || path == kPathSeg || path == kPathWs) && !seg_ok_) return -3;
+    if (path < kPathAuto || path > kPathSeg3 || max_seg < 0) return -3;
+    if ((path == kPathSeg2 || path == kPathSeg || path == kPathWs || path == kPathSeg3) && !seg_ok_) return -3;
     if (path == kPathRange && !fused_ok_) return -3;
     path_ = path;
     max_seg_ = max_seg;

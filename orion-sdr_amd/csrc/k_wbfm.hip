@@ -171,6 +171,12 @@ __device__ __forceinline__ void front2_decim(const f2* __restrict__ U, int l, co
   }
 }
 
+#ifndef ORION_SEG2_PF1
+#define ORION_SEG2_PF1 0  // 1: k_wbfm_seg2 keeps one tile of inputs in flight, not two
+#endif
+#ifndef ORION_SEG2_PHGEN
+#define ORION_SEG2_PHGEN 0  // 1: k_wbfm_seg2 forms staging phasors per tile (32 fewer VGPRs)
+#endif
 template <int R, bool A16, int ABL, bool CLAMP = false>
 __global__ __launch_bounds__(64, R <= 2 ? 3 : 2) void k_wbfm_front2(const WbfmArgs a, const WbfmFrontConst C,
                                                     long long L, int wpc) {
@@ -749,12 +755,12 @@ struct PhGen {
 template <bool A16, bool CLAMP, class PH>
 __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, long long jd0, const PH& ph,
                                         f2 (&v)[8][2], const FuPrefetch& pf, f2 Sv, f2& carry, f2& dA,
-                                        float* __restrict__ phit, int svi) {
+                                        float* __restrict__ phit, int svi, bool copy_halo = true) {
   using G = fu::G;
   constexpr int R = 2;
   f2* __restrict__ U = T.U;
   const int l = T.l;
-  if (n > 0) {
+  if (n > 0 && copy_halo) {
 #pragma unroll
     for (int r2 = 0; r2 < 2; ++r2) {
       const int e = l + 64 * r2;
@@ -1840,9 +1846,17 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
 
   // ---- front setup (as fu_front_range) ----
   const FuPrefetch org = fu_origin(a, g);
+#if ORION_SEG2_PF1
+  f2 va[G::KL][2];  // one tile in flight (4 waves x 8 KB per CU already stream at 6.8 TB/s)
+  f2 (&vb)[G::KL][2] = va;
+  front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, l, va);
+  constexpr int PFD = 1;
+#else
   f2 va[G::KL][2], vb[G::KL][2];
   front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, l, va);
   front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, l, vb);
+  constexpr int PFD = 2;
+#endif
   const f2* __restrict__ tabc = a.tab + static_cast<long long>(g.ch) * kWbfmNS;
   const f2* __restrict__ xc = a.x + g.ch * a.x_stride;
   const f2* __restrict__ hc = a.hist_in + g.ch * kWbfmHist;
@@ -1895,7 +1909,7 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
 #pragma unroll 1
   for (int sub = 0, n = 0; sub < nsub; ++sub) {
     f2 ph[G::KL][2];  // per-lane staging phasors, rebuilt per sub-range (dead during the IIR)
-    {                 // from tb (registers) and uniform e^{j theta 128 k} (scalar loads)
+    if (!ORION_SEG2_PHGEN) {  // from tb (registers) and uniform e^{j theta 128 k} (scalar loads)
 #pragma unroll
       for (int k = 0; k < G::KL; ++k) {
         const f2 ek = tabc[128 * k];
@@ -1913,11 +1927,16 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
         Sv = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1 + static_cast<long long>(l) * G::NEW),
                         a.step[g.ch]);
       const long long jd0 = g.A + static_cast<long long>(n) * TW;
-      const FuPrefetch p0 = n + 2 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 2 * G::NEW, true} : dummy;
-      const FuPrefetch p1 = n + 3 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 3 * G::NEW, true} : dummy;
-      fu_tile<A16, CLAMP>(T, n, porg, jd0, PhArr{ph}, va, p0, Sv, carry, dA, Phi + TW * tin, n & 63);
+      const FuPrefetch p0 = n + PFD < ntiles ? FuPrefetch{org.xl, org.nl, porg + PFD * G::NEW, true} : dummy;
+      const FuPrefetch p1 = n + PFD + 1 < ntiles ? FuPrefetch{org.xl, org.nl, porg + (PFD + 1) * G::NEW, true} : dummy;
+#if ORION_SEG2_PHGEN
+      const PhGen phg = PhGen{tb0, tb1, tabc}.opaque();
+#else
+      const PhArr phg{ph};
+#endif
+      fu_tile<A16, CLAMP>(T, n, porg, jd0, phg, va, p0, Sv, carry, dA, Phi + TW * tin, n & 63);
       if (pend && !(ORION_SEG_ABL & 8)) sg2::fir_block(Bc, P, l, tin, acc);
-      fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + TW, PhArr{ph}, vb, p1, Sv, carry, dA, Phi + TW * (tin + 1),
+      fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + TW, phg, vb, p1, Sv, carry, dA, Phi + TW * (tin + 1),
                           (n + 1) & 63);
       if (pend && !(ORION_SEG_ABL & 8)) sg2::fir_block(Bc, P, l, tin + 1, acc);
     }
@@ -1961,6 +1980,216 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
 #pragma unroll 1
     for (int kb = 0; kb < 8; ++kb) sg2::fir_block(Bc, P, l, kb, acc);
     sg2::fir_store(a, g.ch, As, Lrs, l, acc);
+  }
+  fu::trace(a, g.r, 3);
+}
+
+// ---- segmented chain, three waves per SIMD ------------------------------------------
+// k_wbfm_seg3: k_wbfm_seg2's one round of segments and first-sub-range hand-off,
+// sized for THREE waves per SIMD (<= 168 VGPRs, <= 13.6 KB of LDS per wave): the
+// wave count, not the instruction count, bounds this chain (2048 -> 1792 -> 1536
+// segments: 160 -> 175 -> 200 us), so a third wave per SIMD is worth a leaner
+// wave:
+//   * the back of a sub-range (IIR, then the whole audio FIR) runs as one burst
+//     right after its last tile, with two tiles of inputs in flight, and its FIR
+//     pair image P aliases the front image U: the 17-column halo the next tile
+//     needs is carried across the burst in registers (already times e^{-j theta
+//     NEW}, as fu_tile's copy would make it);
+//   * staging phasors are formed per tile (PhGen), not held (32 VGPRs);
+//   * no LDS tap copy: the one-off d[A-1] sum reads the taps from global memory.
+#ifndef ORION_SEG3_ABL
+#define ORION_SEG3_ABL 0  // register/timing experiments: 1 no sub-range bursts, 2 no successor sub-range
+#endif
+namespace sg3 {
+using sg2::CH;
+using sg2::L;
+using sg2::NH;
+constexpr int kHaloLanes = 72;  // f4 pairs of the halo: 8 rows x 9
+
+// The halo of the next tile, e^{-j theta NEW} applied (fu_tile's copy), saved
+// before P overwrites U and written back to the row heads after the burst.
+struct Halo {
+  f4 h[2];
+  __device__ __forceinline__ void save(const f2* U, f2 corr, int l) {
+    using G = fu::G;
+#pragma unroll
+    for (int r2 = 0; r2 < 2; ++r2) {
+      const int e = l + 64 * r2;
+      if (e < kHaloLanes) {
+        const int c = e / 9, hh = e - 9 * c;
+        const f4 w = *reinterpret_cast<const f4*>(U + c * G::LR + G::TW + 2 * hh);
+        const f2 y0 = cmul(f2{w.x, w.y}, corr), y1 = cmul(f2{w.z, w.w}, corr);
+        h[r2] = f4{y0.x, y0.y, y1.x, y1.y};
+      }
+    }
+  }
+  __device__ __forceinline__ void restore(f2* U, int l) const {
+    using G = fu::G;
+#pragma unroll
+    for (int r2 = 0; r2 < 2; ++r2) {
+      const int e = l + 64 * r2;
+      if (e < kHaloLanes) {
+        const int c = e / 9, hh = e - 9 * c;
+        *reinterpret_cast<f4*>(U + c * G::LR + 2 * hh) = h[r2];
+      }
+    }
+  }
+};
+
+// IIR + whole audio FIR of one sub-range, P in U (the caller saved the halo).
+__device__ __forceinline__ void burst(const WbfmArgs& a, const WbfmFusedConst& Bc, int ch, long long A0, int Lr,
+                                      bool chan_last, const float* Phi, f2* P, int l, double (&sw)[4],
+                                      float (&hist)[2]) {
+  if (!(ORION_SEG3_ABL & 4)) sg2::iir(a, Bc, ch, Lr, chan_last, Phi, Phi + NH, P, l, sw, hist);
+  wave_lds_fence();
+  if (ORION_SEG3_ABL & 8) return;
+  // audio FIR (fir.rs:57-66) in blocks of KB = 8 taps (a 15-pair window: this runs
+  // with two prefetched tiles live); lane l owns outputs j = CH l + i and j + NH
+  constexpr int KB = 8;
+  constexpr int O = fu::PB - (KB - 1);  // pair index of window entry 0 at lane 0, block 0
+  f2 acc[CH];
+#pragma unroll
+  for (int i = 0; i < CH; ++i) acc[i] = f2{0.0f, 0.0f};
+#pragma unroll 1
+  for (int kb = 0; kb < 128 / KB; ++kb) {
+    // tap k = KB kb + kk of output i reads pair e = CH l + i - k + PB = CH (l - kb) + O + m,
+    // m = i + KB - 1 - kk; slot = e + e / CH
+    const f2* __restrict__ Pl = P + (CH + 1) * (l - KB * kb / CH) + O;
+    f2 w[CH + KB - 1];
+#pragma unroll
+    for (int m = 0; m < CH + KB - 1; ++m) w[m] = Pl[m + (O + m) / CH];
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk) {
+      const f2 tap = splat2(Bc.a[KB * kb + kk]);
+#pragma unroll
+      for (int i = 0; i < CH; ++i) acc[i] = fma2(tap, w[i + KB - 1 - kk], acc[i]);
+    }
+  }
+  sg2::fir_store(a, ch, A0, Lr, l, acc);
+  wave_lds_fence();
+}
+}  // namespace sg3
+
+static_assert(fu::G::LDS_F2 * 8 + sg2::L * 4 <= 163840 / 12, "three waves per SIMD: LDS per wave");
+static_assert(sg2::Y::PSlots <= fu::G::LDS_F2, "the FIR pair image fits the front image");
+
+template <bool A16, bool CLAMP>
+__global__ __launch_bounds__(64, 3) void k_wbfm_seg3(const WbfmArgs a, const WbfmFrontConst C,
+                                                     const WbfmFusedConst Bc, int spc, int S) {
+  using G = fu::G;
+  constexpr int TW = G::TW;
+  __shared__ __attribute__((aligned(16))) f2 U[G::LDS_F2];
+  __shared__ __attribute__((aligned(16))) float Phi[sg2::L];
+  f2* const P = U;
+  const int l = threadIdx.x & 63;
+  FuRange g;
+  g.r = blockIdx.x;
+  g.ch = g.r / spc;
+  g.wl = g.r - g.ch * spc;
+  g.A = static_cast<long long>(g.wl) * S;
+  g.B = min(g.A + S, a.n_dec);
+  g.Lr = static_cast<int>(g.B - g.A);
+  g.first = g.wl == 0;
+  g.last = g.B == a.n_dec;
+  const int nsub = (g.Lr + sg2::L - 1) / sg2::L;
+  const int ntiles = nsub * sg::NS;
+  fu::trace(a, g.r, 0);
+
+  const FuPrefetch org = fu_origin(a, g);
+  f2 va[G::KL][2];  // ONE tile in flight: 12 waves per CU keep 96 KB of loads in flight
+  front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, l, va);
+  const f2* __restrict__ tabc = a.tab + static_cast<long long>(g.ch) * kWbfmNS;
+  const f2* __restrict__ xc = a.x + g.ch * a.x_stride;
+  const f2* __restrict__ hc = a.hist_in + g.ch * kWbfmHist;
+  const f2 cn = tabc[G::NEW];
+  const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
+  const FuTile T{a, C, U, Phi, C.g, xc, hc, tabc, g.ch, l, c0 * G::LR + (8 * Q + 2 * l + c0) / 8,
+                 c1 * G::LR + (8 * Q + 2 * l + 1 + c1) / 8, f2{cn.x, -cn.y}, g.first};
+  long long porg = org.porg;
+  {  // halo rows of the first tile (clamped here, exact via the boundary fixup)
+    const long long P0 = porg + 2 * l;
+    const long long hi = (org.nl & ~1LL) - 2;
+    const long long Pc = P0 < 0 ? 0 : (P0 > hi ? hi : P0);
+    const f2 x0 = org.xl[Pc], x1 = org.xl[Pc + 1];
+    const f4 th = *reinterpret_cast<const f4*>(tabc + 2 * l);
+    U[c0 * G::LR + (2 * l + c0) / 8] = cmul_rot(x0, f2{th.x, th.y});
+    U[c1 * G::LR + (2 * l + 1 + c1) / 8] = cmul_rot(x1, f2{th.z, th.w});
+  }
+  {  // p = -l (row c = l, i = 0), l = 1..7: used only by d[A-1]
+    const long long Pm = max(porg - (l & 7), 0LL);
+    const f2 xm = xc[Pm];
+    const f2 tc = tabc[l & 7];
+    if (!g.first && l >= 1 && l < 8) U[l * G::LR] = cmul_rot(xm, f2{tc.x, -tc.y});
+  }
+  f2 tb0, tb1;  // e^{j theta (8Q + 2l + r)}
+  {
+    const f4 tv = *reinterpret_cast<const f4*>(tabc + 8 * Q + 2 * l);
+    tb0 = f2{tv.x, tv.y};
+    tb1 = f2{tv.z, tv.w};
+  }
+  f2 Sv = f2{0, 0};
+  f2 carry = f2{0.0f, 0.0f}, dA = f2{0, 0};
+  double sw[4] = {0, 0, 0, 0};  // IIR state entering the next sub-range
+  float hist[2] = {0, 0};       // its FIR history
+  if (g.first) {  // the carried state of the previous call (fm.rs:29 on reset)
+    const float* __restrict__ ci = a.carry_in + g.ch * kWbfmCarry;
+    carry = f2{ci[4], ci[5]};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sw[k] = ci[k];
+    hist[0] = ci[8 + l];
+    hist[1] = ci[8 + 64 + l];
+  }
+  const FuPrefetch dummy{org.xl, org.nl, -8LL * Q, true};  // past the segment: an L2-resident tile
+  bool halo_ok = true;  // U's head halo is in place (false: fu_tile copies it)
+  sg3::Halo halo;
+
+#pragma unroll 1
+  for (int sub = 0, n = 0; sub < nsub; ++sub) {
+#pragma unroll 1
+    for (int tin = 0; tin < sg::NS; tin += 2, n += 2, porg += 2 * G::NEW) {
+      if ((n & 63) == 0)  // lane l: the common phasor of tile n + l
+        Sv = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1 + static_cast<long long>(l) * G::NEW),
+                        a.step[g.ch]);
+      const long long jd0 = g.A + static_cast<long long>(n) * TW;
+      const FuPrefetch p0 = n + 1 < ntiles ? FuPrefetch{org.xl, org.nl, porg + G::NEW, true} : dummy;
+      const FuPrefetch p1 = n + 2 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 2 * G::NEW, true} : dummy;
+      const PhGen phg = PhGen{tb0, tb1, tabc}.opaque();
+      fu_tile<A16, CLAMP>(T, n, porg, jd0, phg, va, p0, Sv, carry, dA, Phi + TW * tin, n & 63, halo_ok);
+      fu_tile<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + TW, phg, va, p1, Sv, carry, dA, Phi + TW * (tin + 1),
+                          (n + 1) & 63);
+      halo_ok = true;
+    }
+    const long long A0 = g.A + static_cast<long long>(sub) * sg2::L;
+    const int Lr = static_cast<int>(min(static_cast<long long>(sg2::L), g.B - A0));
+    if (sub == 0 && !g.first) {
+      // zero-state pass only; the phi go to the predecessor, which has the true state
+      // (scratch: U's row-0 head, which the next tile's halo copy and staging rewrite)
+      sg2::zs_first(Bc, Phi, Phi + sg2::NH, reinterpret_cast<float*>(U), l, sw, hist);
+      uint32_t* slot = a.hand + static_cast<long long>(g.r) * sg2::L;
+#pragma unroll
+      for (int i = 0; i < sg2::L / 64; ++i) fu::st_agent(slot + l + 64 * i, __float_as_uint(Phi[l + 64 * i]));
+      fu::publish(a.flags + 3LL * g.r, a.epoch, l);
+    } else {
+      wave_lds_fence();
+      halo.save(U, T.corr, l);
+      wave_lds_fence();
+      if (!(ORION_SEG3_ABL & 1)) sg3::burst(a, Bc, g.ch, A0, Lr, g.last && sub == nsub - 1, Phi, P, l, sw, hist);
+      halo.restore(U, l);
+      halo_ok = false;
+    }
+  }
+  fu::trace(a, g.r, 1);
+  if (!g.last && !(ORION_SEG3_ABL & 2)) {  // the successor segment's first sub-range
+    const long long As = g.B, Bs = min(As + S, a.n_dec);
+    const int Lrs = static_cast<int>(min(static_cast<long long>(sg2::L), Bs - As));
+    const bool s_last = Bs == a.n_dec && Bs - As <= sg2::L;
+    fu::wait_for(a.flags + 3LL * (g.r + 1), a.epoch, a.err);
+    fu::trace(a, g.r, 2);
+    const uint32_t* slot = a.hand + static_cast<long long>(g.r + 1) * sg2::L;
+#pragma unroll
+    for (int i = 0; i < sg2::L / 64; ++i) Phi[l + 64 * i] = __uint_as_float(fu::ld_agent(slot + l + 64 * i));
+    wave_lds_fence();
+    sg3::burst(a, Bc, g.ch, As, Lrs, s_last, Phi, P, l, sw, hist);
   }
   fu::trace(a, g.r, 3);
 }
@@ -2369,13 +2598,15 @@ long long wbfm_seg_slots(long long n_dec, int nch) {
 // One round: as many segments as resident waves (per channel: the channel's share,
 // at least one sub-range per segment), each a whole number of sub-ranges.
 void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
-                     int max_segments, bool spread, hipStream_t s) {
+                     int max_segments, int variant, hipStream_t s) {
   static_assert(sg::L == kSgL && sg2::L == kSgL, "sub-range geometry");
   if (a.n_dec <= 0 || nch <= 0) return;
-  static int cap = 0;
+  static int caps[3] = {0, 0, 0};
+  int& cap = caps[variant];
   if (cap == 0) {
     int per_cu = 0, dev = 0, ncu = 0;
-    ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_seg2<true, false>, 64, 0));
+    if (variant == 2) ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_seg3<true, false>, 64, 0));
+    else ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_seg2<true, false>, 64, 0));
     ORION_HIP(hipGetDevice(&dev));
     ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     cap = std::max(1, per_cu) * std::max(1, ncu);
@@ -2399,7 +2630,7 @@ void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFused
     if (a16) K<true, false><<<gi, 64, 0, s>>>(a, f, b, sp, Si);        \
     else K<false, false><<<gi, 64, 0, s>>>(a, f, b, sp, Si);           \
   }
-  if (spread) { ORION_SEG(k_wbfm_seg2) } else { ORION_SEG(k_wbfm_seg) }
+  if (variant == 2) { ORION_SEG(k_wbfm_seg3) } else if (variant == 1) { ORION_SEG(k_wbfm_seg2) } else { ORION_SEG(k_wbfm_seg) }
 #undef ORION_SEG
   ORION_LAUNCH_CHECK();
 }

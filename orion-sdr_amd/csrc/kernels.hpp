@@ -143,7 +143,7 @@ long long wbfm_seg_slots(long long n_dec, int nch);
 // spread: k_wbfm_seg2 (FIR spread over the next sub-range's tiles, first sub-range
 // handed to the predecessor); else k_wbfm_seg. max_segments > 0 caps the waves.
 void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
-                     int max_segments, bool spread, hipStream_t s);
+                     int max_segments, int variant, hipStream_t s);
 // Wave-specialised segments (k_wbfm_ws): streaming and back waves in one
 // workgroup per CU; same geometry requirement and hand-off slots as k_wbfm_seg2.
 void launch_wbfm_ws(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,

@@ -413,7 +413,8 @@ class WbfmChain(_Block):
         super().__init__(h)
         self.m = int(m)
 
-    _PATHS = {"auto": 0, "segmented": 1, "ranges": 2, "split": 3, "segmented_v1": 4, "specialized": 5}
+    _PATHS = {"auto": 0, "segmented": 1, "ranges": 2, "split": 3, "segmented_v1": 4, "specialized": 5,
+              "segmented3": 6}
 
     def configure(self, path: str = "auto", max_segments: int = 0):
         """Engine tuning / tests (no reference counterpart): the kernel path and a

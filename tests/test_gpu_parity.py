@@ -300,6 +300,11 @@ def test_wbfm_full_size_windowed(gpu_lib, oracle):
     ("specialized", 2, 8 * 1024 + 8),
     ("specialized", 6, 1 << 16),     # 6 segments in two workgroups, the second part-filled
     ("specialized", 0, 1 << 20),     # the resident capacity: one sub-range per segment
+    ("segmented3", 3, 1 << 20),
+    ("segmented3", 1, 600_000),
+    ("segmented3", 7, 4097 * 8 + 5),
+    ("segmented3", 2, 8 * 1024 + 8),
+    ("segmented3", 0, 1 << 20),     # the resident capacity: one sub-range per segment
     ("ranges", 0, 1 << 20),
     ("split", 0, 1 << 20)])
 def test_wbfm_kernel_paths(gpu_lib, oracle, path, max_seg, n):
@@ -309,7 +314,8 @@ def test_wbfm_kernel_paths(gpu_lib, oracle, path, max_seg, n):
     report(f"wbfm path={path} max_segments={max_seg} n={n} nrmse", nrmse(got, oracle.wbfm(x)), 1e-5)
 
 
-@pytest.mark.parametrize("path,max_seg", [("segmented", 2), ("segmented", 5), ("specialized", 2), ("specialized", 5)])
+@pytest.mark.parametrize("path,max_seg", [("segmented", 2), ("segmented", 5), ("specialized", 2), ("specialized", 5),
+                                          ("segmented3", 2), ("segmented3", 5)])
 def test_wbfm_segmented_streaming_and_channels(gpu_lib, oracle, path, max_seg):
     """Carried state across calls and independent channels with several
     multi-sub-range segments per channel."""
