@@ -327,9 +327,18 @@ class FirIqBlock final : public Block {
   void aligned(void* io, size_t n, hipStream_t s) {
     reset();
     if (n == 0) return;
+    const long long d = (K_ - 1) / 2;
+    const long long ne = fir_iq_aligned_edges(static_cast<long long>(n), K_);
+    if (hist_len_ >= (K_ <= 64 ? 64 : K_ <= 128 ? 128 : 256)) {
+      if (edges_.size() < static_cast<size_t>(ne) * sizeof(f2)) edges_.resize(static_cast<size_t>(ne) * sizeof(f2));
+      if (launch_fir_iq_aligned_inplace(static_cast<f2*>(io), static_cast<long long>(n), d, K_, fast_, edges_.as<f2>(),
+                                        ne, hist_[cur_ ^ 1].as<f2>(), hist_len_, s)) {
+        cur_ ^= 1;
+        return;
+      }
+    }
     scratch_.resize(n * sizeof(f2));
     ORION_HIP(hipMemcpyAsync(scratch_.as<void>(), io, n * sizeof(f2), hipMemcpyDeviceToDevice, s));
-    const long long d = (K_ - 1) / 2;
     launch_fir_iq(scratch_.as<f2>(), static_cast<long long>(n), zeros_.as<f2>(), hist_len_, static_cast<f2*>(io),
                   static_cast<long long>(n), d, K_, fast_, g_dev_.as<float>(), s);
     // The reference leaves the delay line holding the last K samples it pushed
@@ -347,7 +356,7 @@ class FirIqBlock final : public Block {
   std::vector<float> h_;
   int K_ = 0, hist_len_ = 0;
   Taps256 fast_{};
-  DevBuf g_dev_, hist_[2], zeros_, scratch_, tail_;
+  DevBuf g_dev_, hist_[2], zeros_, scratch_, tail_, edges_;
   int cur_ = 0;
 };
 

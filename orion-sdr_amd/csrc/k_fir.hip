@@ -396,11 +396,16 @@ __global__ __launch_bounds__(NT) void k_fir_iq(const f2* __restrict__ x, long lo
 // the FMAs per LDS read of two outputs per lane. The staged tile is padded by 2
 // samples per 8 (lane stride 80 B: the 16-lane b128 groups hit distinct bank
 // slots).
-template <int KP>
-__global__ __launch_bounds__(NT) void k_fir_iq8(const f2* __restrict__ x, long long n,
+// INPLACE (FirLowpassIq::filter_aligned, fir.rs:260-276, on the caller's buffer):
+// x == y. A tile reads only its own outputs' positions [J, J + TT) from x (all
+// of them before any is written: the barrier), and every sample of its halo
+// from E, the copy k_fir_edges made of each tile boundary before this launch;
+// so no tile reads a sample another tile has overwritten.
+template <int KP, bool INPLACE = false>
+__global__ __launch_bounds__(NT) void k_fir_iq8(const f2* x, long long n,
                                                 const f2* __restrict__ hist, int hist_len,
-                                                f2* __restrict__ y, long long n_out, long long off,
-                                                const Taps256 g) {
+                                                f2* y, long long n_out, long long off,
+                                                const Taps256 g, const f2* __restrict__ E = nullptr) {
   constexpr int TT = 8 * NT;
   constexpr int W = TT + KP + 2, PER = (W + NT - 1) / NT;
   constexpr int WP = W + 2 * (W / 8) + 2;
@@ -411,7 +416,27 @@ __global__ __launch_bounds__(NT) void k_fir_iq8(const f2* __restrict__ x, long l
   for (long long J = static_cast<long long>(blockIdx.x) * TT; J < n_out;
        J += static_cast<long long>(gridDim.x) * TT) {
     const long long org = J + off - KP;  // staged sample p <-> element org + p
-    if (org >= 0 && org + W <= n) {
+    if constexpr (INPLACE) {
+      // halo: HL = J - org samples before the tile, HR = W - HL - TT after it;
+      // every load issued before any is used, each from x or the boundary copies
+      const long long HL = J - org, HR = W - HL - TT;
+      const long long T = J / TT;
+      const f2* El = E + T * (HL + HR) - (J - HL);              // El[e], e in [J - HL, J)   (T >= 1)
+      const f2* Er = E + (T + 1) * (HL + HR) + HL - (J + TT);   // Er[e], e in [J + TT, ...)
+      f2 v[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int p = t + k * NT;
+        const long long e = org + p;
+        const f2* src = e < J ? El : (e >= J + TT ? Er : x);
+        v[k] = (p < W && e >= 0 && e < n) ? src[e] : f2{0.0f, 0.0f};
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int p = t + k * NT;
+        if (p < W) L[pidx(p)] = v[k];
+      }
+    } else if (org >= 0 && org + W <= n) {
       f2 v[PER];
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
@@ -473,6 +498,30 @@ __global__ __launch_bounds__(NT) void k_fir_iq_generic(const f2* __restrict__ x,
     f2 acc = f2{0.0f, 0.0f};
     for (int k = 0; k < K; ++k) acc = fma2(splat2(g[k]), load_hist(x, n, hist, hist_len, i + off - k), acc);
     y[i] = acc;
+  }
+}
+
+// Boundary copies for the in-place k_fir_iq8: E[b] = x[b TT - HL .. b TT + HR)
+// (zeros outside [0, n)), b = 1 .. nb - 1.
+__global__ __launch_bounds__(NT) void k_fir_edges(const f2* __restrict__ x, long long n, long long TT, int HL,
+                                                  int HR, long long nb, f2* __restrict__ E) {
+  const int H = HL + HR;
+  for (long long i = static_cast<long long>(blockIdx.x) * NT + threadIdx.x; i < nb * H;
+       i += static_cast<long long>(gridDim.x) * NT) {
+    const long long b = i / H;
+    if (b == 0) continue;
+    const long long e = b * TT - HL + (i - b * H);
+    E[i] = (e >= 0 && e < n) ? x[e] : f2{0.0f, 0.0f};
+  }
+}
+
+// History after filter_aligned (fir.rs:266-275 pushes x[0 .. n) then d zeros into
+// a reset delay line): h[i] = [x | 0^d][n + d - hist_len + i], zeros before x[0].
+__global__ __launch_bounds__(NT) void k_hist_aligned(const f2* __restrict__ x, long long n, long long d,
+                                                     int hist_len, f2* __restrict__ h) {
+  for (int i = threadIdx.x; i < hist_len; i += NT) {
+    const long long P = n + d - hist_len + i;
+    h[i] = (P >= 0 && P < n) ? x[P] : f2{0.0f, 0.0f};
   }
 }
 
@@ -611,6 +660,32 @@ void launch_fir_iq(const f2* x, long long n, const f2* hist, int hist_len, f2* y
   else if (K <= 256 && hist_len >= 256) k_fir_iq<256, kFirHT><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
   else k_fir_iq_generic<<<grid_for(n_out, NT), NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, K, g_dev);
   ORION_LAUNCH_CHECK();
+}
+
+bool launch_fir_iq_aligned_inplace(f2* io, long long n, long long d, int K, const Taps256& g, f2* edges,
+                                   long long edges_cap, f2* hist_out, int hist_len, hipStream_t s) {
+  if (n <= 0) return true;
+  if (K > 256) return false;
+  const int KP = K <= 64 ? 64 : K <= 128 ? 128 : 256;
+  constexpr long long TT = 8 * NT;
+  const long long W = TT + KP + 2;
+  const int HL = static_cast<int>(KP - d), HR = static_cast<int>(W - (KP - d) - TT);
+  const long long nb = (n + TT - 1) / TT;
+  if (nb * (HL + HR) > edges_cap) return false;
+  // the history (read before the samples are overwritten), then the boundary copies
+  k_hist_aligned<<<1, NT, 0, s>>>(io, n, d, hist_len, hist_out);
+  if (nb > 1) k_fir_edges<<<grid_for(nb * (HL + HR), NT), NT, 0, s>>>(io, n, TT, HL, HR, nb, edges);
+  const int g8 = grid_for(n, 8 * NT);
+  if (KP == 64) k_fir_iq8<64, true><<<g8, NT, 0, s>>>(io, n, nullptr, 0, io, n, d, g, edges);
+  else if (KP == 128) k_fir_iq8<128, true><<<g8, NT, 0, s>>>(io, n, nullptr, 0, io, n, d, g, edges);
+  else k_fir_iq8<256, true><<<g8, NT, 0, s>>>(io, n, nullptr, 0, io, n, d, g, edges);
+  ORION_LAUNCH_CHECK();
+  return true;
+}
+long long fir_iq_aligned_edges(long long n, int K) {
+  const int KP = K <= 64 ? 64 : K <= 128 ? 128 : 256;
+  const long long TT = 8 * NT, W = TT + KP + 2;
+  return ((n + TT - 1) / TT) * (W - TT);
 }
 
 void launch_hist_update_c(const f2* x, long long n, const f2* old_h, f2* new_h, int hist_len,

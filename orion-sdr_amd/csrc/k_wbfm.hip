@@ -1961,14 +1961,19 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
     }
   }
   fu::trace(a, g.r, 1);
-  if (pend) {
-#pragma unroll 1
-    for (int kb = 0; kb < 8; ++kb) sg2::fir_block(Bc, P, l, kb, acc);
-    sg2::fir_store(a, g.ch, pA0, pLr, l, acc);
-  }
-  if (!g.last && !(ORION_SEG_ABL & 4)) {  // the successor segment's first sub-range
-    const long long As = g.B, Bs = min(As + S, a.n_dec);
-    const int Lrs = static_cast<int>(min(static_cast<long long>(sg2::L), Bs - As));
+  // End of the segment: the successor's first sub-range needs this segment's end
+  // state (sw, hist: known now). Its IIR runs first, its FIR pair image in the
+  // front image U (dead after the last tile), and then the two audio FIRs (this
+  // segment's last sub-range and the successor's) run interleaved: two
+  // independent accumulator sets, twice the FMA chains per LDS window.
+  const bool succ = !g.last && !(ORION_SEG_ABL & 4);
+  f2* const P2 = U;
+  long long As = 0;
+  int Lrs = 0;
+  if (succ) {  // the successor segment's first sub-range
+    As = g.B;
+    const long long Bs = min(As + S, a.n_dec);
+    Lrs = static_cast<int>(min(static_cast<long long>(sg2::L), Bs - As));
     const bool s_last = Bs == a.n_dec && Bs - As <= sg2::L;
     fu::wait_for(a.flags + 3LL * (g.r + 1), a.epoch, a.err);
     fu::trace(a, g.r, 2);
@@ -1976,10 +1981,19 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
 #pragma unroll
     for (int i = 0; i < sg2::L / 64; ++i) Phi[l + 64 * i] = __uint_as_float(fu::ld_agent(slot + l + 64 * i));
     wave_lds_fence();
-    sg2::iir(a, Bc, g.ch, Lrs, s_last, Phi, Phi + sg2::NH, P, l, sw, hist);
+    sg2::iir(a, Bc, g.ch, Lrs, s_last, Phi, Phi + sg2::NH, P2, l, sw, hist);
+  }
+  if (pend || succ) {
+    f2 acc2[sg2::CH];
+#pragma unroll
+    for (int i = 0; i < sg2::CH; ++i) acc2[i] = f2{0.0f, 0.0f};
 #pragma unroll 1
-    for (int kb = 0; kb < 8; ++kb) sg2::fir_block(Bc, P, l, kb, acc);
-    sg2::fir_store(a, g.ch, As, Lrs, l, acc);
+    for (int kb = 0; kb < 8; ++kb) {
+      if (pend) sg2::fir_block(Bc, P, l, kb, acc);
+      if (succ) sg2::fir_block(Bc, P2, l, kb, acc2);
+    }
+    if (pend) sg2::fir_store(a, g.ch, pA0, pLr, l, acc);
+    if (succ) sg2::fir_store(a, g.ch, As, Lrs, l, acc2);
   }
   fu::trace(a, g.r, 3);
 }

@@ -58,6 +58,12 @@ void launch_fir_iq(const f2* x_dev, long long n, const f2* hist_dev, int hist_le
                    long long n_out, long long off, int K, const Taps256& g, const float* g_dev,
                    hipStream_t s);
 // Copy the last hist_len samples of [old_hist | x[0..n)] into new_hist.
+// FirLowpassIq::filter_aligned in place (k_fir_iq8 INPLACE + boundary copies);
+// writes the history the reference leaves (last hist_len of [x | 0^d]) to
+// hist_out first. false: K > 256 or edges too small (fir_iq_aligned_edges f2).
+bool launch_fir_iq_aligned_inplace(f2* io, long long n, long long d, int K, const Taps256& g, f2* edges,
+                                   long long edges_cap, f2* hist_out, int hist_len, hipStream_t s);
+long long fir_iq_aligned_edges(long long n, int K);
 void launch_hist_update_c(const f2* x_dev, long long n, const f2* old_dev, f2* new_dev,
                           int hist_len, hipStream_t s, int nch = 1, long long x_stride = 0);
 void launch_hist_update_r(const float* x_dev, long long n, const float* old_dev, float* new_dev,

@@ -290,6 +290,17 @@ class FirLowpassIq(_Block):
         _check(_L.orion_fir_lowpass_iq_filter_aligned(self._h, x.ctypes.data, x.size))
         return x
 
+    def filter_aligned_device(self, io, stream=None):
+        """fir.rs:260-276 in place on a contiguous complex64 CUDA tensor (as the
+        reference's `&mut [C32]`), asynchronous on `stream`. Returns io."""
+        import torch
+
+        if not io.is_cuda or not io.is_contiguous() or io.dtype != torch.complex64 or io.dim() != 1:
+            raise ValueError("filter_aligned_device needs a contiguous 1-D complex64 CUDA tensor")
+        s = stream if stream is not None else torch.cuda.current_stream(io.device).cuda_stream
+        _check(_L.orion_fir_lowpass_iq_filter_aligned_device(self._h, io.data_ptr(), io.shape[0], s))
+        return io
+
 
 class LpCascade(_Block):
     """dsp/iir.rs:49 LpCascade::design(fs, fc) as an f32 stream block."""

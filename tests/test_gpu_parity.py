@@ -656,3 +656,34 @@ def test_process_device_overlap_rejected(gpu_lib):
         gpu_lib.FirLowpass(48e3, 3000.0, 1000.0).process_device(x[:2048], x[1024:3072])
     out = torch.empty_like(x)
     gpu_lib.FirLowpass(48e3, 3000.0, 1000.0).process_device(x, out)  # disjoint: fine
+
+
+@pytest.mark.parametrize("ntaps", [1, 45, 89, 127, 255, 301])
+def test_firiq_filter_aligned_in_place(gpu_lib, oracle, ntaps):
+    """fir.rs:260-276 on device memory, in place (the reference's `&mut [C32]`): tiles
+    read only their own samples from the buffer and their halos from boundary copies
+    made before the launch. Lengths around the 2048-output tile, taps 1..255 (301:
+    the copy-based fallback). The delay line left behind (last K of [x | 0^d]) is
+    checked by a following streaming call against the oracle's stream."""
+    import torch
+
+    taps = np.asarray(oracle.kaiser_lowpass_taps(ntaps, 0.2, 60.0), np.float32) if ntaps > 1 else np.ones(1, np.float32)
+    r = np.random.default_rng(ntaps)
+    for n in (1, 7, 2047, 2048, 2049, 6157, (1 << 20) + 5):
+        x = (r.standard_normal(n) + 1j * r.standard_normal(n)).astype(np.complex64)
+        blk = gpu_lib.FirLowpassIq.from_taps(taps)
+        io = torch.from_numpy(x).cuda()
+        blk.filter_aligned_device(io)
+        torch.cuda.synchronize()
+        ref = oracle.fir_lowpass_iq_aligned(x, taps)
+        got = io.cpu().numpy()
+        assert got.shape == ref.shape
+        err = nrmse(got, ref) if n > 1 else float(abs(got[0] - ref[0]) / max(abs(ref[0]), 1e-30))
+        assert err <= 1e-6, (ntaps, n, err)
+        # the streaming state after filter_aligned: x then d zeros pushed into a reset line
+        z = (r.standard_normal(3000) + 1j * r.standard_normal(3000)).astype(np.complex64)
+        d = (len(taps) - 1) // 2
+        after = blk.process(z)
+        full = oracle.fir_lowpass_iq(np.concatenate([x, np.zeros(d, np.complex64), z]), taps)
+        assert nrmse(after, full[n + d:]) <= 1e-6, (ntaps, n)
+    print(f"[parity] firiq filter_aligned in place ntaps={ntaps}: ok")

@@ -13,12 +13,13 @@ sys.path.insert(0, os.path.join(ROOT, "orion-sdr_amd"))
 import bench  # noqa: E402
 
 paths = sys.argv[1].split(",") if len(sys.argv) > 1 else ["segmented", "segmented_v1", "ranges"]
+cfg = sys.argv[2] if len(sys.argv) > 2 else "c2"
 dev = torch.device("cuda", 0)
-blk, x, n, bps, desc = bench.make_workload("c2", 0, dev)
-out = torch.empty(n // 8, dtype=torch.float32, device=dev)
+blk, x, n, bps, desc = bench.make_workload(cfg, 0, dev)
+out = torch.empty(x.shape[:-1] + (x.shape[-1] // 8,), dtype=torch.float32, device=dev)
 s = torch.cuda.current_stream(dev)
 res = {p: [] for p in paths}
-for rnd in range(6):
+for rnd in range(int(os.environ.get("AB_ROUNDS", "6"))):
     for p in paths:
         name, _, ms = p.partition(":")
         blk.configure(name, int(ms or 0))
