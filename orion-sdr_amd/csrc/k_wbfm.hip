@@ -1654,6 +1654,9 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
 //     waits for another's end. The segment itself starts sub-range 1 from the
 //     zero-state end state and zero-state last 128 outputs of sub-range 0
 //     (exact to f32 when ||A^896|| is negligible: the host checks it).
+#ifndef ORION_SCAN_DPP
+#define ORION_SCAN_DPP 0  // 1: DPP / permlane lane shifts in the sub-range scans (measured slower: 162 vs 156 us)
+#endif
 namespace sg2 {
 using Y = sg::Y;  // L 1024, NH 512, CH 8
 constexpr int L = Y::L, NH = Y::NH, CH = Y::CH;
@@ -1689,12 +1692,14 @@ __device__ __forceinline__ void scan_states(const WbfmFusedConst& Bc, const floa
     qb[k] = s[k].y;
   }
   if (l == 0) matvec_acc<4>(Bc.pw, s_in, qa);  // pw[0] = A^CH
-  wave_scan_inclusive<4>(qa, Bc.pw, l);
+  if constexpr (ORION_SCAN_DPP) wave_scan_inclusive_fast<4>(qa, Bc.pw, l);
+  else wave_scan_inclusive<4>(qa, Bc.pw, l);
   double sb[4];  // the state at the end of half A
 #pragma unroll
   for (int k = 0; k < 4; ++k) sb[k] = sg::uni(__shfl(qa[k], 63, 64));
   if (l == 0) matvec_acc<4>(Bc.pw, sb, qb);
-  wave_scan_inclusive<4>(qb, Bc.pw, l);
+  if constexpr (ORION_SCAN_DPP) wave_scan_inclusive_fast<4>(qb, Bc.pw, l);
+  else wave_scan_inclusive<4>(qb, Bc.pw, l);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     end[k] = sg::uni(__shfl(qb[k], 63, 64));
@@ -1703,11 +1708,83 @@ __device__ __forceinline__ void scan_states(const WbfmFusedConst& Bc, const floa
   }
 }
 
+#ifndef ORION_IIR16
+#define ORION_IIR16 0  // 1: one scan over 16-sample lane chunks (measured slower: 165 vs 157 us on C2)
+#endif
+// ONE Kogge-Stone over lane chunks of C16 = 16 consecutive samples of the whole
+// 1024-sample sub-range instead of two chained scans over its halves (lane chunks
+// of 8): 6 dependent f64 steps instead of 12 (each waits on its shuffles and on
+// scalar loads of its step matrix), at the price of unpacked recurrences. Step s
+// uses (A^16)^(2^s) = (A^8)^(2^(s+1)) = pw[s + 1] (s < 5) and A^512 = mh (s = 5).
+constexpr int C16 = L / 64;
+[[maybe_unused]] __device__ __forceinline__ void scan_states16(const WbfmFusedConst& Bc, const float* __restrict__ Ph, int l,
+                                              const double (&s_in)[4], float (&xs)[C16], float (&ef)[4],
+                                              double (&end)[4]) {
+#pragma unroll
+  for (int q = 0; q < C16 / 4; ++q) {
+    const f4 u = *reinterpret_cast<const f4*>(Ph + C16 * l + 4 * q);
+    xs[4 * q] = u.x;
+    xs[4 * q + 1] = u.y;
+    xs[4 * q + 2] = u.z;
+    xs[4 * q + 3] = u.w;
+  }
+  wave_lds_fence();
+  const RecLP4 lp{{Bc.b0, Bc.b1, Bc.b2, Bc.a1, Bc.a2}};
+  float s0[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < C16; ++i) (void)lp.step(s0, xs[i]);
+  double q[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q[k] = s0[k];
+  if (l == 0) matvec_acc<4>(Bc.pw + 16, s_in, q);  // A^16
+#pragma unroll 1
+  for (int st = 0; st < 6; ++st) {
+    const int d = 1 << st;
+    double o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = __shfl_up(q[k], d, 64);
+    const double* m = st < 5 ? Bc.pw + 16 * (st + 1) : Bc.mh;
+    if (l >= d) matvec_acc<4>(m, o, q);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    end[k] = sg::uni(__shfl(q[k], 63, 64));
+    const double e = __shfl_up(q[k], 1, 64);
+    ef[k] = static_cast<float>(l == 0 ? s_in[k] : e);
+  }
+}
+// P[slot(j + PB)] = (f[j], f[j + NH]): f[j] of this lane's chunk goes to the .x
+// (j < NH) or .y component of its pair.
+[[maybe_unused]] __device__ __forceinline__ void put_pair(f2* P, int j, float f) {
+  float* Pf = reinterpret_cast<float*>(P);
+  if (j < NH) Pf[2 * Y::pslot(j + fu::PB)] = f;
+  else Pf[2 * Y::pslot(j - NH + fu::PB) + 1] = f;
+}
+
 // Zero-state pass of a segment's first sub-range: its zero-state end state sw
 // and zero-state last 128 outputs hist (f[L - 128 + l + 64 r]); tmp: 128 floats
 // of free LDS.
+// S16: the 16-sample-chunk scan (needs PhB = PhA + NH).
+template <bool S16 = (ORION_IIR16 != 0)>
 __device__ __forceinline__ void zs_first(const WbfmFusedConst& Bc, const float* PhA, const float* PhB, float* tmp,
                                          int l, double (&sw)[4], float (&hist)[2]) {
+  if constexpr (S16) {
+    constexpr int TL = 64 - fu::PB / C16;  // lanes whose chunk lies in the last 128
+    const double zero[4] = {0, 0, 0, 0};
+    float xs[C16], ef[4];
+    scan_states16(Bc, PhA, l, zero, xs, ef, sw);
+    const RecLP4 lp{{Bc.b0, Bc.b1, Bc.b2, Bc.a1, Bc.a2}};
+#pragma unroll
+    for (int i = 0; i < C16; ++i) {
+      const float f = lp.step(ef, xs[i]);
+      if (l >= TL) tmp[(l - TL) * C16 + i] = f;
+    }
+    wave_lds_fence();
+    hist[0] = tmp[l];
+    hist[1] = tmp[l + 64];
+    wave_lds_fence();
+    return;
+  }
   constexpr int TL = 64 - fu::PB / CH;  // lanes whose half-B chunk lies in the last 128
   const double zero[4] = {0, 0, 0, 0};
   f2 xs[CH], ef[4];
@@ -1729,28 +1806,48 @@ __device__ __forceinline__ void zs_first(const WbfmFusedConst& Bc, const float* 
 // for j in [-128, NH). Returns the state after f[Lr - 1] in sw and
 // f[Lr - 128 + l + 64 r] in hist. chan_last: also the carried IIR state and FIR
 // history of the next call.
+template <bool S16 = (ORION_IIR16 != 0)>
 __device__ __forceinline__ void iir(const WbfmArgs& a, const WbfmFusedConst& Bc, int ch, int Lr, bool chan_last,
                                     const float* PhA, const float* PhB, f2* P, int l, double (&sw)[4],
                                     float (&hist)[2]) {
-  f2 xs[CH], ef[4];
-  double end[4];
-  scan_states(Bc, PhA, PhB, l, sw, xs, ef, end);
-  const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
   const int jl = Lr - 1;
-  const int hl = jl < NH ? jl / CH : (jl - NH) / CH;  // the lane that computes f[jl]
   float cap[4] = {0, 0, 0, 0};
+  int hl;  // the lane that computes f[jl]
+  if constexpr (S16) {
+    float xs[C16], ef[4];
+    double end[4];
+    scan_states16(Bc, PhA, l, sw, xs, ef, end);  // PhA: the whole sub-range (PhB = PhA + NH)
+    const RecLP4 lp{{Bc.b0, Bc.b1, Bc.b2, Bc.a1, Bc.a2}};
+    hl = jl / C16;
 #pragma unroll
-  for (int i = 0; i < CH; ++i) {
-    const int j = CH * l + i;
-    const f2 f = bq.lp4(ef, xs[i]);
-    P[Y::pslot(j + fu::PB)] = f;
-    if (j == jl) {
+    for (int i = 0; i < C16; ++i) {
+      const int j = C16 * l + i;
+      const float f = lp.step(ef, xs[i]);
+      put_pair(P, j, f);
+      if (j == jl) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) cap[k] = ef[k].x;
+        for (int k = 0; k < 4; ++k) cap[k] = ef[k];
+      }
     }
-    if (j + NH == jl) {
+  } else {
+    f2 xs[CH], ef[4];
+    double end[4];
+    scan_states(Bc, PhA, PhB, l, sw, xs, ef, end);
+    const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
+    hl = jl < NH ? jl / CH : (jl - NH) / CH;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) cap[k] = ef[k].y;
+    for (int i = 0; i < CH; ++i) {
+      const int j = CH * l + i;
+      const f2 f = bq.lp4(ef, xs[i]);
+      P[Y::pslot(j + fu::PB)] = f;
+      if (j == jl) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cap[k] = ef[k].x;
+      }
+      if (j + NH == jl) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cap[k] = ef[k].y;
+      }
     }
   }
 #pragma unroll
@@ -1946,6 +2043,7 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
     }
     const long long A0 = g.A + static_cast<long long>(sub) * sg2::L;
     const int Lr = static_cast<int>(min(static_cast<long long>(sg2::L), g.B - A0));
+    if (sub >= 1 && sub <= 3) fu::trace(a, g.r, 3 + sub);  // debug: sub-range tiles done
     if (sub == 0 && !g.first) {
       // zero-state pass only; the phi go to the predecessor, which has the true state
       sg2::zs_first(Bc, Phi, Phi + sg2::NH, reinterpret_cast<float*>(P), l, sw, hist);
@@ -1955,6 +2053,7 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg2(const WbfmArgs a, const Wbf
       fu::publish(a.flags + 3LL * g.r, a.epoch, l);
     } else if (!(ORION_SEG_ABL & 1)) {
       sg2::iir(a, Bc, g.ch, Lr, g.last && sub == nsub - 1, Phi, Phi + sg2::NH, P, l, sw, hist);
+      if (sub <= 3) fu::trace(a, g.r, 6 + sub);  // debug: its IIR done
       pend = true;
       pA0 = A0;
       pLr = Lr;
@@ -2279,7 +2378,7 @@ __device__ __forceinline__ void job(const WbfmArgs& a, const WbfmFusedConst& Bc,
   const long long A0 = g.A + static_cast<long long>(sub) * sg2::L;
   const int Lr = static_cast<int>(min(static_cast<long long>(sg2::L), g.B - A0));
   if (sub == 0 && !g.first) {
-    sg2::zs_first(Bc, PhA, PhB, reinterpret_cast<float*>(P), l, sw, hist);
+    sg2::zs_first<false>(Bc, PhA, PhB, reinterpret_cast<float*>(P), l, sw, hist);
     uint32_t* slot = a.hand + static_cast<long long>(g.r) * sg2::L;
 #pragma unroll
     for (int i = 0; i < sg2::L / 64; ++i)
@@ -2288,7 +2387,7 @@ __device__ __forceinline__ void job(const WbfmArgs& a, const WbfmFusedConst& Bc,
     if (rel && l == 0) lds_st(rel, sub + 1);
     fu::publish(a.flags + 3LL * g.r, a.epoch, l);
   } else {
-    sg2::iir(a, Bc, g.ch, Lr, chan_last, PhA, PhB, P, l, sw, hist);
+    sg2::iir<false>(a, Bc, g.ch, Lr, chan_last, PhA, PhB, P, l, sw, hist);
     if (rel && l == 0) lds_st(rel, sub + 1);  // iir read the phi first (scan_states)
     f2 acc[sg2::CH];
 #pragma unroll
@@ -2450,14 +2549,14 @@ __global__ __launch_bounds__(ws::kThreads, 1) void k_wbfm_ws(const WbfmArgs a, c
       const long long A0 = gt.A + static_cast<long long>(s) * sg2::L;
       const int Lr = static_cast<int>(min(static_cast<long long>(sg2::L), gt.B - A0));
       if (s == 0 && !gt.first) {
-        sg2::zs_first(Bc, PhA, PhB, reinterpret_cast<float*>(P), l, sw, hist);
+        sg2::zs_first<false>(Bc, PhA, PhB, reinterpret_cast<float*>(P), l, sw, hist);
         uint32_t* slot = a.hand + static_cast<long long>(gt.r) * sg2::L;
 #pragma unroll
         for (int i = 0; i < sg2::L / 64; ++i)
           fu::st_agent(slot + l + 64 * i, __float_as_uint((i < 8 ? PhA : PhB - sg2::NH)[l + 64 * i]));
         fu::publish(a.flags + 3LL * gt.r, a.epoch, l);
       } else {
-        sg2::iir(a, Bc, gt.ch, Lr, gt.last, PhA, PhB, P, l, sw, hist);
+        sg2::iir<false>(a, Bc, gt.ch, Lr, gt.last, PhA, PhB, P, l, sw, hist);
         f2 acc[sg2::CH];
 #pragma unroll
         for (int i = 0; i < sg2::CH; ++i) acc[i] = f2{0.0f, 0.0f};
