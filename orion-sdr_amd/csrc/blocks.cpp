@@ -505,7 +505,8 @@ class WbfmBlock final : public Block {
       int path = path_;
       if (path == kPathAuto) {
         static const char* env = std::getenv("ORION_WBFM_PATH");  // timing experiments
-        path = seg_ok_ ? kPathSeg2 : kPathSplit;
+        path = seg_ok_ ? kPathSeg : kPathSplit;
+        if (env && std::strcmp(env, "seg2") == 0 && seg_ok_) path = kPathSeg2;
         if (env && std::strcmp(env, "split") == 0) path = kPathSplit;
         if (env && std::strcmp(env, "fused") == 0 && fused_ok_) path = kPathRange;
         if (env && std::strcmp(env, "seg") == 0 && seg_ok_) path = kPathSeg;

@@ -1261,6 +1261,9 @@ __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(con
 #define ORION_SEG_ABL 0  // timing experiments only (separate builds): 1 no sub-range backs, 2 no
                          // zero-state pass, 4 no deferred back, 8 no spread FIR blocks (seg2)
 #endif
+#ifndef ORION_SEG_EARLY_PUB
+#define ORION_SEG_EARLY_PUB 1  // k_wbfm_seg publishes a segment's end state before its last audio FIR
+#endif
 #ifndef ORION_SEG_PRIO_Q16
 #define ORION_SEG_PRIO_Q16 9
 #endif
@@ -1368,9 +1371,13 @@ __device__ __forceinline__ void zs_only(const WbfmFusedConst& Bc, const double* 
 // f[A0 + L - 1]) in sw and this sub-range's last 128 IIR outputs in hist. P may
 // alias Phi (Phi is read into registers first). chan_last: the channel's last
 // sub-range (writes the IIR state and FIR history carried to the next call).
+// publish_r >= 0: publish the end state and last 128 IIR outputs to the successor
+// (publish_end) as soon as they are known, before the audio FIR.
+__device__ __forceinline__ void publish_end(const WbfmArgs& a, int r, const double (&sw)[4], const float (&hist)[2],
+                                            int l);
 __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc, int ch, long long A0, int Lr,
                                      bool chan_last, const float* Phi, f2* P, int l, double (&sw)[4],
-                                     float (&hist)[2]) {
+                                     float (&hist)[2], int publish_r = -1) {
   constexpr int NH = Y::NH;
   const double* __restrict__ lm = a.lanemats_sg;
   f2 xs[CH];
@@ -1424,6 +1431,9 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
     P[Y::pslot(t)] = f2{hist[r2], P[Y::pslot(t + NH)].x};
   }
   wave_lds_fence();
+#pragma unroll
+  for (int r2 = 0; r2 < 2; ++r2) hist[r2] = P[Y::pslot(NH + l + 64 * r2)].y;  // f[L - 128 + t]: the next history
+  if (publish_r >= 0) publish_end(a, publish_r, sw, hist, l);
   {  // audio FIR (fir.rs:57-66), as in fu_back_range with taps in blocks of
      // KB = CH (a smaller window: this runs with two prefetched tiles live)
     constexpr int KB = CH;
@@ -1473,8 +1483,6 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
       a.carry_out[ch * kWbfmCarry + 8 + t] = f;
     }
   }
-#pragma unroll
-  for (int r2 = 0; r2 < 2; ++r2) hist[r2] = P[Y::pslot(NH + l + 64 * r2)].y;  // f[L - 128 + t]
   wave_lds_fence();
 }
 
@@ -1605,8 +1613,12 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
         const long long A0 = g.A + static_cast<long long>(sub) * sg::L;
         const int Lr = static_cast<int>(min(static_cast<long long>(sg::L), g.B - A0));
         const bool lastsub = sub == nsub - 1;
-        if (!(ORION_SEG_ABL & 1)) sg::back(a, Bc, g.ch, A0, Lr, g.last && lastsub, Phi, P, l, sw, hist);
-        if (lastsub && !g.last) sg::publish_end(a, g.r, sw, hist, l);
+        if (sub <= 3) fu::trace(a, g.r, 3 + sub);  // debug: sub-range tiles done
+        if (!(ORION_SEG_ABL & 1))
+          sg::back(a, Bc, g.ch, A0, Lr, g.last && lastsub, Phi, P, l, sw, hist,
+                   ORION_SEG_EARLY_PUB && lastsub && !g.last ? g.r : -1);
+        if ((!ORION_SEG_EARLY_PUB || (ORION_SEG_ABL & 1)) && lastsub && !g.last) sg::publish_end(a, g.r, sw, hist, l);
+        if (sub <= 3) fu::trace(a, g.r, 6 + sub);  // debug: its back done
       }
     }
   }

@@ -1,8 +1,9 @@
-"""Debug: phase timestamps of k_wbfm_seg2 (ORION_WBFM_TRACE) on the C2 workload.
+"""Debug: phase timestamps of k_wbfm_seg2 / k_wbfm_seg (ORION_WBFM_TRACE) on the C2 workload.
 Points per wave (s_memrealtime, 100 MHz): 0 start, 1 sub-range loop done,
 2 successor's phi received, 3 end; 3 + s: sub-range s's tiles done, 6 + s: its
 IIR done (s = 1..3).
-  python tools/seg2_trace.py [out.bin]"""
+IIR done = the whole back (IIR + audio FIR) in k_wbfm_seg.
+  python tools/seg2_trace.py [out.bin] [segmented|segmented_v1]"""
 import os
 import sys
 
@@ -19,7 +20,7 @@ dev = torch.device("cuda", 0)
 n = 1 << 26
 x = torch.randn(n, dtype=torch.complex64, device=dev)
 out = torch.empty(n // 8, dtype=torch.float32, device=dev)
-blk = orion_sdr.WbfmChain().configure("segmented", 0)
+blk = orion_sdr.WbfmChain().configure(sys.argv[2] if len(sys.argv) > 2 else "segmented", 0)
 for _ in range(5):  # the last launch's trace is kept
     blk.process_device(x, out, torch.cuda.current_stream(dev).cuda_stream)
 torch.cuda.synchronize()
@@ -45,7 +46,7 @@ for k, v in ph.items():
     print(f"{k:22s} {v.mean():7.2f} {np.percentile(v, 10):7.2f} {np.percentile(v, 50):7.2f} "
           f"{np.percentile(v, 90):7.2f} {v.max():7.2f}")
 r = np.nonzero((np.fromfile(path, dtype=np.int64).reshape(-1, 10)[:, [0, 1, 3, 4, 5, 6, 7, 8, 9]] > 0).all(axis=1))[0]
-half = len(np.fromfile(path, dtype=np.int64)) // 20
+half = (r.max() + 1) // 2
 for nm, m in (("early (r < grid/2)", r < half), ("late", r >= half)):
     e = us[m, 3]
     print(f"{nm:20s} end p10 {np.percentile(e, 10):.1f} p50 {np.median(e):.1f} max {e.max():.1f}")
