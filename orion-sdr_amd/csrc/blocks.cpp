@@ -505,20 +505,22 @@ class WbfmBlock final : public Block {
       int path = path_;
       if (path == kPathAuto) {
         static const char* env = std::getenv("ORION_WBFM_PATH");  // timing experiments
-        path = seg_ok_ ? kPathSeg : kPathSplit;
+        path = seg_ok_ ? kPathSeg4 : kPathSplit;
         if (env && std::strcmp(env, "seg2") == 0 && seg_ok_) path = kPathSeg2;
         if (env && std::strcmp(env, "split") == 0) path = kPathSplit;
         if (env && std::strcmp(env, "fused") == 0 && fused_ok_) path = kPathRange;
         if (env && std::strcmp(env, "seg") == 0 && seg_ok_) path = kPathSeg;
         if (env && std::strcmp(env, "ws") == 0 && seg_ok_) path = kPathWs;
         if (env && std::strcmp(env, "seg3") == 0 && seg_ok_) path = kPathSeg3;
+        if (env && std::strcmp(env, "seg4") == 0 && seg_ok_) path = kPathSeg4;
       }
-      const bool seg = path == kPathSeg || path == kPathSeg2 || path == kPathSeg3 || path == kPathWs;
+      const bool seg = path == kPathSeg || path == kPathSeg2 || path == kPathSeg3 || path == kPathSeg4 || path == kPathWs;
       const bool fused = seg || path == kPathRange;
       if (fused) {
         const long long slots = seg ? wbfm_seg_slots(static_cast<long long>(n_dec), nch_)
                                     : wbfm_fused_slots(static_cast<long long>(n_dec), nch_);
-        const size_t words = (path == kPathSeg2 || path == kPathSeg3 || path == kPathWs) ? kSg2Slot : kFuSlot;
+        const size_t words = path == kPathSeg4 ? kSeg4Slot
+                            : (path == kPathSeg2 || path == kPathSeg3 || path == kPathWs) ? kSg2Slot : kFuSlot;
         if (static_cast<size_t>(slots) * words * 4 > hand_.size()) hand_.resize(static_cast<size_t>(slots) * words * 4);
         if (static_cast<size_t>(slots) * 3 * 4 > flags_.size()) {
           flags_.resize(static_cast<size_t>(slots) * 3 * 4);
@@ -546,7 +548,9 @@ class WbfmBlock final : public Block {
           epoch_ = 0;
         }
         if (path == kPathWs) launch_wbfm_ws(a, cf_, cs_, nch_, max_seg_, s);
-        else if (seg) launch_wbfm_seg(a, cf_, cs_, nch_, max_seg_, path == kPathSeg3 ? 2 : path == kPathSeg2 ? 1 : 0, s);
+        else if (seg)
+          launch_wbfm_seg(a, cf_, cs_, nch_, max_seg_,
+                          path == kPathSeg4 ? 3 : path == kPathSeg3 ? 2 : path == kPathSeg2 ? 1 : 0, s);
         else launch_wbfm_fused(a, cf_, cu_, nch_, s);
         if (trace_path) {  // debug: dump this launch's timestamps (overwrites: last launch wins)
           std::vector<long long> h(static_cast<size_t>(slots) * kFuTracePoints);
@@ -579,8 +583,9 @@ class WbfmBlock final : public Block {
   std::vector<float> taps(int which) const override { return which == 0 ? h_dec_ : h_aud_; }
   void seek(uint64_t index) { k0_ = index; }
   int configure(int path, int max_seg) {
-    if (path < kPathAuto || path > kPathSeg3 || max_seg < 0) return -3;
-    if ((path == kPathSeg2 || path == kPathSeg || path == kPathWs || path == kPathSeg3) && !seg_ok_) return -3;
+    if (path < kPathAuto || path > kPathSeg4 || max_seg < 0) return -3;
+    if ((path == kPathSeg2 || path == kPathSeg || path == kPathWs || path == kPathSeg3 || path == kPathSeg4) && !seg_ok_)
+      return -3;
     if (path == kPathRange && !fused_ok_) return -3;
     path_ = path;
     max_seg_ = max_seg;

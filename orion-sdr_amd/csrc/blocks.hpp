@@ -113,7 +113,7 @@ std::unique_ptr<Block> make_wbfm_chain(const WbfmParams& p, const std::vector<fl
 // orion_wbfm_chain_configure). max_segments > 0 caps the segmented kernels'
 // waves (default: the resident capacity). Returns -4 if b is not a WBFM chain,
 // -3 if this design cannot run on that path.
-enum : int { kPathAuto = 0, kPathSeg2 = 1, kPathRange = 2, kPathSplit = 3, kPathSeg = 4, kPathWs = 5, kPathSeg3 = 6 };
+enum : int { kPathAuto = 0, kPathSeg2 = 1, kPathRange = 2, kPathSplit = 3, kPathSeg = 4, kPathWs = 5, kPathSeg3 = 6, kPathSeg4 = 7 };
 int wbfm_chain_configure(Block* b, int path, int max_segments);
 // Absolute index of the next input sample (the NCO phase origin) of a WBFM
 // chain: a time-sharded stream starts each shard's handle at its halo start

@@ -855,6 +855,173 @@ __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, 
   }
 }
 
+// ---- front tile, four-group decimator (k_wbfm_seg4) ------------------------------
+// fu_tile's polyphase FIR with EIGHT outputs per lane instead of two. The 64 lanes
+// are the four ds_read_b128 lane groups of gfx950 (A = {0-3, 12-15, 20-27},
+// B = {4-11, 16-19, 28-31}, C, D = A, B + 32); group g sums phases 2g and 2g+1 for
+// outputs 8l'..8l'+7 (l' = l & 15), and two permlane swaps (rows 0<->1, 2<->3, then
+// the halves) add the four partial sums, leaving every lane two outputs. Per lane
+// and tile: 24 window + 8 tap ds_read_b128 (fu_tile: 72 window reads), eight
+// independent FMA chains per phase (fu_tile: two). Image rows carry one 16-B pad
+// after every four chunks, so lane windows start 5 chunks apart and the 16 lanes
+// of a read group hit 16 distinct bank quads; the pitch (91 chunks, odd) spreads
+// the phase-scattered b64 staging stores.
+namespace g8 {
+constexpr int PCH = 91;          // row pitch, 16-B chunks
+constexpr int LRS = 2 * PCH;     // row pitch, f2 slots
+constexpr int LDS_F2 = M * LRS;  // 11648 B
+__host__ __device__ constexpr int pchunk(int c) { return 5 * (c >> 2) + (c & 3); }
+__host__ __device__ constexpr int slot(int i) { return 2 * pchunk(i >> 1) + (i & 1); }
+static_assert(slot(fu::G::TW + Q) < LRS && pchunk(fu::G::TW / 2) == 80, "row geometry");
+__device__ __forceinline__ int group(int l) {
+  const int i = l & 31;
+  const bool a = i < 4 || (i >= 12 && i < 16) || (i >= 20 && i < 28);
+  return (l >> 5) * 2 + (a ? 0 : 1);
+}
+// the lane holding the output before this lane's first one (lane 0: the carry)
+__device__ __forceinline__ int prev_lane(int l) {
+  const int row = l >> 4, lp = l & 15;
+  return row == 0 ? 47 + lp : row == 2 ? lp : row == 1 ? 32 + lp : 16 + lp;
+}
+// this lane's first output (tile-relative): rows 0, 2, 1, 3 own 8l' + {0,1}, {2,3}, {4,5}, {6,7}
+__device__ __forceinline__ int first_out(int l) {
+  const int row = l >> 4;
+  return 8 * (l & 15) + 2 * (row == 0 ? 0 : row == 2 ? 1 : row == 1 ? 2 : 3);
+}
+}  // namespace g8
+
+template <bool A16, bool CLAMP>
+__device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg, long long jd0,
+                                         const f2 (&ph)[8][2], f2 (&v)[8][2], const FuPrefetch& pf, f2 Sv,
+                                         f2& carry, float* __restrict__ phit, int svi) {
+  using G = fu::G;
+  f2* __restrict__ U = T.U;
+  const int l = T.l;
+  if (n > 0) {  // halo: entries TW .. TW+Q of every row -> 0 .. Q, times e^{-j theta NEW}
+#pragma unroll
+    for (int r2 = 0; r2 < 2; ++r2) {
+      const int e = l + 64 * r2;
+      if (e < 72) {
+        const int c = e / 9, h = e - 9 * c;
+        const int dst = c * g8::LRS + 2 * g8::pchunk(h);
+        const f4 w = *reinterpret_cast<const f4*>(U + dst + 2 * 80);  // pchunk(TW/2 + h) = 80 + pchunk(h)
+        const f2 y0 = cmul(f2{w.x, w.y}, T.corr), y1 = cmul(f2{w.z, w.w}, T.corr);
+        *reinterpret_cast<f4*>(U + dst) = f4{y0.x, y0.y, y1.x, y1.y};
+      }
+    }
+    wave_lds_fence();
+  }
+  const bool bnd = porg < 0 || porg + 8LL * (G::TW + Q) > T.a.n;
+#pragma unroll
+  for (int k = 0; k < G::KL; ++k) {  // entry i + 16k = slot(i) + 20k
+    U[T.s0 + 20 * k] = cmul_rot_pk(v[k][0], ph[k][0]);
+    U[T.s1 + 20 * k] = cmul_rot_pk(v[k][1], ph[k][1]);
+    if (k % 4 == 3) asm volatile("" ::: "memory");
+  }
+  asm volatile("" ::: "memory");
+  front2_load<2, A16, CLAMP>(pf.xl, pf.nl, pf.porg, l, v);  // unconditional (see fu_tile)
+  if (bnd) {
+    wave_lds_fence();
+#pragma unroll 1
+    for (int p = (n == 0 ? 0 : 8 * Q) + l; p < 8 * (G::TW + Q); p += 64) {
+      const long long Pp = porg + p;
+      if (!CLAMP || Pp < 0 || Pp >= T.a.n || p < 8 * Q) {
+        const int c = (-p) & 7;
+        U[c * g8::LRS + g8::slot((p + c) / 8)] = cmul_rot(load_hist(T.xc, T.a.n, T.hc, kWbfmHist, Pp), T.tabc[p]);
+      }
+    }
+  }
+  wave_lds_fence();
+  // group g: phases 2g, 2g+1; window entries 8l' .. 8l'+23 of the phase's row
+  const int g = g8::group(l), lp = l & 15;
+  f2 d[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) d[r] = f2{0.0f, 0.0f};
+#pragma unroll 1
+  for (int s = 0; s < 2; ++s) {
+    const int c = 2 * g + s;
+    const f4* __restrict__ row = reinterpret_cast<const f4*>(U + c * g8::LRS) + 5 * lp;
+    f4 w[12];
+#pragma unroll
+    for (int h = 0; h < 12; ++h) w[h] = row[5 * (h >> 2) + (h & 3)];
+    const f4* __restrict__ tq = reinterpret_cast<const f4*>(T.Gt + c * Q);
+    float t[Q];
+#pragma unroll
+    for (int q4 = 0; q4 < Q / 4; ++q4) {
+      const f4 u = tq[q4];
+      t[4 * q4] = u.x;
+      t[4 * q4 + 1] = u.y;
+      t[4 * q4 + 2] = u.z;
+      t[4 * q4 + 3] = u.w;
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int m = r + Q - q;  // window entry 1 .. 23 (tap q of output 8l' + r)
+        const f4& wc = w[m >> 1];
+        d[r] = fma2(splat2(t[q]), (m & 1) ? f2{wc.z, wc.w} : f2{wc.x, wc.y}, d[r]);
+      }
+  }
+  // rows 0<->1, 2<->3: even rows keep outputs 0..3, odd rows 4..7 (x: d[i], y: d[i+4])
+  f2 K[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const auto sx = __builtin_amdgcn_permlane16_swap(__float_as_uint(d[i].x), __float_as_uint(d[i + 4].x), false, false);
+    const auto sy = __builtin_amdgcn_permlane16_swap(__float_as_uint(d[i].y), __float_as_uint(d[i + 4].y), false, false);
+    K[i] = f2{__uint_as_float(sx[0]), __uint_as_float(sy[0])} + f2{__uint_as_float(sx[1]), __uint_as_float(sy[1])};
+  }
+  // halves: rows 0, 1 keep K[0..1], rows 2, 3 K[2..3]
+  f2 F[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const auto sx = __builtin_amdgcn_permlane32_swap(__float_as_uint(K[i].x), __float_as_uint(K[i + 2].x), false, false);
+    const auto sy = __builtin_amdgcn_permlane32_swap(__float_as_uint(K[i].y), __float_as_uint(K[i + 2].y), false, false);
+    F[i] = f2{__uint_as_float(sx[0]), __uint_as_float(sy[0])} + f2{__uint_as_float(sx[1]), __uint_as_float(sy[1])};
+  }
+  const f2 S = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.x), svi)),
+                  __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.y), svi))};
+  F[0] = cmul(F[0], S);
+  F[1] = cmul(F[1], S);
+  if (n == 0 && !T.first) {  // d[A-1] from this tile's image (as fu_tile)
+    f2 acc = f2{0.0f, 0.0f};
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      const int k = 2 * l + t2, c = k & 7, q = k >> 3;
+      acc = fma2(splat2(T.Gt[c * Q + q]), U[c * g8::LRS + g8::slot(15 - q)], acc);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+      acc += f2{__shfl_xor(acc.x, off, 64), __shfl_xor(acc.y, off, 64)};
+    carry = cmul(acc, S);
+  }
+  const int src = g8::prev_lane(l);
+  f2 pv = f2{__shfl(F[1].x, src, 64), __shfl(F[1].y, src, 64)};
+  if (l == 0) pv = carry;
+  const int j0 = g8::first_out(l);
+  *reinterpret_cast<f2*>(phit + j0) = f2{fm_disc_pk_rcp(F[0], pv, T.C.k), fm_disc_pk_rcp(F[1], F[0], T.C.k)};
+  carry = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(F[1].x), 63)),
+             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(F[1].y), 63))};
+  const WbfmArgs& a = T.a;
+  if (jd0 <= a.n_dec - 1 && a.n_dec - 1 < jd0 + G::TW) {  // carried state of the next call
+    const int rl = static_cast<int>(a.n_dec - 1 - jd0);
+    float* co = a.carry_out + T.ch * kWbfmCarry;
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+      if (j0 + r == rl) {
+        co[4] = F[r].x;
+        co[5] = F[r].y;
+        co[6] = 0.0f;
+        co[7] = 0.0f;
+      }
+#pragma unroll
+    for (int t2 = 0; t2 < kWbfmHist / 64; ++t2) {
+      const int t = l + 64 * t2;
+      a.hist_out[T.ch * kWbfmHist + t] = load_hist(T.xc, a.n, T.hc, kWbfmHist, a.n - kWbfmHist + t);
+    }
+  }
+}
+
 // Range geometry shared by the front and the back of one range.
 struct FuRange {
   int r, ch, wl;
@@ -1374,10 +1541,10 @@ __device__ __forceinline__ void zs_only(const WbfmFusedConst& Bc, const double* 
 // publish_r >= 0: publish the end state and last 128 IIR outputs to the successor
 // (publish_end) as soon as they are known, before the audio FIR.
 __device__ __forceinline__ void publish_end(const WbfmArgs& a, int r, const double (&sw)[4], const float (&hist)[2],
-                                            int l);
+                                            int l, int stride = kFuSlot);
 __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc, int ch, long long A0, int Lr,
                                      bool chan_last, const float* Phi, f2* P, int l, double (&sw)[4],
-                                     float (&hist)[2], int publish_r = -1) {
+                                     float (&hist)[2], int publish_r = -1, int stride = kFuSlot) {
   constexpr int NH = Y::NH;
   const double* __restrict__ lm = a.lanemats_sg;
   f2 xs[CH];
@@ -1433,7 +1600,7 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
   wave_lds_fence();
 #pragma unroll
   for (int r2 = 0; r2 < 2; ++r2) hist[r2] = P[Y::pslot(NH + l + 64 * r2)].y;  // f[L - 128 + t]: the next history
-  if (publish_r >= 0) publish_end(a, publish_r, sw, hist, l);
+  if (publish_r >= 0) publish_end(a, publish_r, sw, hist, l, stride);
   {  // audio FIR (fir.rs:57-66), as in fu_back_range with taps in blocks of
      // KB = CH (a smaller window: this runs with two prefetched tiles live)
     constexpr int KB = CH;
@@ -1488,8 +1655,8 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
 
 // Publish a segment's end state and last 128 IIR outputs to its successor.
 __device__ __forceinline__ void publish_end(const WbfmArgs& a, int r, const double (&sw)[4], const float (&hist)[2],
-                                            int l) {
-  uint32_t* slot = a.hand + static_cast<long long>(r) * kFuSlot;
+                                            int l, int stride) {
+  uint32_t* slot = a.hand + static_cast<long long>(r) * stride;
   if (l < 8) {
     const int kk = l >> 1;
     const double v8 = kk == 0 ? sw[0] : kk == 1 ? sw[1] : kk == 2 ? sw[2] : sw[3];
@@ -1644,6 +1811,158 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
   }
   fu::trace(a, g.r, 2);
   sg::back(a, Bc, g.ch, g.A, min(sg::L, g.Lr), g.last && nsub == 1, Phi0, P, l, sw, hist);
+  fu::trace(a, g.r, 3);
+}
+
+// ---- segmented chain, four-group decimator ----------------------------------------
+// k_wbfm_seg4: k_wbfm_seg with fu_tile8's front tile. The padded image needs 2.3 KB
+// more LDS, so sub-range 0's phi (kept for the deferred back) go to the segment's
+// global slot (after its end-state record) instead of a third LDS buffer, and come
+// back at the end (L2/MALL-resident by then).
+constexpr int kSegSlot = kSeg4Slot;  // u32 words: end-state record, then sub-range 0's phi
+template <bool A16, bool CLAMP>
+__global__ __launch_bounds__(64, 2) void k_wbfm_seg4(const WbfmArgs a, const WbfmFrontConst C,
+                                                     const WbfmFusedConst Bc, int spc, int S) {
+  using G = fu::G;
+  constexpr int TW = G::TW;
+  __shared__ __attribute__((aligned(16))) f2 U[g8::LDS_F2];
+  __shared__ __attribute__((aligned(16))) unsigned char wreg[sg::WBytes];
+  __shared__ __attribute__((aligned(16))) float Gt[128];
+  float* Phi = reinterpret_cast<float*>(wreg);
+  f2* P = reinterpret_cast<f2*>(wreg);
+  const int l = threadIdx.x & 63;
+  Gt[l] = C.g[l];
+  Gt[l + 64] = C.g[l + 64];
+  FuRange g;
+  g.r = blockIdx.x;
+  g.ch = g.r / spc;
+  g.wl = g.r - g.ch * spc;
+  g.A = static_cast<long long>(g.wl) * S;
+  g.B = min(g.A + S, a.n_dec);
+  g.Lr = static_cast<int>(g.B - g.A);
+  g.first = g.wl == 0;
+  g.last = g.B == a.n_dec;
+  const int nsub = (g.Lr + sg::L - 1) / sg::L;
+  const int ntiles = nsub * sg::NS;
+  const bool late = blockIdx.x >= (gridDim.x >> 1);
+  uint32_t* const myslot = a.hand + static_cast<long long>(g.r) * kSegSlot;
+  fu::trace(a, g.r, 0);
+
+  const FuPrefetch org = fu_origin(a, g);
+  f2 va[G::KL][2], vb[G::KL][2];
+  front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, l, va);
+  front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, l, vb);
+  const f2* __restrict__ tabc = a.tab + static_cast<long long>(g.ch) * kWbfmNS;
+  const f2* __restrict__ xc = a.x + g.ch * a.x_stride;
+  const f2* __restrict__ hc = a.hist_in + g.ch * kWbfmHist;
+  const f2 cn = tabc[G::NEW];
+  const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
+  const FuTile T{a, C, U, Phi, Gt, xc, hc, tabc, g.ch, l, c0 * g8::LRS + g8::slot((8 * Q + 2 * l + c0) / 8),
+                 c1 * g8::LRS + g8::slot((8 * Q + 2 * l + 1 + c1) / 8), f2{cn.x, -cn.y}, g.first};
+  long long porg = org.porg;
+  {  // halo rows of the first tile (clamped here, exact via the boundary fixup)
+    const long long P0 = porg + 2 * l;
+    const long long hi = (org.nl & ~1LL) - 2;
+    const long long Pc = P0 < 0 ? 0 : (P0 > hi ? hi : P0);
+    const f2 x0 = org.xl[Pc], x1 = org.xl[Pc + 1];
+    const f4 th = *reinterpret_cast<const f4*>(tabc + 2 * l);
+    U[c0 * g8::LRS + g8::slot((2 * l + c0) / 8)] = cmul_rot(x0, f2{th.x, th.y});
+    U[c1 * g8::LRS + g8::slot((2 * l + 1 + c1) / 8)] = cmul_rot(x1, f2{th.z, th.w});
+  }
+  {  // p = -l (row c = l, entry 0), l = 1..7: used only by d[A-1]
+    const long long Pm = max(porg - (l & 7), 0LL);
+    const f2 xm = xc[Pm];
+    const f2 tc = tabc[l & 7];
+    if (!g.first && l >= 1 && l < 8) U[l * g8::LRS] = cmul_rot(xm, f2{tc.x, -tc.y});
+  }
+  f2 Sv = f2{0, 0};
+  f2 carry = f2{0.0f, 0.0f};
+  if (g.first) {
+    const float* ci = a.carry_in + g.ch * kWbfmCarry;
+    carry = f2{ci[4], ci[5]};
+  }
+  double sw[4] = {0, 0, 0, 0};
+  float hist[2] = {0, 0};
+  const FuPrefetch dummy{org.xl, org.nl, -8LL * Q, true};
+
+#pragma unroll 1
+  for (int sub = 0, n = 0; sub < nsub; ++sub) {
+    f2 ph[G::KL][2];
+    {
+      const f4 tv = *reinterpret_cast<const f4*>(tabc + 8 * Q + 2 * l);
+      const f2 tb0 = f2{tv.x, tv.y}, tb1 = f2{tv.z, tv.w};
+#pragma unroll
+      for (int k = 0; k < G::KL; ++k) {
+        const f2 ek = tabc[128 * k];
+        ph[k][0] = cmul(tb0, ek);
+        ph[k][1] = cmul(tb1, ek);
+      }
+    }
+#pragma unroll 1
+    for (int tin = 0; tin < sg::NS; tin += 2, n += 2, porg += 2 * G::NEW) {
+      if (kSegPrio) {  // see k_wbfm_seg
+        if ((16 * n < kSegPrioQ16 * ntiles) == late) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+      if ((n & 63) == 0)
+        Sv = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1 + static_cast<long long>(l) * G::NEW),
+                        a.step[g.ch]);
+      const long long jd0 = g.A + static_cast<long long>(n) * TW;
+      const FuPrefetch p0 = n + 2 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 2 * G::NEW, true} : dummy;
+      const FuPrefetch p1 = n + 3 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 3 * G::NEW, true} : dummy;
+      float* dst = Phi + TW * tin;
+      fu_tile8<A16, CLAMP>(T, n, porg, jd0, ph, va, p0, Sv, carry, dst, n & 63);
+      fu_tile8<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + TW, ph, vb, p1, Sv, carry, dst + TW, (n + 1) & 63);
+    }
+    wave_lds_fence();
+    if (sub == 0) {
+      // keep sub-range 0's phi for the deferred back in the segment's global slot
+      f4* gs = reinterpret_cast<f4*>(myslot + kFuSlot);
+#pragma unroll
+      for (int i = 0; i < sg::L / 256; ++i) gs[l + 64 * i] = *reinterpret_cast<const f4*>(Phi + 4 * (l + 64 * i));
+      if (!(ORION_SEG_ABL & 2)) sg::zs_only(Bc, a.lanemats_sg, Phi, Phi, l, sw, hist);
+      if (nsub == 1 && !g.last) sg::publish_end(a, g.r, sw, hist, l, kSegSlot);
+    } else {
+      const long long A0 = g.A + static_cast<long long>(sub) * sg::L;
+      const int Lr = static_cast<int>(min(static_cast<long long>(sg::L), g.B - A0));
+      const bool lastsub = sub == nsub - 1;
+      if (sub <= 3) fu::trace(a, g.r, 3 + sub);
+      if (!(ORION_SEG_ABL & 1))
+        sg::back(a, Bc, g.ch, A0, Lr, g.last && lastsub, Phi, P, l, sw, hist, lastsub && !g.last ? g.r : -1,
+                 kSegSlot);
+      else if (lastsub && !g.last)
+        sg::publish_end(a, g.r, sw, hist, l, kSegSlot);
+      if (sub <= 3) fu::trace(a, g.r, 6 + sub);
+    }
+  }
+  fu::trace(a, g.r, 1);
+  if (ORION_SEG_ABL & 4) return;
+  // ---- deferred: sub-range 0 from the predecessor's end state ----
+  {
+    const f4* gs = reinterpret_cast<const f4*>(myslot + kFuSlot);
+    f4 u[sg::L / 256];
+#pragma unroll
+    for (int i = 0; i < sg::L / 256; ++i) u[i] = __builtin_nontemporal_load(gs + l + 64 * i);
+#pragma unroll
+    for (int i = 0; i < sg::L / 256; ++i) *reinterpret_cast<f4*>(Phi + 4 * (l + 64 * i)) = u[i];
+  }
+  if (g.first) {
+    const float* __restrict__ ci = a.carry_in + g.ch * kWbfmCarry;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sw[k] = ci[k];
+    hist[0] = ci[8 + l];
+    hist[1] = ci[8 + 64 + l];
+  } else {
+    fu::wait_for(a.flags + 3LL * (g.r - 1), a.epoch, a.err);
+    const uint32_t* ps = a.hand + static_cast<long long>(g.r - 1) * kSegSlot;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sw[k] = sg::uni(fu::u2d(fu::ld_agent(ps + 2 + 2 * k), fu::ld_agent(ps + 3 + 2 * k)));
+    hist[0] = __uint_as_float(fu::ld_agent(ps + 16 + l));
+    hist[1] = __uint_as_float(fu::ld_agent(ps + 16 + 64 + l));
+  }
+  wave_lds_fence();
+  fu::trace(a, g.r, 2);
+  sg::back(a, Bc, g.ch, g.A, min(sg::L, g.Lr), g.last && nsub == 1, Phi, P, l, sw, hist);
   fu::trace(a, g.r, 3);
 }
 
@@ -2726,11 +3045,12 @@ void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFused
                      int max_segments, int variant, hipStream_t s) {
   static_assert(sg::L == kSgL && sg2::L == kSgL, "sub-range geometry");
   if (a.n_dec <= 0 || nch <= 0) return;
-  static int caps[3] = {0, 0, 0};
+  static int caps[4] = {0, 0, 0, 0};
   int& cap = caps[variant];
   if (cap == 0) {
     int per_cu = 0, dev = 0, ncu = 0;
     if (variant == 2) ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_seg3<true, false>, 64, 0));
+    else if (variant == 3) ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_seg4<true, false>, 64, 0));
     else ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_seg2<true, false>, 64, 0));
     ORION_HIP(hipGetDevice(&dev));
     ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
@@ -2755,7 +3075,7 @@ void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFused
     if (a16) K<true, false><<<gi, 64, 0, s>>>(a, f, b, sp, Si);        \
     else K<false, false><<<gi, 64, 0, s>>>(a, f, b, sp, Si);           \
   }
-  if (variant == 2) { ORION_SEG(k_wbfm_seg3) } else if (variant == 1) { ORION_SEG(k_wbfm_seg2) } else { ORION_SEG(k_wbfm_seg) }
+  if (variant == 3) { ORION_SEG(k_wbfm_seg4) } else if (variant == 2) { ORION_SEG(k_wbfm_seg3) } else if (variant == 1) { ORION_SEG(k_wbfm_seg2) } else { ORION_SEG(k_wbfm_seg) }
 #undef ORION_SEG
   ORION_LAUNCH_CHECK();
 }

@@ -145,6 +145,7 @@ long long wbfm_fused_slots(long long n_dec, int nch);
 constexpr int kSgL = 1024;                           // outputs per sub-range
 constexpr int kSgC = kSgL / 128;                     // IIR samples per lane and half (8)
 constexpr int kSg2Slot = kSgL;                       // u32 words per k_wbfm_seg2 hand-off slot (phi)
+constexpr int kSeg4Slot = kFuSlot + kSg2Slot;        // k_wbfm_seg4: end-state record, then sub-range 0's phi
 long long wbfm_seg_slots(long long n_dec, int nch);
 // spread: k_wbfm_seg2 (FIR spread over the next sub-range's tiles, first sub-range
 // handed to the predecessor); else k_wbfm_seg. max_segments > 0 caps the waves.

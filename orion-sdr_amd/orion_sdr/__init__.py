@@ -425,7 +425,7 @@ class WbfmChain(_Block):
         self.m = int(m)
 
     _PATHS = {"auto": 0, "segmented": 1, "ranges": 2, "split": 3, "segmented_v1": 4, "specialized": 5,
-              "segmented3": 6}
+              "segmented3": 6, "segmented4": 7}
 
     def configure(self, path: str = "auto", max_segments: int = 0):
         """Engine tuning / tests (no reference counterpart): the kernel path and a

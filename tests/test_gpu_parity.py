@@ -305,6 +305,14 @@ def test_wbfm_full_size_windowed(gpu_lib, oracle):
     ("segmented3", 7, 4097 * 8 + 5),
     ("segmented3", 2, 8 * 1024 + 8),
     ("segmented3", 0, 1 << 20),     # the resident capacity: one sub-range per segment
+    ("segmented4", 3, 1 << 20),
+    ("segmented4", 1, 600_000),
+    ("segmented4", 7, 4097 * 8 + 5),
+    ("segmented4", 2, 8 * 1024 + 8),
+    ("segmented4", 0, 1 << 20),     # the resident capacity: one sub-range per segment
+    ("segmented4", 0, 100),         # tiny input: clamped loads, boundary fixups
+    ("segmented_v1", 1, 600_000),
+    ("segmented_v1", 7, 4097 * 8 + 5),
     ("ranges", 0, 1 << 20),
     ("split", 0, 1 << 20)])
 def test_wbfm_kernel_paths(gpu_lib, oracle, path, max_seg, n):
@@ -315,7 +323,8 @@ def test_wbfm_kernel_paths(gpu_lib, oracle, path, max_seg, n):
 
 
 @pytest.mark.parametrize("path,max_seg", [("segmented", 2), ("segmented", 5), ("specialized", 2), ("specialized", 5),
-                                          ("segmented3", 2), ("segmented3", 5)])
+                                          ("segmented3", 2), ("segmented3", 5), ("segmented4", 2),
+                                          ("segmented4", 5), ("segmented_v1", 2), ("segmented_v1", 5)])
 def test_wbfm_segmented_streaming_and_channels(gpu_lib, oracle, path, max_seg):
     """Carried state across calls and independent channels with several
     multi-sub-range segments per channel."""
