@@ -268,6 +268,175 @@ __global__ __launch_bounds__(64, 3) void k_decim_w(const f2* __restrict__ x, lon
   }
 }
 
+// ------------------------------------ four-group wave-independent decimator ---
+// k_decim_w4<Q>: k_decim_w with the decimator split over the four ds_read_b128
+// lane groups of gfx950 (as k_wbfm.hip's fu_tile8): lane group g (A = lanes 0-3,
+// 12-15, 20-27; B = 4-11, 16-19, 28-31; C, D = A, B + 32) sums phases 2g and 2g+1
+// for EIGHT outputs per lane (8l'..8l'+7, l' = l & 15), Q taps per phase in blocks
+// of 16 (12 window + 4 tap ds_read_b128, 128 v_pk_fma_f32 in eight chains per
+// block), and two permlane-swap rounds add the four partial sums, leaving each
+// lane two outputs (rows 0, 2, 1, 3 own 8l' + {0,1}, {2,3}, {4,5}, {6,7}). Image
+// rows carry a 16-B pad after every four 16-B chunks (lane windows 5 chunks
+// apart: conflict-free reads), pitch odd (the phase-scattered b64 staging stores
+// spread over banks). Per lane and tile (Q = 32): 64 ds_read_b128 against
+// k_decim_w's 136. Taps live in LDS (per-lane phases).
+#ifndef ORION_DW4_UNROLL
+#define ORION_DW4_UNROLL 4  // tap blocks unrolled: their LDS reads overlap the previous block's FMAs (1: 0.66 ms on C3, 4: 0.635)
+#endif
+template <int Q>
+struct Dw4 {
+  static constexpr int TW = 128;
+  static constexpr int NEW = 8 * TW;
+  static constexpr int KL = NEW / 128;
+  static constexpr int HALO = Q + 2;               // entries carried tile to tile
+  static constexpr int NCH = (TW + HALO + 1) / 2;  // 16-B chunks of a row in use
+  __host__ __device__ static constexpr int pchunk(int c) { return 5 * (c >> 2) + (c & 3); }
+  __host__ __device__ static constexpr int slot(int i) { return 2 * pchunk(i >> 1) + (i & 1); }
+  static constexpr int PCH = (pchunk(NCH - 1) + 1) | 1;  // row pitch in chunks, odd
+  static constexpr int LRS = 2 * PCH;
+  static constexpr int LDS_F2 = 8 * LRS;
+  static_assert(Q % 16 == 0 && (TW / 2) % 4 == 0, "geometry");
+};
+__device__ __forceinline__ int dw4_group(int l) {
+  const int i = l & 31;
+  const bool a = i < 4 || (i >= 12 && i < 16) || (i >= 20 && i < 28);
+  return (l >> 5) * 2 + (a ? 0 : 1);
+}
+__device__ __forceinline__ int dw4_first_out(int l) {
+  const int row = l >> 4;
+  return 8 * (l & 15) + 2 * (row == 0 ? 0 : row == 2 ? 1 : row == 1 ? 2 : 3);
+}
+
+template <int Q, bool A16, bool CLAMP>
+__device__ __forceinline__ void dw4_tile(f2* __restrict__ U, const float* __restrict__ Gt, int l, int n,
+                                         long long porg, long long J, const f2* __restrict__ xc, long long nx,
+                                         const f2* __restrict__ hc, int hist_len, f2 (&v)[Dw4<Q>::KL][2],
+                                         long long pforg, int s0, int s1, f2* __restrict__ outc, long long n_out) {
+  using D = Dw4<Q>;
+  if (n > 0) {  // halo: entries TW .. TW+Q+1 -> 0 .. Q+1 (chunks TW/2 + h -> h)
+#pragma unroll
+    for (int r2 = 0; r2 < (8 * D::HALO / 2 + 63) / 64; ++r2) {
+      const int e = l + 64 * r2;
+      if (e < 8 * D::HALO / 2) {
+        const int c = e / (D::HALO / 2), h = e - (D::HALO / 2) * c;
+        const int dst = c * D::LRS + 2 * D::pchunk(h);
+        *reinterpret_cast<f4*>(U + dst) = *reinterpret_cast<const f4*>(U + dst + 2 * D::pchunk(D::TW / 2));
+      }
+    }
+    wave_lds_fence();
+  }
+#pragma unroll
+  for (int k = 0; k < D::KL; ++k) {  // entry i + 16k = slot(i) + 20k
+    U[s0 + 20 * k] = v[k][0];
+    U[s1 + 20 * k] = v[k][1];
+  }
+  asm volatile("" ::: "memory");
+  dw_load<Q, A16, CLAMP>(xc, nx, pforg, l, v);  // the tile two ahead (unconditional: see fu_tile)
+  const bool bnd = porg < 0 || porg + 8LL * (D::TW + Q) > nx;
+  if (bnd || n == 0) {
+    wave_lds_fence();
+#pragma unroll 1
+    for (int p = (n == 0 ? 0 : 8 * Q) + l; p < 8 * (D::TW + Q); p += 64) {
+      const long long P = porg + p;
+      if (p < 8 * Q || !CLAMP || P < 0 || P >= nx) {
+        const int c = (-p) & 7;
+        U[c * D::LRS + D::slot((p + c) / 8)] = load_hist(xc, nx, hc, hist_len, P);
+      }
+    }
+  }
+  wave_lds_fence();
+  const int g = dw4_group(l), lp = l & 15;
+  f2 d[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) d[r] = f2{0.0f, 0.0f};
+#pragma unroll ORION_DW4_UNROLL
+  for (int b = 0; b < 2 * (Q / 16); ++b) {
+    const int c = 2 * g + (b & 1), hq = b >> 1;
+    // taps 16hq .. 16hq+15 of phase c read window entries from 2 cb, cb = Q/2 - 8 - 8hq chunks
+    const int cb = Q / 2 - 8 - 8 * hq;
+    const f4* __restrict__ row = reinterpret_cast<const f4*>(U + c * D::LRS) + 5 * lp + 5 * (cb >> 2);
+    f4 w[12];
+#pragma unroll
+    for (int h = 0; h < 12; ++h) w[h] = row[5 * (h >> 2) + (h & 3)];
+    const f4* __restrict__ tq = reinterpret_cast<const f4*>(Gt + c * Q + 16 * hq);
+    float t[16];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const f4 u = tq[q4];
+      t[4 * q4] = u.x;
+      t[4 * q4 + 1] = u.y;
+      t[4 * q4 + 2] = u.z;
+      t[4 * q4 + 3] = u.w;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int m = r + 16 - q;  // window entry 1 .. 23
+        const f4& wc = w[m >> 1];
+        d[r] = fma2(splat2(t[q]), (m & 1) ? f2{wc.z, wc.w} : f2{wc.x, wc.y}, d[r]);
+      }
+  }
+  f2 K[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // rows 0<->1, 2<->3: even rows keep outputs 0..3, odd rows 4..7
+    const auto sx = __builtin_amdgcn_permlane16_swap(__float_as_uint(d[i].x), __float_as_uint(d[i + 4].x), false, false);
+    const auto sy = __builtin_amdgcn_permlane16_swap(__float_as_uint(d[i].y), __float_as_uint(d[i + 4].y), false, false);
+    K[i] = f2{__uint_as_float(sx[0]), __uint_as_float(sy[0])} + f2{__uint_as_float(sx[1]), __uint_as_float(sy[1])};
+  }
+  f2 F[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // halves: rows 0, 1 keep K[0..1], rows 2, 3 K[2..3]
+    const auto sx = __builtin_amdgcn_permlane32_swap(__float_as_uint(K[i].x), __float_as_uint(K[i + 2].x), false, false);
+    const auto sy = __builtin_amdgcn_permlane32_swap(__float_as_uint(K[i].y), __float_as_uint(K[i + 2].y), false, false);
+    F[i] = f2{__uint_as_float(sx[0]), __uint_as_float(sy[0])} + f2{__uint_as_float(sx[1]), __uint_as_float(sy[1])};
+  }
+  const long long j = J + dw4_first_out(l);
+  if (j + 1 < n_out && (reinterpret_cast<uintptr_t>(outc + j) & 15) == 0) {
+    __builtin_nontemporal_store(f4{F[0].x, F[0].y, F[1].x, F[1].y}, reinterpret_cast<f4*>(outc + j));
+  } else {
+    if (j < n_out) outc[j] = F[0];
+    if (j + 1 < n_out) outc[j + 1] = F[1];
+  }
+}
+
+template <int Q, bool A16, bool CLAMP>
+__global__ __launch_bounds__(64, 2) void k_decim_w4(const f2* __restrict__ x, long long x_stride, long long n,
+                                                   const f2* __restrict__ hist, int hist_len, f2* __restrict__ out,
+                                                   long long out_stride, long long n_out, const Taps256 g, int wpc,
+                                                   long long L) {
+  using D = Dw4<Q>;
+  __shared__ __attribute__((aligned(16))) f2 U[D::LDS_F2];
+  __shared__ __attribute__((aligned(16))) float Gt[8 * Q];
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 8 * Q / 64; ++k) Gt[l + 64 * k] = g.g[l + 64 * k];
+  const int ch = blockIdx.x / wpc;
+  const long long A = static_cast<long long>(blockIdx.x - ch * wpc) * L;
+  const long long B = min(A + L, n_out);
+  if (A >= B) return;
+  const int ntiles = (static_cast<int>((B - A + D::TW - 1) / D::TW) + 1) & ~1;
+  const f2* __restrict__ xc = x + ch * x_stride;
+  const f2* __restrict__ hc = hist + static_cast<long long>(ch) * hist_len;
+  f2* __restrict__ outc = out + ch * out_stride;
+  const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
+  const int s0 = c0 * D::LRS + D::slot((8 * Q + 2 * l + c0) / 8);
+  const int s1 = c1 * D::LRS + D::slot((8 * Q + 2 * l + 1 + c1) / 8);
+  long long porg = 8LL * (A - Q);
+  f2 va[D::KL][2], vb[D::KL][2];
+  dw_load<Q, A16, CLAMP>(xc, n, porg, l, va);
+  dw_load<Q, A16, CLAMP>(xc, n, porg + D::NEW, l, vb);
+  const long long dummy = -8LL * Q;
+#pragma unroll 1
+  for (int t = 0; t < ntiles; t += 2, porg += 2 * D::NEW) {
+    const long long J = A + static_cast<long long>(t) * D::TW;
+    dw4_tile<Q, A16, CLAMP>(U, Gt, l, t, porg, J, xc, n, hc, hist_len, va,
+                            t + 2 < ntiles ? porg + 2 * D::NEW : dummy, s0, s1, outc, B);
+    dw4_tile<Q, A16, CLAMP>(U, Gt, l, t + 1, porg + D::NEW, J + D::TW, xc, n, hc, hist_len, vb,
+                            t + 3 < ntiles ? porg + 3 * D::NEW : dummy, s0, s1, outc, B);
+  }
+}
+
 __global__ __launch_bounds__(NT) void k_decim_generic(const f2* __restrict__ x, long long x_stride,
                                                       long long n, const f2* __restrict__ hist,
                                                       int hist_len, f2* __restrict__ out,
@@ -578,11 +747,17 @@ void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* 
     const char* e = std::getenv("ORION_DECIM_LEGACY");
     return e && e[0] == '1';
   }();
+  static const bool w2 = [] {  // experiments: k_decim_w (two outputs per lane) instead of k_decim_w4
+    const char* e = std::getenv("ORION_DECIM_W2");
+    return e && e[0] == '1';
+  }();
   if (M == 8 && K <= 256 && hist_len >= 8 * (K <= 128 ? 16 : 32) && !legacy) {
-    static int cap = 0;
+    static int caps[2] = {0, 0};
+    int& cap = caps[w2 ? 1 : 0];
     if (cap == 0) {
       int per_cu = 0, dev = 0, ncu = 0;
-      ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decim_w<32, true, false>, 64, 0));
+      if (w2) ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decim_w<32, true, false>, 64, 0));
+      else ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decim_w4<32, true, false>, 64, 0));
       ORION_HIP(hipGetDevice(&dev));
       ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
       cap = std::max(4, per_cu & ~3) * std::max(1, ncu);  // a multiple of 4 per CU: balanced SIMDs
@@ -596,15 +771,19 @@ void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* 
     if (grid > (1LL << 31) - 1) throw HipError("decimator grid too large");
     const bool clamp = n < 2 * 1024;
     const int gi = static_cast<int>(grid), wi = static_cast<int>(wpc);
-#define ORION_DW(QQ)                                                                                        \
+#define ORION_DW(KK, QQ)                                                                                    \
   if (clamp) {                                                                                              \
-    if (a16) k_decim_w<QQ, true, true><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
-    else k_decim_w<QQ, false, true><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
+    if (a16) KK<QQ, true, true><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
+    else KK<QQ, false, true><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
   } else {                                                                                                  \
-    if (a16) k_decim_w<QQ, true, false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
-    else k_decim_w<QQ, false, false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
+    if (a16) KK<QQ, true, false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
+    else KK<QQ, false, false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
   }
-    if (K <= 128) { ORION_DW(16) } else { ORION_DW(32) }
+    if (w2) {
+      if (K <= 128) { ORION_DW(k_decim_w, 16) } else { ORION_DW(k_decim_w, 32) }
+    } else {
+      if (K <= 128) { ORION_DW(k_decim_w4, 16) } else { ORION_DW(k_decim_w4, 32) }
+    }
 #undef ORION_DW
   } else if (M == 8 && K <= 256 && hist_len >= 8 * (K <= 128 ? 16 : 32)) {
     const long long tiles = (n_out + 511) / 512;

@@ -866,6 +866,9 @@ __device__ __forceinline__ void fu_tile(const FuTile& T, int n, long long porg, 
 // after every four chunks, so lane windows start 5 chunks apart and the 16 lanes
 // of a read group hit 16 distinct bank quads; the pitch (91 chunks, odd) spreads
 // the phase-scattered b64 staging stores.
+#ifndef ORION_SEG4_PHASE_UNROLL
+#define ORION_SEG4_PHASE_UNROLL 1
+#endif
 namespace g8 {
 constexpr int PCH = 91;          // row pitch, 16-B chunks
 constexpr int LRS = 2 * PCH;     // row pitch, f2 slots
@@ -937,7 +940,7 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
   f2 d[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) d[r] = f2{0.0f, 0.0f};
-#pragma unroll 1
+#pragma unroll ORION_SEG4_PHASE_UNROLL
   for (int s = 0; s < 2; ++s) {
     const int c = 2 * g + s;
     const f4* __restrict__ row = reinterpret_cast<const f4*>(U + c * g8::LRS) + 5 * lp;
@@ -1431,6 +1434,12 @@ __global__ __launch_bounds__(64, fu::Geo<N>::WavesPerSimd) void k_wbfm_fused(con
 #ifndef ORION_SEG_EARLY_PUB
 #define ORION_SEG_EARLY_PUB 1  // k_wbfm_seg publishes a segment's end state before its last audio FIR
 #endif
+#ifndef ORION_SEG_BACK_KB
+#define ORION_SEG_BACK_KB 8  // audio FIR taps per block in k_wbfm_seg's sub-range back
+#endif
+#ifndef ORION_SEG_BACK_UNROLL
+#define ORION_SEG_BACK_UNROLL 1
+#endif
 #ifndef ORION_SEG_PRIO_Q16
 #define ORION_SEG_PRIO_Q16 9
 #endif
@@ -1603,12 +1612,12 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
   if (publish_r >= 0) publish_end(a, publish_r, sw, hist, l, stride);
   {  // audio FIR (fir.rs:57-66), as in fu_back_range with taps in blocks of
      // KB = CH (a smaller window: this runs with two prefetched tiles live)
-    constexpr int KB = CH;
+    constexpr int KB = ORION_SEG_BACK_KB;
     constexpr int O = fu::PB - (KB - 1);  // pair index of window entry 0 at lane 0, block 0
     f2 acc[CH];
 #pragma unroll
     for (int i = 0; i < CH; ++i) acc[i] = f2{0.0f, 0.0f};
-#pragma unroll 1
+#pragma unroll ORION_SEG_BACK_UNROLL
     for (int kb = 0; kb < 128 / KB; ++kb) {
       // tap k = KB kb + kk of output i reads pair e = CH l + i - k + PB
       // = CH (l - kb) + O + m, m = i + KB - 1 - kk
