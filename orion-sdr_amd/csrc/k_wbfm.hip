@@ -891,9 +891,56 @@ __device__ __forceinline__ int first_out(int l) {
   const int row = l >> 4;
   return 8 * (l & 15) + 2 * (row == 0 ? 0 : row == 2 ? 1 : row == 1 ? 2 : 3);
 }
+// One phase c of a lane's eight outputs: 12 window + 4 tap ds_read_b128 and 128
+// v_pk_fma_f32. FIRST: the chains start with a product (d need not be zeroed).
+// ORD: taps read first and the taps walked from q = Q-1 down, so the first FMAs
+// need only the first window reads (entries 1..8) rather than the last.
+template <bool FIRST, bool ORD>
+__device__ __forceinline__ void phase(const f2* __restrict__ U, int c, int lp, const float* __restrict__ Gt,
+                                      f2 (&d)[8]) {
+  const f4* __restrict__ row = reinterpret_cast<const f4*>(U + c * LRS) + 5 * lp;
+  const f4* __restrict__ tq = reinterpret_cast<const f4*>(Gt + c * Q);
+  f4 w[12];
+  float t[Q];
+  if constexpr (ORD) {
+#pragma unroll
+    for (int q4 = Q / 4 - 1; q4 >= 0; --q4) {
+      const f4 u = tq[q4];
+      t[4 * q4] = u.x;
+      t[4 * q4 + 1] = u.y;
+      t[4 * q4 + 2] = u.z;
+      t[4 * q4 + 3] = u.w;
+    }
+#pragma unroll
+    for (int h = 0; h < 12; ++h) w[h] = row[5 * (h >> 2) + (h & 3)];
+  } else {
+#pragma unroll
+    for (int h = 0; h < 12; ++h) w[h] = row[5 * (h >> 2) + (h & 3)];
+#pragma unroll
+    for (int q4 = 0; q4 < Q / 4; ++q4) {
+      const f4 u = tq[q4];
+      t[4 * q4] = u.x;
+      t[4 * q4 + 1] = u.y;
+      t[4 * q4 + 2] = u.z;
+      t[4 * q4 + 3] = u.w;
+    }
+  }
+#pragma unroll
+  for (int qi = 0; qi < Q; ++qi) {
+    const int q = ORD ? Q - 1 - qi : qi;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int m = r + Q - q;  // window entry 1 .. 23 (tap q of output 8l' + r)
+      const f4& wc = w[m >> 1];
+      const f2 xv = (m & 1) ? f2{wc.z, wc.w} : f2{wc.x, wc.y};
+      if (FIRST && qi == 0) d[r] = splat2(t[q]) * xv;
+      else d[r] = fma2(splat2(t[q]), xv, d[r]);
+    }
+  }
+}
 }  // namespace g8
 
-template <bool A16, bool CLAMP>
+template <bool A16, bool CLAMP, int X>
 __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg, long long jd0,
                                          const f2 (&ph)[8][2], f2 (&v)[8][2], const FuPrefetch& pf, f2 Sv,
                                          f2& carry, float* __restrict__ phit, int svi) {
@@ -938,6 +985,13 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
   // group g: phases 2g, 2g+1; window entries 8l' .. 8l'+23 of the phase's row
   const int g = g8::group(l), lp = l & 15;
   f2 d[8];
+  if constexpr ((X & 1) != 0) {
+    // phase 2g opens the eight chains with a product (no zeroing), phase 2g+1
+    // follows; the barrier keeps the second phase's reads behind the first's FMAs
+    g8::phase<true, (X & 2) != 0>(U, 2 * g, lp, T.Gt, d);
+    asm volatile("" ::: "memory");
+    g8::phase<false, (X & 2) != 0>(U, 2 * g + 1, lp, T.Gt, d);
+  } else {
 #pragma unroll
   for (int r = 0; r < 8; ++r) d[r] = f2{0.0f, 0.0f};
 #pragma unroll ORION_SEG4_PHASE_UNROLL
@@ -965,6 +1019,7 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
         const f4& wc = w[m >> 1];
         d[r] = fma2(splat2(t[q]), (m & 1) ? f2{wc.z, wc.w} : f2{wc.x, wc.y}, d[r]);
       }
+  }
   }
   // rows 0<->1, 2<->3: even rows keep outputs 0..3, odd rows 4..7 (x: d[i], y: d[i+4])
   f2 K[4];
@@ -1824,12 +1879,20 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
 }
 
 // ---- segmented chain, four-group decimator ----------------------------------------
+#ifndef ORION_SEG4_X
+#define ORION_SEG4_X 0  // fu_tile8 bits: 1 first phase opens the chains with a product, 2 taps-first read order
+#endif
+#ifndef ORION_SEG4_XALT
+#define ORION_SEG4_XALT 3  // a second instantiation for in-process A/B (ORION_SEG4_X_LIVE=<bits>)
+#endif
+constexpr int kSeg4X = ORION_SEG4_X;
+constexpr int kSeg4XAlt = ORION_SEG4_XALT;
 // k_wbfm_seg4: k_wbfm_seg with fu_tile8's front tile. The padded image needs 2.3 KB
 // more LDS, so sub-range 0's phi (kept for the deferred back) go to the segment's
 // global slot (after its end-state record) instead of a third LDS buffer, and come
 // back at the end (L2/MALL-resident by then).
 constexpr int kSegSlot = kSeg4Slot;  // u32 words: end-state record, then sub-range 0's phi
-template <bool A16, bool CLAMP>
+template <bool A16, bool CLAMP, int X>
 __global__ __launch_bounds__(64, 2) void k_wbfm_seg4(const WbfmArgs a, const WbfmFrontConst C,
                                                      const WbfmFusedConst Bc, int spc, int S) {
   using G = fu::G;
@@ -1920,8 +1983,8 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg4(const WbfmArgs a, const Wbf
       const FuPrefetch p0 = n + 2 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 2 * G::NEW, true} : dummy;
       const FuPrefetch p1 = n + 3 < ntiles ? FuPrefetch{org.xl, org.nl, porg + 3 * G::NEW, true} : dummy;
       float* dst = Phi + TW * tin;
-      fu_tile8<A16, CLAMP>(T, n, porg, jd0, ph, va, p0, Sv, carry, dst, n & 63);
-      fu_tile8<A16, CLAMP>(T, n + 1, porg + G::NEW, jd0 + TW, ph, vb, p1, Sv, carry, dst + TW, (n + 1) & 63);
+      fu_tile8<A16, CLAMP, X>(T, n, porg, jd0, ph, va, p0, Sv, carry, dst, n & 63);
+      fu_tile8<A16, CLAMP, X>(T, n + 1, porg + G::NEW, jd0 + TW, ph, vb, p1, Sv, carry, dst + TW, (n + 1) & 63);
     }
     wave_lds_fence();
     if (sub == 0) {
@@ -3059,7 +3122,7 @@ void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFused
   if (cap == 0) {
     int per_cu = 0, dev = 0, ncu = 0;
     if (variant == 2) ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_seg3<true, false>, 64, 0));
-    else if (variant == 3) ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_seg4<true, false>, 64, 0));
+    else if (variant == 3) ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_seg4<true, false, kSeg4X>, 64, 0));
     else ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_seg2<true, false>, 64, 0));
     ORION_HIP(hipGetDevice(&dev));
     ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
@@ -3084,8 +3147,24 @@ void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFused
     if (a16) K<true, false><<<gi, 64, 0, s>>>(a, f, b, sp, Si);        \
     else K<false, false><<<gi, 64, 0, s>>>(a, f, b, sp, Si);           \
   }
-  if (variant == 3) { ORION_SEG(k_wbfm_seg4) } else if (variant == 2) { ORION_SEG(k_wbfm_seg3) } else if (variant == 1) { ORION_SEG(k_wbfm_seg2) } else { ORION_SEG(k_wbfm_seg) }
+  static const int seg4x_env = [] {  // timing experiments: the seg4 variant bits (kSeg4XAlt)
+    const char* e = std::getenv("ORION_SEG4_X");
+    return e ? std::atoi(e) : -1;
+  }();
+  const char* ex = std::getenv("ORION_SEG4_X_LIVE");  // in-process A/B (tools/ab_paths.py)
+  const int seg4x = ex ? std::atoi(ex) : seg4x_env;
+#define ORION_SEG4(XV)                                                         \
+  if (clamp) {                                                                 \
+    if (a16) k_wbfm_seg4<true, true, XV><<<gi, 64, 0, s>>>(a, f, b, sp, Si);   \
+    else k_wbfm_seg4<false, true, XV><<<gi, 64, 0, s>>>(a, f, b, sp, Si);      \
+  } else {                                                                     \
+    if (a16) k_wbfm_seg4<true, false, XV><<<gi, 64, 0, s>>>(a, f, b, sp, Si);  \
+    else k_wbfm_seg4<false, false, XV><<<gi, 64, 0, s>>>(a, f, b, sp, Si);     \
+  }
+  if (variant == 3 && kSeg4XAlt != kSeg4X && seg4x == kSeg4XAlt) { ORION_SEG4(kSeg4XAlt) } else
+  if (variant == 3) { ORION_SEG4(kSeg4X) } else if (variant == 2) { ORION_SEG(k_wbfm_seg3) } else if (variant == 1) { ORION_SEG(k_wbfm_seg2) } else { ORION_SEG(k_wbfm_seg) }
 #undef ORION_SEG
+#undef ORION_SEG4
   ORION_LAUNCH_CHECK();
 }
 

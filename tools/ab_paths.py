@@ -21,7 +21,9 @@ s = torch.cuda.current_stream(dev)
 res = {p: [] for p in paths}
 for rnd in range(int(os.environ.get("AB_ROUNDS", "6"))):
     for p in paths:
-        name, _, ms = p.partition(":")
+        spec, _, xv = p.partition("@")  # "@<bits>": k_wbfm_seg4's alternate variant (ORION_SEG4_X_LIVE)
+        os.environ["ORION_SEG4_X_LIVE"] = xv or "-1"
+        name, _, ms = spec.partition(":")
         blk.configure(name, int(ms or 0))
         blk.process_device(x, out, s.cuda_stream)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -31,6 +33,9 @@ for rnd in range(int(os.environ.get("AB_ROUNDS", "6"))):
         e1.record(s)
         torch.cuda.synchronize()
         res[p].append(1e3 * e0.elapsed_time(e1) / 10)
+base = np.array(res[paths[0]][1:])
 for p in paths:
     v = np.array(res[p][1:])
-    print(f"{p:14s} median {np.median(v):7.1f} us  min {v.min():7.1f} us  ({' '.join(f'{t:.0f}' for t in res[p])})")
+    d = np.median(v - base)  # paired with the first path's same round (the clock drifts between rounds)
+    print(f"{p:14s} median {np.median(v):7.1f} us  min {v.min():7.1f} us  paired diff {d:+6.1f} us  "
+          f"({' '.join(f'{t:.0f}' for t in res[p])})")
