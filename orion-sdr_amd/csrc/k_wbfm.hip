@@ -1312,11 +1312,17 @@ __device__ __forceinline__ void fu_back_range(const WbfmArgs& a, const WbfmFront
     const int jl = Lr - 1;  // local index of the channel's last sample (last range)
     float cap[4] = {0, 0, 0, 0};
     bool have = false;
+    // pslot(CH l + PB + i) = pslot(CH l + PB) + i for i < CH: one base address (the
+    // per-i form is not seen as linear and its eight addresses spill to scratch,
+    // whose reloads wait vmcnt(0) on the prefetched tiles)
+    int po = Y::pslot(CH * l + fu::PB);
+    asm volatile("" : "+v"(po));  // not hoisted out of the sub-range loop (see iir16's pass 2)
+    f2* __restrict__ pb = P + po;
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const int j = CH * l + i;
       const f2 f = bq.lp4(ef, xs[i]);
-      P[Y::pslot(j + fu::PB)] = f;
+      pb[i] = f;
       if (last) {
         if (j == jl) {
 #pragma unroll
@@ -1596,6 +1602,97 @@ __device__ __forceinline__ void zs_only(const WbfmFusedConst& Bc, const double* 
   wave_lds_fence();
 }
 
+// Sub-range IIR with lane l owning the 16 CONSECUTIVE samples 16l .. 16l+15: chunk E
+// (16l .. 16l+7) in the x halves and chunk O (16l+8 .. 16l+15) in the y halves of
+// xs, both zero-state passes packed. The lane aggregate A^8 zE + zO is scanned over
+// the 64 lanes (Kogge-Stone, f64, step matrices A^(16 2^s) = pw[s+1], mh) with the
+// entering state sw folded into lane 0, so the scan yields every lane's TRUE entering
+// state directly: no per-lane transition matrices (lanemats) and half the f64 work
+// of zero_state + the A^{CH l} products. ef: the f32 entering states of E and O;
+// send: the f64 end state after sample L-1 (uniform).
+static_assert(offsetof(WbfmFusedConst, mh) == offsetof(WbfmFusedConst, pw) + 6 * 16 * sizeof(double),
+              "iir16 reads A^512 as pw[6]");
+__device__ __forceinline__ void iir16(const WbfmFusedConst& Bc, const float* __restrict__ Phi, int l,
+                                      const double (&sw)[4], f2 (&xs)[CH], f2 (&ef)[4], double (&send)[4]) {
+#pragma unroll
+  for (int i = 0; i < CH; i += 4) {
+    const f4 u = *reinterpret_cast<const f4*>(Phi + 16 * l + i);
+    const f4 w = *reinterpret_cast<const f4*>(Phi + 16 * l + 8 + i);
+    xs[i] = f2{u.x, w.x};
+    xs[i + 1] = f2{u.y, w.y};
+    xs[i + 2] = f2{u.z, w.z};
+    xs[i + 3] = f2{u.w, w.w};
+  }
+  wave_lds_fence();
+  const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
+  f2 z[4] = {f2{0, 0}, f2{0, 0}, f2{0, 0}, f2{0, 0}};
+#pragma unroll
+  for (int i = 0; i < CH; ++i) (void)bq.lp4(z, xs[i]);
+  double zE[4], q[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    zE[k] = z[k].x;
+    q[k] = z[k].y;
+  }
+  matvec_acc<4>(Bc.pw, zE, q);  // A^8 zE + zO
+  {
+    double f[4] = {0, 0, 0, 0};
+    matvec_acc<4>(Bc.pw + 16, sw, f);  // A^16 sw
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] += l == 0 ? f[k] : 0.0;
+  }
+#pragma unroll 1
+  for (int st = 0; st < 6; ++st) {
+    const int dd = 1 << st;
+    double o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = __shfl_up(q[k], dd, 64);
+    if (l >= dd) matvec_acc<4>(Bc.pw + (st + 1) * 16, o, q);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const long long b = __double_as_longlong(q[k]);
+    const int lo = __builtin_amdgcn_readlane(static_cast<int>(b), 63);
+    const int hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), 63);
+    send[k] = __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+  }
+  double eE[4], eO[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double o = __shfl_up(q[k], 1, 64);
+    eE[k] = l == 0 ? sw[k] : o;
+    eO[k] = zE[k];
+  }
+  matvec_acc<4>(Bc.pw, eE, eO);  // entering O = A^8 (entering E) + zE
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ef[k] = f2{static_cast<float>(eE[k]), static_cast<float>(eO[k])};
+}
+
+// zs_only with iir16: sub-range 0's zero-state end state sw and zero-state last 128
+// IIR outputs (lanes 56..63 run their pass 2; tmp: 128 floats of free LDS).
+__device__ __forceinline__ void zs_only16(const WbfmFusedConst& Bc, const float* Phi, float* tmp, int l,
+                                          double (&sw)[4], float (&hout)[2]) {
+  const double zero[4] = {0, 0, 0, 0};
+  f2 xs[CH], ef[4];
+  iir16(Bc, Phi, l, zero, xs, ef, sw);
+  const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
+  int to = 16 * (l - 56);
+  asm volatile("" : "+v"(to));  // not hoisted and spilled (see iir16's pass 2)
+  float* __restrict__ tl = tmp + to;
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const f2 f = bq.lp4(ef, xs[i]);
+    if (l >= 56) {  // f[16l + i], f[16l + 8 + i]: tail index 16(l - 56) + i (+ 8)
+      tl[i] = f.x;
+      tl[8 + i] = f.y;
+    }
+  }
+  wave_lds_fence();
+  hout[0] = tmp[l];
+  hout[1] = tmp[l + 64];
+  wave_lds_fence();
+}
+
 // The back of one sub-range [A0, A0 + Lr) from its exact entering state sw and
 // FIR history hist (f[A0 - 128 + l + 64 r]): pass 2 (the reference's f32
 // recurrence) -> pair image P -> audio FIR -> y. Returns the end state (after
@@ -1606,16 +1703,60 @@ __device__ __forceinline__ void zs_only(const WbfmFusedConst& Bc, const double* 
 // (publish_end) as soon as they are known, before the audio FIR.
 __device__ __forceinline__ void publish_end(const WbfmArgs& a, int r, const double (&sw)[4], const float (&hist)[2],
                                             int l, int stride = kFuSlot);
+template <int KB = ORION_SEG_BACK_KB, bool I16 = false>
 __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc, int ch, long long A0, int Lr,
                                      bool chan_last, const float* Phi, f2* P, int l, double (&sw)[4],
-                                     float (&hist)[2], int publish_r = -1, int stride = kFuSlot) {
+                                     float (&hist)[2], int publish_r = -1, int stride = kFuSlot, int trace_r = -1) {
   constexpr int NH = Y::NH;
-  const double* __restrict__ lm = a.lanemats_sg;
+  const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
   f2 xs[CH];
+  f2 ef[4];
+  if constexpr (I16) {  // lane l: samples 16l .. 16l+15 (iir16), written to P one scalar at a time
+    double send[4];
+    iir16(Bc, Phi, l, sw, xs, ef, send);
+    if (trace_r >= 0) fu::trace(a, trace_r, 10);
+    const int jl = Lr - 1;
+    float cap[4] = {0, 0, 0, 0};
+    bool have = false;
+    // f[16l + i] -> pair slot pslot((16l mod NH) + PB + i), component l >= 32; the
+    // slots of i and i + 8 are CH + 1 apart (one pad per CH pairs)
+    // (the offset is laundered: hoisted out of the sub-range loop it would be one
+    // more long-lived register, spilled, with a vmcnt(0) reload)
+    int po = 2 * Y::pslot(16 * (l & 31) + fu::PB) + (l >> 5);
+    asm volatile("" : "+v"(po));
+    float* __restrict__ pe = reinterpret_cast<float*>(P) + po;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int j = 16 * l + i;  // and j + 8
+      const f2 f = bq.lp4(ef, xs[i]);
+      pe[2 * i] = f.x;
+      pe[2 * (i + CH + 1)] = f.y;
+      if (chan_last) {
+        if (j == jl) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) cap[k] = ef[k].x;
+          have = true;
+        }
+        if (j + 8 == jl) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) cap[k] = ef[k].y;
+          have = true;
+        }
+      }
+    }
+    if (have) {
+      float* co = a.carry_out + ch * kWbfmCarry;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) co[k] = cap[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      sw[k] = static_cast<double>(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(ef[k].y), 63)));
+  } else {
+  const double* __restrict__ lm = a.lanemats_sg;
   double ez[2][4], agg[4];
   zero_state(Bc, lm, Phi, l, xs, ez, agg);
-  const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
-  f2 ef[4];
+  if (trace_r >= 0) fu::trace(a, trace_r, 10);  // debug: zero-state pass + scan done
   {  // true entering states: half A += A^{CH l} sw, half B += A^{CH l} A^NH sw
     double sB[4] = {0, 0, 0, 0};
     matvec_acc<4>(Bc.mh, sw, sB);
@@ -1628,11 +1769,17 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
     const int jl = Lr - 1;
     float cap[4] = {0, 0, 0, 0};
     bool have = false;
+    // pslot(CH l + PB + i) = pslot(CH l + PB) + i for i < CH: one base address (the
+    // per-i form is not seen as linear and its eight addresses spill to scratch,
+    // whose reloads wait vmcnt(0) on the prefetched tiles)
+    int po = Y::pslot(CH * l + fu::PB);
+    asm volatile("" : "+v"(po));  // not hoisted out of the sub-range loop (see iir16's pass 2)
+    f2* __restrict__ pb = P + po;
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const int j = CH * l + i;
       const f2 f = bq.lp4(ef, xs[i]);
-      P[Y::pslot(j + fu::PB)] = f;
+      pb[i] = f;
       if (chan_last) {
         if (j == jl) {
 #pragma unroll
@@ -1655,6 +1802,7 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
     for (int k = 0; k < 4; ++k)
       sw[k] = static_cast<double>(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(ef[k].y), 63)));
   }
+  }
   wave_lds_fence();
 #pragma unroll
   for (int r2 = 0; r2 < 2; ++r2) {  // pairs j in [-128, 0): (history, f[j + NH])
@@ -1665,9 +1813,9 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
 #pragma unroll
   for (int r2 = 0; r2 < 2; ++r2) hist[r2] = P[Y::pslot(NH + l + 64 * r2)].y;  // f[L - 128 + t]: the next history
   if (publish_r >= 0) publish_end(a, publish_r, sw, hist, l, stride);
+  if (trace_r >= 0) fu::trace(a, trace_r, 11);  // debug: IIR done
   {  // audio FIR (fir.rs:57-66), as in fu_back_range with taps in blocks of
      // KB = CH (a smaller window: this runs with two prefetched tiles live)
-    constexpr int KB = ORION_SEG_BACK_KB;
     constexpr int O = fu::PB - (KB - 1);  // pair index of window entry 0 at lane 0, block 0
     f2 acc[CH];
 #pragma unroll
@@ -1715,6 +1863,7 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
     }
   }
   wave_lds_fence();
+  if (trace_r >= 0) fu::trace(a, trace_r, 12);  // debug: audio FIR done
 }
 
 // Publish a segment's end state and last 128 IIR outputs to its successor.
@@ -1880,10 +2029,11 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
 
 // ---- segmented chain, four-group decimator ----------------------------------------
 #ifndef ORION_SEG4_X
-#define ORION_SEG4_X 0  // fu_tile8 bits: 1 first phase opens the chains with a product, 2 taps-first read order
+#define ORION_SEG4_X 7  // bits: 1 first phase opens the chains with a product, 2 taps-first read order (fu_tile8),
+                         // 4 audio FIR in blocks of 16 taps (sg::back), 8 iir16 (16 consecutive samples per lane)
 #endif
 #ifndef ORION_SEG4_XALT
-#define ORION_SEG4_XALT 3  // a second instantiation for in-process A/B (ORION_SEG4_X_LIVE=<bits>)
+#define ORION_SEG4_XALT 15  // a second instantiation for in-process A/B (ORION_SEG4_X_LIVE=<bits>)
 #endif
 constexpr int kSeg4X = ORION_SEG4_X;
 constexpr int kSeg4XAlt = ORION_SEG4_XALT;
@@ -1992,7 +2142,8 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg4(const WbfmArgs a, const Wbf
       f4* gs = reinterpret_cast<f4*>(myslot + kFuSlot);
 #pragma unroll
       for (int i = 0; i < sg::L / 256; ++i) gs[l + 64 * i] = *reinterpret_cast<const f4*>(Phi + 4 * (l + 64 * i));
-      if (!(ORION_SEG_ABL & 2)) sg::zs_only(Bc, a.lanemats_sg, Phi, Phi, l, sw, hist);
+      if constexpr ((X & 8) != 0) sg::zs_only16(Bc, Phi, Phi, l, sw, hist);
+      else if (!(ORION_SEG_ABL & 2)) sg::zs_only(Bc, a.lanemats_sg, Phi, Phi, l, sw, hist);
       if (nsub == 1 && !g.last) sg::publish_end(a, g.r, sw, hist, l, kSegSlot);
     } else {
       const long long A0 = g.A + static_cast<long long>(sub) * sg::L;
@@ -2000,8 +2151,8 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg4(const WbfmArgs a, const Wbf
       const bool lastsub = sub == nsub - 1;
       if (sub <= 3) fu::trace(a, g.r, 3 + sub);
       if (!(ORION_SEG_ABL & 1))
-        sg::back(a, Bc, g.ch, A0, Lr, g.last && lastsub, Phi, P, l, sw, hist, lastsub && !g.last ? g.r : -1,
-                 kSegSlot);
+        sg::back<(X & 4) ? 16 : ORION_SEG_BACK_KB, (X & 8) != 0>(a, Bc, g.ch, A0, Lr, g.last && lastsub, Phi, P, l, sw, hist, lastsub && !g.last ? g.r : -1,
+                 kSegSlot, sub == 1 ? g.r : -1);
       else if (lastsub && !g.last)
         sg::publish_end(a, g.r, sw, hist, l, kSegSlot);
       if (sub <= 3) fu::trace(a, g.r, 6 + sub);
@@ -2034,7 +2185,7 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg4(const WbfmArgs a, const Wbf
   }
   wave_lds_fence();
   fu::trace(a, g.r, 2);
-  sg::back(a, Bc, g.ch, g.A, min(sg::L, g.Lr), g.last && nsub == 1, Phi, P, l, sw, hist);
+  sg::back<(X & 4) ? 16 : ORION_SEG_BACK_KB, (X & 8) != 0>(a, Bc, g.ch, g.A, min(sg::L, g.Lr), g.last && nsub == 1, Phi, P, l, sw, hist);
   fu::trace(a, g.r, 3);
 }
 
@@ -2238,11 +2389,17 @@ __device__ __forceinline__ void iir(const WbfmArgs& a, const WbfmFusedConst& Bc,
     scan_states(Bc, PhA, PhB, l, sw, xs, ef, end);
     const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
     hl = jl < NH ? jl / CH : (jl - NH) / CH;
+    // pslot(CH l + PB + i) = pslot(CH l + PB) + i for i < CH: one base address (the
+    // per-i form is not seen as linear and its eight addresses spill to scratch,
+    // whose reloads wait vmcnt(0) on the prefetched tiles)
+    int po = Y::pslot(CH * l + fu::PB);
+    asm volatile("" : "+v"(po));  // not hoisted out of the sub-range loop (see iir16's pass 2)
+    f2* __restrict__ pb = P + po;
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const int j = CH * l + i;
       const f2 f = bq.lp4(ef, xs[i]);
-      P[Y::pslot(j + fu::PB)] = f;
+      pb[i] = f;
       if (j == jl) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) cap[k] = ef[k].x;

@@ -134,7 +134,7 @@ struct WbfmArgs {
   long long* trace;                                 // debug: per-wave phase timestamps (or null)
   int fu_abl;                                       // timing ablations of the fused kernel (0)
 };
-constexpr int kFuTracePoints = 10;
+constexpr int kFuTracePoints = 16;
 void launch_wbfm(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmBackConst& b, int nch,
                  hipStream_t s);
 // Fused chain: requires ||A^kFuL|| negligible (the block checks it); returns the

@@ -24,7 +24,7 @@ blk = orion_sdr.WbfmChain().configure(sys.argv[2] if len(sys.argv) > 2 else "seg
 for _ in range(5):  # the last launch's trace is kept
     blk.process_device(x, out, torch.cuda.current_stream(dev).cuda_stream)
 torch.cuda.synchronize()
-t = np.fromfile(path, dtype=np.int64).reshape(-1, 10)
+t = np.fromfile(path, dtype=np.int64).reshape(-1, 16)
 t = t[(t[:, [0, 1, 3, 4, 5, 6, 7, 8, 9]] > 0).all(axis=1)]
 us = (t - t[:, 0].min()) / 100.0
 print(f"waves {len(t)}  span {us[:, 3].max():.1f} us  last start {us[:, 0].max():.1f} us")
@@ -40,12 +40,16 @@ ph = {
     "tail (IIR + 2 FIR)": us[:, 3] - us[:, 2],
     "whole": us[:, 3] - us[:, 0],
 }
+if (t[:, 10] > 0).all():  # k_wbfm_seg4: sub-range 1's back split
+    ph["  sub1 zero-state+scan"] = us[:, 10] - us[:, 4]
+    ph["  sub1 states+pass2"] = us[:, 11] - us[:, 10]
+    ph["  sub1 audio FIR"] = us[:, 12] - us[:, 11]
 print(f"{'phase':22s} {'mean':>7s} {'p10':>7s} {'p50':>7s} {'p90':>7s} {'max':>7s}")
 for k, v in ph.items():
     v = v[np.isfinite(v)]
     print(f"{k:22s} {v.mean():7.2f} {np.percentile(v, 10):7.2f} {np.percentile(v, 50):7.2f} "
           f"{np.percentile(v, 90):7.2f} {v.max():7.2f}")
-r = np.nonzero((np.fromfile(path, dtype=np.int64).reshape(-1, 10)[:, [0, 1, 3, 4, 5, 6, 7, 8, 9]] > 0).all(axis=1))[0]
+r = np.nonzero((np.fromfile(path, dtype=np.int64).reshape(-1, 16)[:, [0, 1, 3, 4, 5, 6, 7, 8, 9]] > 0).all(axis=1))[0]
 half = (r.max() + 1) // 2
 for nm, m in (("early (r < grid/2)", r < half), ("late", r >= half)):
     e = us[m, 3]
