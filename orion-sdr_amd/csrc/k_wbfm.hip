@@ -2029,7 +2029,7 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
 
 // ---- segmented chain, four-group decimator ----------------------------------------
 #ifndef ORION_SEG4_X
-#define ORION_SEG4_X 7  // bits: 1 first phase opens the chains with a product, 2 taps-first read order (fu_tile8),
+#define ORION_SEG4_X 15  // bits: 1 first phase opens the chains with a product, 2 taps-first read order (fu_tile8),
                          // 4 audio FIR in blocks of 16 taps (sg::back), 8 iir16 (16 consecutive samples per lane)
 #endif
 #ifndef ORION_SEG4_XALT
