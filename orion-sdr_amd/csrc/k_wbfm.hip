@@ -2029,11 +2029,12 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
 
 // ---- segmented chain, four-group decimator ----------------------------------------
 #ifndef ORION_SEG4_X
-#define ORION_SEG4_X 15  // bits: 1 first phase opens the chains with a product, 2 taps-first read order (fu_tile8),
-                         // 4 audio FIR in blocks of 16 taps (sg::back), 8 iir16 (16 consecutive samples per lane)
+#define ORION_SEG4_X 31  // bits: 1 first phase opens the chains with a product, 2 taps-first read order (fu_tile8),
+                         // 4 audio FIR in blocks of 16 taps (sg::back), 8 iir16 (16 consecutive samples per lane),
+                         // 16 XCD-contiguous segment runs
 #endif
 #ifndef ORION_SEG4_XALT
-#define ORION_SEG4_XALT 15  // a second instantiation for in-process A/B (ORION_SEG4_X_LIVE=<bits>)
+#define ORION_SEG4_XALT 31  // a second instantiation for in-process A/B (ORION_SEG4_X_LIVE=<bits>)
 #endif
 constexpr int kSeg4X = ORION_SEG4_X;
 constexpr int kSeg4XAlt = ORION_SEG4_XALT;
@@ -2057,6 +2058,13 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg4(const WbfmArgs a, const Wbf
   Gt[l + 64] = C.g[l + 64];
   FuRange g;
   g.r = blockIdx.x;
+  if constexpr ((X & 16) != 0) {
+    // workgroups reach the XCDs round-robin (blockIdx % 8): give each XCD a
+    // contiguous run of segments, so that a segment's predecessor (whose end
+    // state it waits for) and its halo tile mostly sit on the same XCD
+    const int nb = static_cast<int>(gridDim.x);
+    if ((nb & 7) == 0) g.r = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
+  }
   g.ch = g.r / spc;
   g.wl = g.r - g.ch * spc;
   g.A = static_cast<long long>(g.wl) * S;

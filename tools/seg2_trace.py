@@ -57,3 +57,13 @@ for nm, m in (("early (r < grid/2)", r < half), ("late", r >= half)):
 for q in (4, 7, 5, 8, 6, 9, 1, 3):
     print(f"pt{q}: start-to-point p10/p50/p90 {np.percentile(us[:, q], 10):.1f} {np.percentile(us[:, q], 50):.1f} "
           f"{np.percentile(us[:, q], 90):.1f}")
+# slowest waves: which phase is long, and where they sit
+end = us[:, 3]
+slow = end >= np.percentile(end, 95)
+print(f"slowest 5% ({slow.sum()} waves, end >= {np.percentile(end, 95):.1f} us): phase means vs all")
+for k, v in ph.items():
+    print(f"  {k:22s} {v[slow].mean():7.2f} vs {v.mean():7.2f}")
+rr = r[: len(us)]
+print("end p50 by XCD (blockIdx % 8):", " ".join(f"{np.median(end[rr % 8 == x]):.1f}" for x in range(8)))
+print("slow waves per XCD:", " ".join(str(int(slow[rr % 8 == x].sum())) for x in range(8)))
+print("slow waves' start p50 / all:", f"{np.median(us[slow, 0]):.2f} / {np.median(us[:, 0]):.2f}")
