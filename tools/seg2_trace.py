@@ -67,3 +67,10 @@ rr = r[: len(us)]
 print("end p50 by XCD (blockIdx % 8):", " ".join(f"{np.median(end[rr % 8 == x]):.1f}" for x in range(8)))
 print("slow waves per XCD:", " ".join(str(int(slow[rr % 8 == x].sum())) for x in range(8)))
 print("slow waves' start p50 / all:", f"{np.median(us[slow, 0]):.2f} / {np.median(us[:, 0]):.2f}")
+raw = np.fromfile(path, dtype=np.int64).reshape(-1, 16)
+if (raw[:, 14] > 0).any():  # k_wbfm_seg4 geometry
+    Lr = raw[r, 14]
+    print("segment lengths: min/p50/max", Lr.min(), int(np.median(Lr)), Lr.max(),
+          " by XCD (mean):", " ".join(f"{Lr[rr % 8 == x].mean():.0f}" for x in range(8)))
+    sl = raw[r, 14][slow]
+    print("slow waves' lengths:", np.unique(sl, return_counts=True))
