@@ -237,11 +237,23 @@ def main():
                                           else f"channel-sharded x{world}, no data-path collective")),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "k_wbfm" if args.config in ("c2", "c4") else ("k_decim8" if args.config == "c3"
-                                                                            else "k_scan_*"),
+                     "kernel": "k_wbfm_seg4" if args.config in ("c2", "c4") else ("k_decim_w4" if args.config == "c3"
+                                                                                 else "k_lpdc_sp"),
                      "kernel_ms": round(kern_ms, 4), "bytes_per_sample": bps},
         "cpu_baseline": None,
     }
+    # on-box read ceiling (after the timed region): the library's streaming-read probe
+    # over this rank's input, 10 launches between events
+    nb = orion_sdr.diag_stream_read(x, stream.cuda_stream)
+    p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    p0.record(stream)
+    for _ in range(10):
+        orion_sdr.diag_stream_read(x, stream.cuda_stream)
+    p1.record(stream)
+    torch.cuda.synchronize(dev)
+    peak_meas = nb / (p0.elapsed_time(p1) / 10 * 1e-3) / 1e9
+    line["roofline"]["peak_measured"] = round(peak_meas, 1)
+    line["roofline"]["frac_measured"] = round(achieved / peak_meas, 4)
     traffic_file = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(traffic_file):
         tr = json.load(open(traffic_file))

@@ -54,6 +54,11 @@ const char* orion_last_error(void);          /* thread-local message of the last
 int orion_device_count(void);
 int orion_set_device(int device);
 int orion_synchronize(void* stream);
+/* On-box bandwidth probe (no reference counterpart; bench.py's measured read
+ * peak): one streaming read of the first orion_diag_stream_read_bytes(bytes)
+ * bytes of the 16-B aligned device buffer `dev`, asynchronous on `stream`. */
+size_t orion_diag_stream_read_bytes(size_t bytes);
+int orion_diag_stream_read(const void* dev, size_t bytes, void* stream);
 
 /* ---- constructors (one per reference constructor) ---------------------- */
 /* dsp/rotator.rs:16-26 Rotator::new(freq_hz, fs); Block-like rotate_block (:74-85). cf32->cf32 */

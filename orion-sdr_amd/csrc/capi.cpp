@@ -63,6 +63,23 @@ int orion_set_device(int d) {
     return ORION_OK;
   });
 }
+size_t orion_diag_stream_read_bytes(size_t bytes) {
+  try {
+    return static_cast<size_t>(orion::stream_read_bytes(static_cast<long long>(bytes)));
+  } catch (...) {
+    return 0;
+  }
+}
+int orion_diag_stream_read(const void* dev, size_t bytes, void* stream) {
+  if (!dev) return fail(ORION_E_NULL, "null buffer");
+  if (reinterpret_cast<uintptr_t>(dev) % 16) return fail(ORION_E_ARG, "buffer not 16-B aligned");
+  return guarded([&] {
+    static orion::DevBuf sink(256);
+    orion::launch_stream_read(dev, static_cast<long long>(bytes), sink.as<float>(),
+                              static_cast<hipStream_t>(stream));
+    return ORION_OK;
+  });
+}
 int orion_synchronize(void* stream) {
   return guarded([&] {
     ORION_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));

@@ -1,0 +1,61 @@
+// k_diag.hip — on-box bandwidth probe (no reference counterpart). bench.py quotes
+// its streaming-read rate beside the 8 TB/s spec peak, as the achievable ceiling a
+// read-dominated kernel is measured against ("the fraction of a
+// measured on-box copy kernel"). Shape from the round-2 stream microbenchmark
+// (tools/micro/stream_mlp.hip: its fastest configuration): four
+// one-wave workgroups per CU, each streaming one contiguous range with one 8-KiB
+// tile of nontemporal 16-B loads in flight.
+#include <hip/hip_runtime.h>
+
+#include "hip_common.hpp"
+#include "kernels.hpp"
+
+namespace orion {
+namespace {
+
+constexpr int kDiagKL = 8;                  // f4 per lane per tile (8 KiB per wave)
+constexpr int kDiagTile = 64 * kDiagKL;     // f4 per tile
+
+__global__ __launch_bounds__(64) void k_stream_read(const f4* __restrict__ x, long long tiles_per_wave,
+                                                    long long n4, float* __restrict__ sink) {
+  const int l = threadIdx.x;
+  const f4* p = x + static_cast<long long>(blockIdx.x) * tiles_per_wave * kDiagTile;
+  f4 acc = {0, 0, 0, 0};
+  f4 v[kDiagKL];
+#pragma unroll
+  for (int k = 0; k < kDiagKL; ++k) v[k] = __builtin_nontemporal_load(p + l + 64 * k);
+  for (long long t = 0; t < tiles_per_wave; ++t) {
+    f4 cur[kDiagKL];
+#pragma unroll
+    for (int k = 0; k < kDiagKL; ++k) cur[k] = v[k];
+    asm volatile("" ::: "memory");
+    // the next tile (the last wave's last tile re-reads its own: always in range)
+    const f4* q = p + (t + 1 < tiles_per_wave ? t + 1 : t) * kDiagTile;
+#pragma unroll
+    for (int k = 0; k < kDiagKL; ++k) v[k] = __builtin_nontemporal_load(q + l + 64 * k);
+#pragma unroll
+    for (int k = 0; k < kDiagKL; ++k) acc += cur[k];
+  }
+  // the reduction is kept alive (never true for finite data summing to this)
+  if (acc.x + acc.y + acc.z + acc.w == -1.2345e-30f) sink[0] = acc.x;
+  (void)n4;
+}
+
+}  // namespace
+
+long long stream_read_bytes(long long bytes) {
+  const long long per_wave = static_cast<long long>(kDiagTile) * 16;
+  const long long waves = 4LL * device_cus();
+  const long long tiles = bytes / (per_wave * waves);
+  return tiles * per_wave * waves;
+}
+
+void launch_stream_read(const void* x, long long bytes, float* sink, hipStream_t s) {
+  const long long waves = 4LL * device_cus();
+  const long long tiles = bytes / (static_cast<long long>(kDiagTile) * 16 * waves);
+  if (tiles < 1) throw HipError("stream probe: buffer smaller than one tile per wave");
+  k_stream_read<<<static_cast<int>(waves), 64, 0, s>>>(static_cast<const f4*>(x), tiles, bytes / 16, sink);
+  ORION_LAUNCH_CHECK();
+}
+
+}  // namespace orion

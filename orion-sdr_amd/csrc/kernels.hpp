@@ -158,4 +158,9 @@ void launch_wbfm_ws(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedC
 void launch_wbfm_fused(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
                        hipStream_t s);
 
+int device_cus();
+// On-box bandwidth probe (k_diag.hip): a streaming read of the first
+// stream_read_bytes(bytes) bytes of x (16-B aligned) with the WBFM front's load shape.
+long long stream_read_bytes(long long bytes);
+void launch_stream_read(const void* x, long long bytes, float* sink, hipStream_t s);
 }  // namespace orion

@@ -28,7 +28,7 @@ __all__ = [
     "FmQuadratureDemod", "PmQuadratureDemod", "SsbProductDemod", "AmEnvelopeDemod",
     "CwEnvelopeDemod", "WbfmChain", "AgcRms", "AgcRmsIq", "AmDsbMod", "FmPhaseAccumMod", "SsbPhasingMod",
     "fir_lowpass_design", "kaiser_lowpass_taps",
-    "kaiser_transition_norm", "kaiser_num_taps", "lp_cascade_design", "lib_path", "OrionError",
+    "kaiser_transition_norm", "kaiser_num_taps", "lp_cascade_design", "lib_path", "OrionError", "diag_stream_read",
     "AudioToIqChain", "IqToIqChain", "IqToAudioChain", "Graph", "stream_shard", "STREAM_HALO",
 ]
 
@@ -110,6 +110,8 @@ def _load():
         "orion_kaiser_transition_norm": (f, [sz, f]),
         "orion_kaiser_num_taps": (sz, [f, f]),
         "orion_lp_cascade_design": (None, [f, f, fp]),
+        "orion_diag_stream_read_bytes": (sz, [sz]),
+        "orion_diag_stream_read": (i, [vp, sz, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -570,6 +572,14 @@ def lp_cascade_design(fs: float, fc: float) -> np.ndarray:
     o = np.zeros(5, np.float32)
     _L.orion_lp_cascade_design(fs, fc, _fptr(o))
     return o
+
+
+def diag_stream_read(x, stream: int = 0) -> int:
+    """On-box bandwidth probe (no reference counterpart): one streaming read of the
+    leading bytes of the device tensor x on `stream`; returns the bytes read."""
+    nb = _L.orion_diag_stream_read_bytes(x.numel() * x.element_size())
+    _check(_L.orion_diag_stream_read(C.c_void_p(x.data_ptr()), nb, C.c_void_p(stream)))
+    return int(nb)
 
 
 def device_count() -> int:

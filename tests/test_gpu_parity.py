@@ -696,3 +696,18 @@ def test_firiq_filter_aligned_in_place(gpu_lib, oracle, ntaps):
         full = oracle.fir_lowpass_iq(np.concatenate([x, np.zeros(d, np.complex64), z]), taps)
         assert nrmse(after, full[n + d:]) <= 1e-6, (ntaps, n)
     print(f"[parity] firiq filter_aligned in place ntaps={ntaps}: ok")
+
+
+@pytest.mark.gpu
+def test_diag_stream_read(gpu_lib):
+    """The bench's on-box read probe: reads a whole number of tiles of the buffer,
+    rejects a misaligned pointer, and leaves the data untouched."""
+    import torch
+
+    x = torch.arange(1 << 22, dtype=torch.float32, device="cuda")
+    nb = gpu_lib.diag_stream_read(x)
+    torch.cuda.synchronize()
+    assert 0 < nb <= x.numel() * 4 and nb % (16 * 64 * 8) == 0
+    assert torch.equal(x, torch.arange(1 << 22, dtype=torch.float32, device="cuda"))
+    with pytest.raises(gpu_lib.OrionError):
+        gpu_lib.diag_stream_read(x[1:])
