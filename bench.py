@@ -7,13 +7,15 @@ C2-sized channel (2^26 cf32 @ 10 Msps, its own tuning offset; BASELINE.json
 configs[1]). Channels are independent: no collective on the data path
 ("scaling": "weak"); the only collectives are the timing barrier / max.
 
-The roofline object prices the one kernel the chain runs (k_wbfm_seg2) with
+The roofline object prices the one kernel the chain runs (k_wbfm_seg4) with
 HIP events on the stream it is launched on (one pair around the K launches, so
 inter-launch gaps count against it): algorithmic bytes per launch
 (8 B cf32 in + 4 B f32 audio out per 8 inputs = 8.5 B per input sample, SURVEY
 §8d) / average kernel time, against the 8.0 TB/s HBM3E peak. The cpu_baseline
 is the scalar oracle ("port" of the reference Rust, 1 thread, the reference is
-single-threaded) timed on this host on a bounded prefix of the same input.
+single-threaded) timed on this host on a bounded prefix of the same input; the
+multi-channel configs time the oracle on min(channels, 16) host threads, one
+channel per thread, on a bounded prefix of that many channels.
 
 Other workloads (--config c3|c4|c5) are available for DESIGN.md tables; the
 driver's default line is c2.
@@ -143,6 +145,37 @@ def make_workload(cfg, rank, dev, n_override=None, world=1, shard="stream"):
     raise SystemExit(f"unknown --config {cfg}")
 
 
+def cpu_baseline_channels(x_dev, cfg, seconds_target, f_offs=None):
+    """Multi-channel configs: the scalar oracle on min(channels, 16) host threads
+    (ctypes releases the GIL; the oracle's own std::thread pool, one channel per
+    thread), on a bounded prefix of that many channels."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    thr = max(1, min(x_dev.shape[0], 16, os.cpu_count() or 1))
+    if cfg == "c3":
+        run, what = (lambda xh: O.decim_channels(xh, 10e6, 8, 190e3, 39370.0, thr)), "o_run_decim_channels"
+    elif cfg == "c4":
+        run, what = (lambda xh: O.wbfm_channels(xh, np.asarray(f_offs[:thr], np.float32), thr)), "o_run_wbfm_channels"
+    else:
+        run, what = (lambda xh: O.ssb_demod_channels(xh, 48e3, 1500.0, 2800.0, thr)), "o_run_ssb_demod_channels"
+    probe = 1 << 15
+    xh = x_dev[:thr, :probe].cpu().numpy()
+    t0 = time.perf_counter()
+    run(xh)
+    rate = probe / (time.perf_counter() - t0)  # samples per channel per second
+    n = int(min(x_dev.shape[1], max(probe, rate * seconds_target)))
+    n -= n % 8
+    xh = x_dev[:thr, :n].cpu().numpy()
+    t0 = time.perf_counter()
+    run(xh)
+    dt = time.perf_counter() - t0
+    return dict(value=round(thr * n / dt / 1e6, 4), unit="Msamples/s", cores=thr, kind="port",
+                sample=f"first {n} samples of channels 0..{thr - 1} of the rank-0 {cfg.upper()} input, "
+                       f"oracle/orion_oracle.c {what}, {thr} threads (one channel each), {os.uname().nodename}",
+                seconds=round(dt, 2))
+
+
 def cpu_baseline(x_dev, cfg, seconds_target, max_samples):
     """Scalar oracle ("port") on this host, 1 thread, bounded prefix of the input."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -268,6 +301,9 @@ def main():
             den = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
             cb["gpu_vs_cpu_nrmse"] = float(np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2)) / den)
             line["cpu_baseline"] = cb
+    elif rank == 0 and world == 1 and not args.no_cpu:
+        f_offs = [f for f, _ in channel_plan("c4", 0, 1)] if args.config == "c4" else None
+        line["cpu_baseline"] = cpu_baseline_channels(x, args.config, min(args.cpu_seconds, 10.0), f_offs)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
