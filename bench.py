@@ -147,32 +147,38 @@ def make_workload(cfg, rank, dev, n_override=None, world=1, shard="stream"):
 
 def cpu_baseline_channels(x_dev, cfg, seconds_target, f_offs=None):
     """Multi-channel configs: the scalar oracle on min(channels, 16) host threads
-    (ctypes releases the GIL; the oracle's own std::thread pool, one channel per
-    thread), on a bounded prefix of that many channels."""
+    (the oracle's own std::thread pool, channels split over the threads; ctypes
+    releases the GIL), over every channel of the step, on a prefix of each sized
+    to about `seconds_target` of CPU time (the whole step, repeated, when it is
+    shorter than that)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
-    thr = max(1, min(x_dev.shape[0], 16, os.cpu_count() or 1))
+    nch, n_all = x_dev.shape
+    thr = max(1, min(nch, 16, os.cpu_count() or 1))
     if cfg == "c3":
         run, what = (lambda xh: O.decim_channels(xh, 10e6, 8, 190e3, 39370.0, thr)), "o_run_decim_channels"
     elif cfg == "c4":
-        run, what = (lambda xh: O.wbfm_channels(xh, np.asarray(f_offs[:thr], np.float32), thr)), "o_run_wbfm_channels"
+        run, what = (lambda xh: O.wbfm_channels(xh, np.asarray(f_offs, np.float32), thr)), "o_run_wbfm_channels"
     else:
         run, what = (lambda xh: O.ssb_demod_channels(xh, 48e3, 1500.0, 2800.0, thr)), "o_run_ssb_demod_channels"
-    probe = 1 << 15
-    xh = x_dev[:thr, :probe].cpu().numpy()
+    probe = min(n_all, 1 << 14)
+    xh = x_dev[:, :probe].cpu().numpy()
     t0 = time.perf_counter()
     run(xh)
-    rate = probe / (time.perf_counter() - t0)  # samples per channel per second
-    n = int(min(x_dev.shape[1], max(probe, rate * seconds_target)))
+    rate = nch * probe / (time.perf_counter() - t0)  # samples per second over all threads
+    n = int(min(n_all, max(probe, rate * seconds_target / nch)))
     n -= n % 8
-    xh = x_dev[:thr, :n].cpu().numpy()
+    reps = max(1, int(rate * seconds_target / (nch * n))) if n == n_all else 1
+    xh = x_dev[:, :n].cpu().numpy()
     t0 = time.perf_counter()
-    run(xh)
+    for _ in range(reps):
+        run(xh)
     dt = time.perf_counter() - t0
-    return dict(value=round(thr * n / dt / 1e6, 4), unit="Msamples/s", cores=thr, kind="port",
-                sample=f"first {n} samples of channels 0..{thr - 1} of the rank-0 {cfg.upper()} input, "
-                       f"oracle/orion_oracle.c {what}, {thr} threads (one channel each), {os.uname().nodename}",
+    return dict(value=round(reps * nch * n / dt / 1e6, 4), unit="Msamples/s", cores=thr, kind="port",
+                sample=f"first {n} samples of all {nch} channels of the rank-0 {cfg.upper()} input"
+                       f"{f' (the whole step, {reps} calls)' if reps > 1 or n == n_all else ''}, oracle/orion_oracle.c "
+                       f"{what}, {thr} threads, {os.uname().nodename}",
                 seconds=round(dt, 2))
 
 
