@@ -1,4 +1,6 @@
 // k_scan.hip — chunked state-carry scan kernels (see scan.hpp) for gfx950.
+#include <cstdlib>
+
 #include "scan.hpp"
 
 namespace orion {
@@ -13,6 +15,9 @@ constexpr int PADN = CH + CH / 16 + 16;
 #endif
 #ifndef ORION_SP_WAVES
 #define ORION_SP_WAVES 1  // occupancy hint for k_lpdc_sp (experiments: 6)
+#endif
+#ifndef ORION_SP_MINW
+#define ORION_SP_MINW 4  // waves per SIMD k_lpdc_sp is compiled for at kSpC samples per lane (<= 128 VGPRs)
 #endif
 #ifndef ORION_SP_TAB2
 #define ORION_SP_TAB2 1  // SSB mixing phasor = (Swg tab[t]) tab[k NT]: one uniform table load per sample, not a per-lane one
@@ -426,10 +431,54 @@ __device__ __forceinline__ void dc_combine(double m1, double d1, double& m2, dou
   m2 = m2 * m1;
 }
 
-template <Pre PR>
-__global__ __launch_bounds__(NT, ORION_SP_WAVES) void k_lpdc_sp(const ScanArgs a, const double* __restrict__ mlp, int nch,
+// Staging of k_lpdc_sp (Ssb / AmAbs front ends) at SC samples per lane: every load
+// of the thread first, then the premap into the padded image (posS). The SSB mixing
+// phasor of sample e = t + k NT is (S_h tab[t]) tab[(k mod 16) NT], S_h the exact
+// phasor of the chunk's sample 4096 h (the table holds kScanCH phasors).
+template <int SC>
+__device__ __forceinline__ int posS(int e) { return e + e / SC; }
+template <Pre PR, int SC>
+__device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long base, int cnt, float* sb) {
+  static_assert(SC * NT <= 2 * kScanCH, "two phasor table spans cover the chunk");
+  const f2* __restrict__ x = static_cast<const f2*>(a.x) + ch * a.x_stride + base;
+  f2 St[2] = {f2{1.0f, 0.0f}, f2{1.0f, 0.0f}};
+  if constexpr (PR == Pre::Ssb) {
+#pragma unroll
+    for (int h = 0; h < (SC * NT + kScanCH - 1) / kScanCH; ++h)
+      St[h] = cmul(phasor_q64(static_cast<uint64_t>(a.k0 + base + 1 + h * kScanCH), a.step), a.tab[threadIdx.x]);
+  }
+  f2 v[SC];
+#pragma unroll
+  for (int k = 0; k < SC; ++k) {
+    const int e = threadIdx.x + k * NT;
+    v[k] = e < cnt ? x[e] : f2{0.0f, 0.0f};
+  }
+#pragma unroll
+  for (int k = 0; k < SC; ++k) {
+    const int e = threadIdx.x + k * NT;
+    const f2 z = v[k];
+    float o;
+    if constexpr (PR == Pre::Ssb) {
+      constexpr int KT = kScanCH / NT;
+      const f2 p = cmul(St[k / KT], a.tab[(k % KT) * NT]);
+      o = __builtin_fmaf(z.x, p.x, z.y * p.y);  // ssb.rs:37
+    } else {
+      o = __builtin_fmaf(a.c.k1, fabsf(z.x), a.c.k2 * fabsf(z.y));  // am.rs:238
+    }
+    sb[posS<SC>(e)] = o;
+  }
+}
+
+template <Pre PR, int SC>
+__global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void k_lpdc_sp(const ScanArgs a, const double* __restrict__ mlp, int nch,
                                                uint32_t* __restrict__ rec, uint32_t epoch) {
   constexpr int S = 4;
+  constexpr int C = SC, CH = SC * NT, PADN = CH + CH / SC + SC;
+  // matrices of the lane step A^C: (A^C)^(2^s) are kPwc + s (C = kScanC) or kPwc + 1 + s
+  // (C = 2 kScanC: the same powers shifted by one; s = 5 is then kM64); A^(64 C) per wave
+  static_assert(SC == kScanC || SC == 2 * kScanC, "lane run");
+  constexpr int kPw = ScanMatsLayout::kPwc + (SC == kScanC ? 0 : 1);
+  constexpr int kWv = SC == kScanC ? ScanMatsLayout::kM64 : ScanMatsLayout::kM128;
   __shared__ float sb[PADN];
   __shared__ double tot[4][S];
   __shared__ double dtot[4][2];
@@ -446,13 +495,13 @@ __global__ __launch_bounds__(NT, ORION_SP_WAVES) void k_lpdc_sp(const ScanArgs a
   const float* __restrict__ ci = a.carry_in + ch * kScanCarry;
   const RecLP4 lp{{a.c.b0, a.c.b1, a.c.b2, a.c.a1, a.c.a2}};
   const float r = a.c.r;
-  stage<PR>(a, ch, base, cnt, sb);
+  stage_sp<PR, SC>(a, ch, base, cnt, sb);
   __syncthreads();
 
   // ---- LP4: zero-state lane aggregates, block scan, exact re-run ----
   float xs[C];
 #pragma unroll
-  for (int i = 0; i < C; ++i) xs[i] = sb[pos(t * C + i)];
+  for (int i = 0; i < C; ++i) xs[i] = sb[posS<SC>(t * C + i)];
   float s0[S] = {0, 0, 0, 0};
 #if !(ORION_SP_ABL & 4)
 #pragma unroll
@@ -462,7 +511,7 @@ __global__ __launch_bounds__(NT, ORION_SP_WAVES) void k_lpdc_sp(const ScanArgs a
   double q[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) q[i] = s0[i];
-  wave_scan_inclusive<S>(q, mlp + ScanMatsLayout::kPwc * S * S, lane);
+  wave_scan_inclusive<S>(q, mlp + kPw * S * S, lane);
   if (lane == 63)
 #pragma unroll
     for (int i = 0; i < S; ++i) tot[wave][i] = q[i];
@@ -474,7 +523,7 @@ __global__ __launch_bounds__(NT, ORION_SP_WAVES) void k_lpdc_sp(const ScanArgs a
     double v[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) v[i] = tot[w][i];
-    matvec_acc<S>(mlp + ScanMatsLayout::kM64 * S * S, cw, v);
+    matvec_acc<S>(mlp + kWv * S * S, cw, v);
 #pragma unroll
     for (int i = 0; i < S; ++i) cw[i] = v[i];
   }
@@ -483,8 +532,8 @@ __global__ __launch_bounds__(NT, ORION_SP_WAVES) void k_lpdc_sp(const ScanArgs a
   double e[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) q[i] = s0[i];
-  if (lane == 0) matvec_acc<S>(mlp + ScanMatsLayout::kPwc * S * S, cw, q);  // pw[0] = A^C
-  wave_scan_inclusive<S>(q, mlp + ScanMatsLayout::kPwc * S * S, lane);
+  if (lane == 0) matvec_acc<S>(mlp + kPw * S * S, cw, q);  // pw[0] = A^C
+  wave_scan_inclusive<S>(q, mlp + kPw * S * S, lane);
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     const double o = __shfl_up(q[i], 1, 64);
@@ -498,11 +547,11 @@ __global__ __launch_bounds__(NT, ORION_SP_WAVES) void k_lpdc_sp(const ScanArgs a
     if (t * C + i < cnt) xs[i] = lp.step(ef, xs[i]);  // LP output x (f32, reference update)
   __syncthreads();  // every lane has read its sb inputs
 #pragma unroll
-  for (int i = 0; i < C; ++i) sb[pos(t * C + i)] = xs[i];
+  for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
   __syncthreads();
 
   // ---- DC blocker: zero-state lane pairs (r^k, y_k), block scan ----
-  const float xprev0 = t * C == 0 ? ci[4] : sb[pos(t * C - 1)];  // x before the lane's first sample
+  const float xprev0 = t * C == 0 ? ci[4] : sb[posS<SC>(t * C - 1)];  // x before the lane's first sample
   double m = 1.0, d = 0.0;
   {
     float xp = xprev0, y = 0.0f;
@@ -628,7 +677,7 @@ __global__ __launch_bounds__(NT, ORION_SP_WAVES) void k_lpdc_sp(const ScanArgs a
     float xl = 0.0f;
 #pragma unroll
     for (int i = 0; i < C; ++i)
-      if (i == il) xl = sb[pos(t * C + i)];
+      if (i == il) xl = sb[posS<SC>(t * C + i)];
     co[4] = xl;
     co[5] = y;
     co[6] = ci[6];
@@ -636,10 +685,10 @@ __global__ __launch_bounds__(NT, ORION_SP_WAVES) void k_lpdc_sp(const ScanArgs a
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < C; ++i) sb[pos(t * C + i)] = xs[i];
+  for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
   __syncthreads();
   float* yo = static_cast<float*>(a.y) + ch * a.y_stride + o0;
-  for (int e2 = warm + t; e2 < cnt; e2 += NT) yo[e2 - warm] = sb[pos(e2)];
+  for (int e2 = warm + t; e2 < cnt; e2 += NT) yo[e2 - warm] = sb[posS<SC>(e2)];
 }
 
 // SsbPhasingMod in one pass (modulate/ssb.rs:43-114): per chunk, the audio-NCO
@@ -776,14 +825,34 @@ long long lpdc_sp_chunks(long long n) {
   return n <= CH ? 1 : 1 + (n - CH + (CH - kSpWarm) - 1) / (CH - kSpWarm);
 }
 
+long long lpdc_sp_demod_chunks(long long n, int sc) {
+  const long long ch = static_cast<long long>(sc) * NT;
+  return n <= ch ? 1 : 1 + (n - ch + (ch - kSpWarm) - 1) / (ch - kSpWarm);
+}
+int lpdc_sp_lane_samples() {
+  static const int sc = [] {
+    const char* e = std::getenv("ORION_SP_C16");
+    return e && std::atoi(e) == 1 ? kScanC : kSpC;
+  }();
+  return sc;
+}
+
 void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, uint32_t* rec, uint32_t epoch,
                     hipStream_t s) {
   if (a.n <= 0 || nch <= 0) return;
-  const long long grid = lpdc_sp_chunks(a.n) * nch;
+  const int sc = lpdc_sp_lane_samples();
+  const long long grid = lpdc_sp_demod_chunks(a.n, sc) * nch;
   if (grid > (1LL << 31) - 1) throw HipError("single-pass scan grid too large");
-  if (pre == Pre::Ssb) k_lpdc_sp<Pre::Ssb><<<static_cast<int>(grid), NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
-  else if (pre == Pre::AmAbs) k_lpdc_sp<Pre::AmAbs><<<static_cast<int>(grid), NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
-  else throw std::invalid_argument("single-pass LpDc scan: unsupported front end");
+  const int g = static_cast<int>(grid);
+  if (pre == Pre::Ssb) {
+    if (sc == kSpC) k_lpdc_sp<Pre::Ssb, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    else k_lpdc_sp<Pre::Ssb, kScanC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+  } else if (pre == Pre::AmAbs) {
+    if (sc == kSpC) k_lpdc_sp<Pre::AmAbs, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    else k_lpdc_sp<Pre::AmAbs, kScanC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+  } else {
+    throw std::invalid_argument("single-pass LpDc scan: unsupported front end");
+  }
   ORION_LAUNCH_CHECK();
 }
 

@@ -46,7 +46,8 @@ struct ScanMatsLayout {
   static constexpr int kM64 = 6;    // A^(64C)
   static constexpr int kPch = 7;    // (A^CH)^(2^s), s = 0..7
   static constexpr int kLane = 15;  // A^(C*L), L = 0..63
-  static constexpr int kCount = 79;
+  static constexpr int kM128 = 79;  // A^(128C): the wave-to-wave step of k_lpdc_sp at 2C samples per lane
+  static constexpr int kCount = 80;
 };
 
 struct ScanCoef {
@@ -81,6 +82,13 @@ void launch_scan(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, hipSt
 // lpdc_sp_chunks(n) * nch * 8 u32 look-back records; epoch: this launch's tag.
 constexpr int kSpWarm = 256;
 long long lpdc_sp_chunks(long long n);
+// k_lpdc_sp's own geometry: kSpC samples per lane (2 kScanC: the wave scans and the
+// LP4 state folding cost per lane, not per sample, so longer lane runs amortise them),
+// chunks of kSpCH samples; ORION_SP_C16=1 runs the kScanC form (timing comparisons).
+constexpr int kSpC = 2 * kScanC;
+constexpr int kSpCH = kSpC * kScanNT;
+long long lpdc_sp_demod_chunks(long long n, int sc);
+int lpdc_sp_lane_samples();  // kSpC, or kScanC under ORION_SP_C16=1
 // SsbPhasingMod in one pass (k_ssb_mod_sp): valid when ||A_lp^kSpWarm|| is
 // negligible; mats_lp = the LP4 scan matrices; carry = [I 4][Q 4] floats.
 void launch_ssb_mod_sp(const float* x, f2* y, long long n, uint64_t k0, uint64_t step_aud, uint64_t step_rf,

@@ -46,6 +46,7 @@ class ScanStage {
       p = mat_mul(p, p, S);
     }
     put(ScanMatsLayout::kM64, mat_pow(ss.A, S, 64ull * kScanC));
+    put(ScanMatsLayout::kM128, mat_pow(ss.A, S, 128ull * kScanC));
     p = mat_pow(ss.A, S, kScanCH);
     for (int s = 0; s < 8; ++s) {
       put(ScanMatsLayout::kPch + s, p);
@@ -90,7 +91,7 @@ class ScanStage {
     a.carry_out = carry_[cur_ ^ 1].as<float>();
     a.c = c_;
     if (sp_ok_ && mode_ == 0) {
-      const size_t words = static_cast<size_t>(lpdc_sp_chunks(n)) * nch_ * 8;
+      const size_t words = static_cast<size_t>(lpdc_sp_demod_chunks(n, lpdc_sp_lane_samples())) * nch_ * 8;
       if (words * 4 > rec_buf_.size()) {
         rec_buf_.resize(words * 4);
         rec_buf_.zero(s);
