@@ -462,6 +462,8 @@ __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long ba
       constexpr int KT = kScanCH / NT;
       const f2 p = cmul(St[k / KT], a.tab[(k % KT) * NT]);
       o = __builtin_fmaf(z.x, p.x, z.y * p.y);  // ssb.rs:37
+    } else if constexpr (PR == Pre::AmSqrt) {
+      o = __builtin_fmaf(z.x, z.x, z.y * z.y);  // am.rs:204
     } else {
       o = __builtin_fmaf(a.c.k1, fabsf(z.x), a.c.k2 * fabsf(z.y));  // am.rs:238
     }
@@ -544,7 +546,10 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   for (int i = 0; i < S; ++i) ef[i] = static_cast<float>(e[i]);
 #pragma unroll
   for (int i = 0; i < C; ++i)
-    if (t * C + i < cnt) xs[i] = lp.step(ef, xs[i]);  // LP output x (f32, reference update)
+    if (t * C + i < cnt) {
+      xs[i] = lp.step(ef, xs[i]);  // LP output x (f32, reference update)
+      if constexpr (PR == Pre::AmSqrt) xs[i] = sqrtf(xs[i]);  // am.rs:54 process_mapped(.., f32::sqrt)
+    }
   __syncthreads();  // every lane has read its sb inputs
 #pragma unroll
   for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
@@ -689,6 +694,150 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   __syncthreads();
   float* yo = static_cast<float*>(a.y) + ch * a.y_stride + o0;
   for (int e2 = warm + t; e2 < cnt; e2 += NT) yo[e2 - warm] = sb[posS<SC>(e2)];
+}
+
+// ---- single-pass scan for recurrences that forget (k_scan_sp) ---------------------
+// LpCascade and the demodulators built on it (FM, PM, AM PowerSqrt) and the CW
+// one-pole, when the chunk transition A^CH is negligible (the host checks
+// ||A^kSpCH|| < 1e-10: whatever state enters chunk c-1 is gone by its end), so the
+// state entering chunk c is chunk c-1's zero-state end state. Every chunk publishes
+// that aggregate as soon as its zero-state pass and block scan are done, then reads
+// its predecessor's (chunk-major grid: the predecessor was dispatched earlier and
+// publishes before it waits, so no chain of waits forms). Against the three-kernel
+// scan this drops the carry pass and the second read of the input. kSpC samples per
+// lane as k_lpdc_sp. Records: 16 u32 per (channel, chunk), [0, 2S) the aggregate
+// (f64), 15 the flag (launch epoch).
+template <RecK RK, Pre PR, Post PO>
+__global__ __launch_bounds__(NT, 4) void k_scan_sp(const ScanArgs a, int nch, uint32_t* __restrict__ rec,
+                                                   uint32_t epoch) {
+  using R = typename RecSel<RK>::T;
+  constexpr int S = R::S;
+  constexpr int SC = kSpC, C = SC, CH = SC * NT, PADN = CH + CH / SC + SC;
+  constexpr int kPw = ScanMatsLayout::kPwc + 1;    // (A^C)^(2^s), C = 2 kScanC
+  constexpr int kWv = ScanMatsLayout::kM128;       // A^(64 C)
+  constexpr int KT = kScanCH / NT;                 // staging steps per oscillator-table span
+  __shared__ float sb[PADN];
+  __shared__ double tot[4][S];
+  __shared__ double cin_sh[S];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int ch = static_cast<int>(blockIdx.x % nch);
+  const int c = static_cast<int>(blockIdx.x / nch);
+  const long long base = static_cast<long long>(c) * CH;
+  const int cnt = static_cast<int>(min(static_cast<long long>(CH), a.n - base));
+  const int nchunk = static_cast<int>((a.n + CH - 1) / CH);
+  const bool last = c == nchunk - 1;
+  const float* __restrict__ ci = a.carry_in + ch * kScanCarry;
+  const R rr = RecSel<RK>::make(a.c);
+  f2 Sw[2] = {f2{1.0f, 0.0f}, f2{1.0f, 0.0f}};  // oscillator at the chunk's samples 0 and kScanCH
+  if constexpr (PR == Pre::Fm) {
+    if (a.translate) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) Sw[h] = phasor_q64(static_cast<uint64_t>(a.k0 + base + 1 + h * kScanCH), a.step);
+    }
+  }
+#pragma unroll 8
+  for (int k = 0; k < SC; ++k) {  // 8 loads in flight per batch: unrolled 32, the loads spill
+    const int e = t + k * NT;
+    const int h = k >= KT ? 1 : 0;
+    if (e < cnt) sb[posS<SC>(e)] = premap<PR>(a, ch, base + e, base + h * kScanCH, h ? Sw[1] : Sw[0]);
+  }
+  __syncthreads();
+
+  float xs[C];
+#pragma unroll
+  for (int i = 0; i < C; ++i) xs[i] = sb[posS<SC>(t * C + i)];
+  float s0[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) s0[i] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < C; ++i)
+    if (t * C + i < cnt) (void)rr.step(s0, xs[i]);
+  double q[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) q[i] = s0[i];
+  wave_scan_inclusive<S>(q, a.mats + kPw * S * S, lane);
+  if (lane == 63)
+#pragma unroll
+    for (int i = 0; i < S; ++i) tot[wave][i] = q[i];
+  __syncthreads();
+  if (t == 0) {
+    double agg[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) agg[i] = 0.0;
+    for (int w = 0; w < 4; ++w) {
+      double v[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) v[i] = tot[w][i];
+      matvec_acc<S>(a.mats + kWv * S * S, agg, v);
+#pragma unroll
+      for (int i = 0; i < S; ++i) agg[i] = v[i];
+    }
+    if (!last) {
+      uint32_t* my = rec + (static_cast<long long>(ch) * nchunk + c) * 16;
+#pragma unroll
+      for (int i = 0; i < S; ++i) sp_st64(my + 2 * i, agg[i]);
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the aggregate is visible before its flag
+      sp_st(my + 15, epoch);
+    }
+    if (c == 0) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) cin_sh[i] = static_cast<double>(ci[i]);
+    } else {
+      const uint32_t* pr = rec + (static_cast<long long>(ch) * nchunk + c - 1) * 16;
+      int it = 0;
+      while (sp_ld(pr + 15) != epoch && ++it < (1 << 22)) __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+      for (int i = 0; i < S; ++i) cin_sh[i] = sp_ld64(pr + 2 * i);
+    }
+  }
+  __syncthreads();
+  double cw[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) cw[i] = cin_sh[i];
+  for (int w = 0; w < wave; ++w) {
+    double v[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) v[i] = tot[w][i];
+    matvec_acc<S>(a.mats + kWv * S * S, cw, v);
+#pragma unroll
+    for (int i = 0; i < S; ++i) cw[i] = v[i];
+  }
+  // the wave's entering state folded into lane 0 and the wave re-scanned (k_lpdc_sp)
+#pragma unroll
+  for (int i = 0; i < S; ++i) q[i] = s0[i];
+  if (lane == 0) matvec_acc<S>(a.mats + kPw * S * S, cw, q);
+  wave_scan_inclusive<S>(q, a.mats + kPw * S * S, lane);
+  float ef[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const double o = __shfl_up(q[i], 1, 64);
+    ef[i] = static_cast<float>(lane == 0 ? cw[i] : o);
+  }
+#pragma unroll
+  for (int i = 0; i < C; ++i)
+    if (t * C + i < cnt) xs[i] = postmap<PO>(a, rr.step(ef, xs[i]));  // the reference's f32 update
+  if (last && t * C <= cnt - 1 && cnt - 1 < t * C + C) {  // carried state of the next call
+    float* co = a.carry_out + ch * kScanCarry;
+#pragma unroll
+    for (int i = 0; i < S; ++i) co[i] = ef[i];  // ef ran to the lane's last valid sample
+    for (int i = S; i < 6; ++i) co[i] = 0.0f;
+    if constexpr (PR == Pre::Fm || PR == Pre::Pm) {
+      const f2* x = static_cast<const f2*>(a.x) + ch * a.x_stride;
+      const int h = (cnt - 1) / kScanCH;
+      const f2 z = cin<PR>(a, x, a.n - 1, base + h * kScanCH, Sw[h]);
+      co[6] = z.x;
+      co[7] = z.y;
+    } else {
+      co[6] = ci[6];
+      co[7] = ci[7];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
+  __syncthreads();
+  float* y = static_cast<float*>(a.y) + ch * a.y_stride + base;
+  for (int e2 = t; e2 < cnt; e2 += NT) y[e2] = sb[posS<SC>(e2)];
 }
 
 // SsbPhasingMod in one pass (modulate/ssb.rs:43-114): per chunk, the audio-NCO
@@ -850,10 +999,42 @@ void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, 
   } else if (pre == Pre::AmAbs) {
     if (sc == kSpC) k_lpdc_sp<Pre::AmAbs, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
     else k_lpdc_sp<Pre::AmAbs, kScanC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+  } else if (pre == Pre::AmSqrt) {
+    if (sc == kSpC) k_lpdc_sp<Pre::AmSqrt, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    else k_lpdc_sp<Pre::AmSqrt, kScanC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else {
     throw std::invalid_argument("single-pass LpDc scan: unsupported front end");
   }
   ORION_LAUNCH_CHECK();
+}
+
+long long scan_sp_chunks(long long n) { return (n + kSpCH - 1) / kSpCH; }
+
+bool scan_sp_supported(RecK rec, Pre pre, Post post) {
+  return (rec == RecK::LP4 && post == Post::Id && (pre == Pre::Real || pre == Pre::Fm || pre == Pre::Pm)) ||
+         (rec == RecK::LP4 && pre == Pre::AmSqrt && post == Post::Sqrt) ||
+         (rec == RecK::ONEPOLE && pre == Pre::Cw && post == Post::Gain);
+}
+
+void launch_scan_sp(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, uint32_t* recs, uint32_t epoch,
+                    hipStream_t s) {
+  if (a.n <= 0 || nch <= 0) return;
+  const long long grid = scan_sp_chunks(a.n) * nch;
+  if (grid > (1LL << 31) - 1) throw HipError("single-pass scan grid too large");
+  const int g = static_cast<int>(grid);
+#define ORION_SP(RK, PR, PO)                                                                         \
+  if (rec == RecK::RK && pre == Pre::PR && post == Post::PO) {                                       \
+    k_scan_sp<RecK::RK, Pre::PR, Post::PO><<<g, NT, 0, s>>>(a, nch, recs, epoch);                    \
+    ORION_LAUNCH_CHECK();                                                                            \
+    return;                                                                                          \
+  }
+  ORION_SP(LP4, Real, Id)
+  ORION_SP(LP4, Fm, Id)
+  ORION_SP(LP4, Pm, Id)
+  ORION_SP(LP4, AmSqrt, Sqrt)
+  ORION_SP(ONEPOLE, Cw, Gain)
+#undef ORION_SP
+  throw std::invalid_argument("single-pass scan: unsupported combination");
 }
 
 void launch_scan(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, hipStream_t s) {

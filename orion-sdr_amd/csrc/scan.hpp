@@ -97,5 +97,13 @@ void launch_ssb_mod_sp(const float* x, f2* y, long long n, uint64_t k0, uint64_t
 void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, uint32_t* rec, uint32_t epoch,
                     hipStream_t s);
 int scan_state_dim(RecK rec);
+// Single-pass scan (k_scan_sp) for LpCascade / FM / PM / AM PowerSqrt / CW when the
+// recurrence forgets its state within one kSpCH-sample chunk (the host checks
+// ||A^kSpCH|| < 1e-10): chunk c starts from chunk c-1's zero-state end state.
+// recs: scan_sp_chunks(n) * nch * 16 u32 records; epoch: this launch's tag.
+bool scan_sp_supported(RecK rec, Pre pre, Post post);
+long long scan_sp_chunks(long long n);
+void launch_scan_sp(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, uint32_t* recs, uint32_t epoch,
+                    hipStream_t s);
 
 }  // namespace orion

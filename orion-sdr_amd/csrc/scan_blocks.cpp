@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "scan.hpp"
@@ -21,7 +22,15 @@ class ScanStage {
     // LpDcCascade after an SSB / AM-abs front end: single pass when the LP4
     // forgets its state within the kSpWarm-sample warm-up (SsbProductDemod at
     // 48 kHz: ||A^256|| ~ 1e-20)
-    if (rec == RecK::LPDC && (pre == Pre::Ssb || pre == Pre::AmAbs)) {
+    // LpCascade-type stages that forget within one kSpCH chunk: single pass
+    if (scan_sp_supported(rec, pre, post)) {
+      const auto m = mat_pow(ss.A, ss.S, kSpCH);
+      double fro = 0.0;
+      for (double v : m) fro += v * v;
+      const char* e = std::getenv("ORION_SCAN_3K");  // timing comparisons: keep the three-kernel scan
+      sp1_ok_ = std::sqrt(fro) < 1e-10 && !(e && std::atoi(e) == 1);
+    }
+    if (rec == RecK::LPDC && (pre == Pre::Ssb || pre == Pre::AmAbs || pre == Pre::AmSqrt)) {
       const StateSpace lp = lp_cascade_ss(BiquadCoeffs{c.b0, c.b1, c.b2, c.a1, c.a2});
       const auto m = mat_pow(lp.A, 4, kSpWarm);
       double fro = 0.0;
@@ -57,6 +66,7 @@ class ScanStage {
   }
   // 0 auto (single pass where valid), 1 force the three-kernel scan (tests)
   void set_mode(int m) { mode_ = m; }
+  bool lpdc_single_pass() const { return sp_ok_; }
   void set_osc(const Oscillator& o) {
     step_ = o.step_q64;
     const auto t = phasor_table(o.theta, kScanCH);
@@ -90,8 +100,9 @@ class ScanStage {
     a.carry_in = carry_[cur_].as<float>();
     a.carry_out = carry_[cur_ ^ 1].as<float>();
     a.c = c_;
-    if (sp_ok_ && mode_ == 0) {
-      const size_t words = static_cast<size_t>(lpdc_sp_demod_chunks(n, lpdc_sp_lane_samples())) * nch_ * 8;
+    if ((sp_ok_ || sp1_ok_) && mode_ == 0) {
+      const size_t words = sp1_ok_ ? static_cast<size_t>(scan_sp_chunks(n)) * nch_ * 16
+                                   : static_cast<size_t>(lpdc_sp_demod_chunks(n, lpdc_sp_lane_samples())) * nch_ * 8;
       if (words * 4 > rec_buf_.size()) {
         rec_buf_.resize(words * 4);
         rec_buf_.zero(s);
@@ -101,7 +112,8 @@ class ScanStage {
         rec_buf_.zero(s);
         epoch_ = 1;
       }
-      launch_lpdc_sp(pre_, a, mats_lp_.as<double>(), nch_, rec_buf_.as<uint32_t>(), epoch_, s);
+      if (sp1_ok_) launch_scan_sp(rec_, pre_, post_, a, nch_, rec_buf_.as<uint32_t>(), epoch_, s);
+      else launch_lpdc_sp(pre_, a, mats_lp_.as<double>(), nch_, rec_buf_.as<uint32_t>(), epoch_, s);
     } else {
       launch_scan(rec_, pre_, post_, a, nch_, s);
     }
@@ -118,7 +130,8 @@ class ScanStage {
   uint64_t step_ = 0;
   DevBuf mats_, tab_, carry_[2], ws_, mats_lp_, rec_buf_;
   int cur_ = 0;
-  bool sp_ok_ = false;
+  bool sp_ok_ = false;   // k_lpdc_sp (LpDcCascade after SSB / AM-abs)
+  bool sp1_ok_ = false;  // k_scan_sp (stages that forget within one chunk)
   int mode_ = 0;
   uint32_t epoch_ = 0;
 };
@@ -197,6 +210,10 @@ class AmBlock final : public ScanBlock {
     lp_ = std::make_unique<ScanStage>(RecK::LP4, Pre::AmSqrt, Post::Sqrt, lp_cascade_ss(d_.bq), c, 1);
     dc_ = std::make_unique<ScanStage>(RecK::DC, Pre::Real, Post::Id, dc_ss(d_.r), c, 1);
     lpdc_ = std::make_unique<ScanStage>(RecK::LPDC, Pre::AmAbs, Post::Id, lpdc_ss(d_), c, 1);
+    // PowerSqrt in one pass (k_lpdc_sp with the sqrt between the LP4 and the DC
+    // blocker) when the LP4 forgets within the warm-up; otherwise the two scans
+    sq_ = std::make_unique<ScanStage>(RecK::LPDC, Pre::AmSqrt, Post::Id, lpdc_ss(d_), c, 1);
+    if (!sq_->lpdc_single_pass()) sq_.reset();
     reset_state();
   }
   void set_abs(float k1, float k2) {
@@ -215,6 +232,11 @@ class AmBlock final : public ScanBlock {
                  static_cast<long long>(k0_), s);
       return;
     }
+    if (sq_) {
+      sq_->run(in, static_cast<long long>(stride), static_cast<long long>(n), out, static_cast<long long>(out_stride),
+               static_cast<long long>(k0_), s);
+      return;
+    }
     tmp_.resize(n * sizeof(float) + 16);
     lp_->run(in, static_cast<long long>(stride), static_cast<long long>(n), tmp_.as<void>(), static_cast<long long>(n),
              static_cast<long long>(k0_), s);
@@ -225,12 +247,13 @@ class AmBlock final : public ScanBlock {
     lp_->set_carry(carry_zero());
     dc_->set_carry(carry_zero());
     lpdc_->set_carry(carry_zero());
+    if (sq_) sq_->set_carry(carry_zero());
   }
 
  private:
   LpDcCoeffs d_;
   bool abs_ = false;
-  std::unique_ptr<ScanStage> lp_, dc_, lpdc_;
+  std::unique_ptr<ScanStage> lp_, dc_, lpdc_, sq_;
   DevBuf tmp_;
 };
 

@@ -196,6 +196,42 @@ def test_pm_ssb_am_cw(gpu_lib, oracle):
     report("ssb batch nrmse", nrmse(got, oracle.ssb_demod_channels(x, FS, 1500.0, 2800.0, 8)), 1e-4)
 
 
+def test_single_pass_scan_geometry(gpu_lib, oracle):
+    """Single-pass scan (k_scan_sp: LpCascade, FM, PM, AM PowerSqrt, CW; chunk c starts
+    from chunk c-1's published zero-state end state): one chunk (8192), one sample past
+    it, several chunks plus a ragged tail, and ragged streamed calls carrying the state."""
+    a = real_tone(FS, 1000.0, 120_000, 0.5)
+    iq = oracle.add_awgn(oracle.fm_mod(a, FS, 2500.0), 1e-3, 11)
+    xr = RNG.standard_normal(120_000).astype(np.float32)
+    cases = [
+        ("lp_cascade 1.25M/13.5k", lambda: gpu_lib.LpCascade(1.25e6, 13.5e3), xr,
+         lambda v: oracle.lp_cascade(v, 1.25e6, 13.5e3), None),
+        ("fm", lambda: gpu_lib.FmQuadratureDemod(FS, 2500.0, 5000.0), iq,
+         lambda v: oracle.fm_demod(v, FS, 2500.0, 5000.0), 1e-5),
+        ("pm", lambda: gpu_lib.PmQuadratureDemod(FS, 0.9, 5000.0), iq,
+         lambda v: oracle.pm_demod(v, FS, 0.9, 5000.0), 1e-5),
+        ("am sqrt", lambda: gpu_lib.AmEnvelopeDemod(FS, 5000.0), iq,
+         lambda v: oracle.am_demod(v, FS, 5000.0), 1e-5),
+        ("cw", lambda: gpu_lib.CwEnvelopeDemod(FS, 700.0, 300.0), iq,
+         lambda v: oracle.cw_demod(v, FS, 700.0, 300.0), 1e-5),
+    ]
+    for name, mk, x, ref_of, tol in cases:
+        ref = ref_of(x)
+        t = floor_tol(tol if tol is not None else 1e-6, ref_of, x)
+        for n in (8192, 8193, 3 * 8192 + 5):
+            report(f"{name} single-pass n={n} nrmse", nrmse(mk().process(x[:n]), ref[:n]), t)
+        # streamed: also no worse than the three-kernel scan on the same calls (both carry
+        # the f32 state across calls, where the f32 rounding of the carried state differs
+        # from the reference's by its own sensitivity)
+        os.environ["ORION_SCAN_3K"] = "1"
+        try:
+            e3 = nrmse(stream(mk(), x, 10007), ref)
+        finally:
+            del os.environ["ORION_SCAN_3K"]
+        report(f"{name} three-kernel streamed 10007 nrmse", e3, max(t, e3))
+        report(f"{name} single-pass streamed 10007 nrmse", nrmse(stream(mk(), x, 10007), ref), max(t, 1.25 * e3))
+
+
 def test_single_pass_lpdc_geometry(gpu_lib, oracle):
     """Single-pass LpDcCascade (SSB, AM AbsApprox): chunk-boundary lengths
     (4096 = one chunk, 4097, 4096 + 3840 + 1), calls of ragged length carrying
@@ -203,7 +239,7 @@ def test_single_pass_lpdc_geometry(gpu_lib, oracle):
     a = real_tone(FS, 1200.0, 200_000, 0.4)
     iq = oracle.add_awgn(oracle.ssb_mod(a, FS, 2800.0, 1500.0), 1e-3, 7)
     ref = oracle.ssb_demod(iq, FS, 1500.0, 2800.0)
-    for n in (4096, 4097, 4096 + 3840 + 1, 4096 + 3 * 3840):
+    for n in (4096, 4097, 4096 + 3840 + 1, 4096 + 3 * 3840, 8192, 8193, 8192 + 7936 + 1, 8192 + 3 * 7936):
         report(f"ssb single-pass n={n} nrmse", nrmse(gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0).process(iq[:n]),
                                                      ref[:n]), 1e-4)
     got = stream(gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0), iq, 7937)
