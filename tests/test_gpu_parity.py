@@ -126,6 +126,11 @@ def test_fir_lowpass(gpu_lib, oracle):
         x = RNG.standard_normal(200_000).astype(np.float32)
         got = stream(gpu_lib.FirLowpass(*args), x, 77_777)
         report(f"fir {len(oracle.fir_lowpass_taps(*args))} taps nrmse", nrmse(got, oracle.fir_lowpass(x, *args)), 1e-6)
+    # k_fir_real8 tile geometry (4096 outputs per tile as two 2048-output halves)
+    x = RNG.standard_normal(3 * 4096 + 77).astype(np.float32)
+    ref = oracle.fir_lowpass(x, 1.25e6, 15e3, 10e3)
+    for n in (5, 2047, 2049, 4096, 4097, 3 * 4096 + 77):
+        report(f"fir 125 taps n={n} nrmse", nrmse(gpu_lib.FirLowpass(1.25e6, 15e3, 10e3).process(x[:n]), ref[:n]), 1e-6)
 
 
 def test_fir_lowpass_iq(gpu_lib, oracle):
