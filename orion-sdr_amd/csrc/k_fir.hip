@@ -492,6 +492,88 @@ __global__ __launch_bounds__(NT) void k_fir_real(const float* __restrict__ x, lo
   }
 }
 
+// Real FIR with sixteen outputs per lane (4096 per workgroup tile) as eight packed
+// pairs: the staged image holds P[p] = (x[org + p], x[org + 2048 + p]), so one
+// v_pk_fma_f32 advances output j of the tile's first half and output j + 2048 of
+// its second with the same tap, and the inner loop is k_fir_iq8's (24-sample
+// window, 12 ds_read_b128 per 16-tap block for 128 packed FMAs, padded image).
+// Two outputs per lane (k_fir_real) stay behind ORION_FIR_REAL2=1.
+template <int KP>
+__global__ __launch_bounds__(NT) void k_fir_real8(const float* __restrict__ x, long long n,
+                                                  const float* __restrict__ hist, int hist_len,
+                                                  float* __restrict__ y, const Taps256 g) {
+  constexpr int TH = 8 * NT, TT = 2 * TH;  // 2048 outputs per half, 4096 per tile
+  constexpr int W = TH + KP + 2, PER = (W + NT - 1) / NT;
+  constexpr int WP = W + 2 * (W / 8) + 2;
+  static_assert(KP % 16 == 0, "taps padded to 16");
+  __shared__ __attribute__((aligned(16))) f2 L[WP];
+  auto pidx = [](int p) { return p + 2 * (p >> 3); };
+  auto ld = [&](long long P) {
+    float v = 0.0f;
+    if (P >= 0) v = P < n ? x[P] : 0.0f;
+    else if (P >= -hist_len) v = hist[hist_len + P];
+    return v;
+  };
+  const int t = threadIdx.x;
+  for (long long J = static_cast<long long>(blockIdx.x) * TT; J < n; J += static_cast<long long>(gridDim.x) * TT) {
+    const long long org = J - KP;  // staged p <-> elements org + p (first half), org + TH + p (second)
+    if (org >= 0 && org + TH + W <= n) {  // interior: every load issued before any is used
+      float v0[PER], v1[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int p = t + k * NT;
+        v0[k] = p < W ? x[org + p] : 0.0f;
+        v1[k] = p < W ? x[org + TH + p] : 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int p = t + k * NT;
+        if (p < W) L[pidx(p)] = f2{v0[k], v1[k]};
+      }
+    } else {
+      for (int p = t; p < W; p += NT) L[pidx(p)] = f2{ld(org + p), ld(org + TH + p)};
+    }
+    __syncthreads();
+    f2 acc[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = f2{0.0f, 0.0f};
+#pragma unroll 1
+    for (int kb = 0; kb < KP / 16; ++kb) {
+      const int pb = 8 * t + KP - 16 * kb - 16;  // as k_fir_iq8 (off = 0)
+      f2 w[24];
+#pragma unroll
+      for (int h = 0; h < 12; ++h) {
+        const f4 v = *reinterpret_cast<const f4*>(L + pidx(pb + 2 * h));
+        w[2 * h] = f2{v.x, v.y};
+        w[2 * h + 1] = f2{v.z, v.w};
+      }
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const f2 tap = splat2(g.g[16 * kb + kk]);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc[r] = fma2(tap, w[16 + r - kk], acc[r]);
+      }
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const long long j0 = J + half * TH + 8 * t;
+      float o[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) o[r] = half ? acc[r].y : acc[r].x;
+      if (j0 + 8 <= n && (reinterpret_cast<uintptr_t>(y + j0) & 15) == 0) {
+        f4* yo = reinterpret_cast<f4*>(y + j0);
+        yo[0] = f4{o[0], o[1], o[2], o[3]};
+        yo[1] = f4{o[4], o[5], o[6], o[7]};
+      } else {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if (j0 + r < n) y[j0 + r] = o[r];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(NT) void k_fir_real_generic(const float* __restrict__ x, long long n,
                                                          const float* __restrict__ hist,
                                                          int hist_len, float* __restrict__ y,
@@ -813,6 +895,19 @@ void launch_decim(const f2* x, long long n, const f2* hist, int hist_len, f2* ou
 void launch_fir_real(const float* x, long long n, const float* hist, int hist_len, float* y, int K,
                      const Taps256& g, const float* g_dev, hipStream_t s) {
   if (n <= 0) return;
+  static const bool two = [] {
+    const char* e = std::getenv("ORION_FIR_REAL2");  // timing comparisons: two outputs per lane
+    return e && std::atoi(e) == 1;
+  }();
+  if (!two && K <= 256 && hist_len >= K) {
+    const int g16 = static_cast<int>(std::min<long long>(kMaxGrid, (n + 16 * NT - 1) / (16 * NT)));
+    if (K <= 64 && hist_len >= 64) k_fir_real8<64><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g);
+    else if (K <= 128 && hist_len >= 128) k_fir_real8<128><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g);
+    else if (K <= 256 && hist_len >= 256) k_fir_real8<256><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g);
+    else k_fir_real_generic<<<grid_for(n, NT), NT, 0, s>>>(x, n, hist, hist_len, y, K, g_dev);
+    ORION_LAUNCH_CHECK();
+    return;
+  }
   const int grid = grid_for(n, 512);
   if (K <= 64 && hist_len >= 64) k_fir_real<64><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, g);
   else if (K <= 128 && hist_len >= 128) k_fir_real<128><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, g);
