@@ -440,6 +440,18 @@ __device__ __forceinline__ int posS(int e) { return e + e / SC; }
 template <Pre PR, int SC>
 __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long base, int cnt, float* sb) {
   static_assert(SC * NT <= 2 * kScanCH, "two phasor table spans cover the chunk");
+  if constexpr (PR == Pre::Real) {  // DcBlocker: f32 input
+    const float* __restrict__ xr = static_cast<const float*>(a.x) + ch * a.x_stride + base;
+    float v[SC];
+#pragma unroll
+    for (int k = 0; k < SC; ++k) {
+      const int e = threadIdx.x + k * NT;
+      v[k] = e < cnt ? xr[e] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < SC; ++k) sb[posS<SC>(threadIdx.x + k * NT)] = v[k];
+    return;
+  }
   const f2* __restrict__ x = static_cast<const f2*>(a.x) + ch * a.x_stride + base;
   f2 St[2] = {f2{1.0f, 0.0f}, f2{1.0f, 0.0f}};
   if constexpr (PR == Pre::Ssb) {
@@ -488,11 +500,15 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int ch = static_cast<int>(blockIdx.x % nch);
   const int c = static_cast<int>(blockIdx.x / nch);
-  const int warm = c == 0 ? 0 : kSpWarm;
-  const long long o0 = c == 0 ? 0 : CH + static_cast<long long>(c - 1) * (CH - kSpWarm);
+  // PR == Real: the DcBlocker alone (no LP4, no warm-up, chunks abut); its state
+  // (x1, y1) sits at carry [0, 1] (RecDC) instead of [4, 5] (RecLpDc)
+  constexpr bool LP = PR != Pre::Real;
+  constexpr int WARM = LP ? kSpWarm : 0, DX = LP ? 4 : 0, DY = DX + 1;
+  const int warm = c == 0 ? 0 : WARM;
+  const long long o0 = c == 0 ? 0 : CH + static_cast<long long>(c - 1) * (CH - WARM);
   const long long base = o0 - warm;                          // first staged sample
   const int cnt = static_cast<int>(min(static_cast<long long>(CH), a.n - base));  // staged samples
-  const int nchunk = a.n <= CH ? 1 : 1 + static_cast<int>((a.n - CH + (CH - kSpWarm) - 1) / (CH - kSpWarm));
+  const int nchunk = a.n <= CH ? 1 : 1 + static_cast<int>((a.n - CH + (CH - WARM) - 1) / (CH - WARM));
   const bool last = c == nchunk - 1;
   const float* __restrict__ ci = a.carry_in + ch * kScanCarry;
   const RecLP4 lp{{a.c.b0, a.c.b1, a.c.b2, a.c.a1, a.c.a2}};
@@ -504,6 +520,8 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   float xs[C];
 #pragma unroll
   for (int i = 0; i < C; ++i) xs[i] = sb[posS<SC>(t * C + i)];
+  float ef[S] = {0, 0, 0, 0};
+  if constexpr (LP) {
   float s0[S] = {0, 0, 0, 0};
 #if !(ORION_SP_ABL & 4)
 #pragma unroll
@@ -541,7 +559,6 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
     const double o = __shfl_up(q[i], 1, 64);
     e[i] = lane == 0 ? cw[i] : o;
   }
-  float ef[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) ef[i] = static_cast<float>(e[i]);
 #pragma unroll
@@ -554,9 +571,15 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
 #pragma unroll
   for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
   __syncthreads();
+  }  // LP
 
   // ---- DC blocker: zero-state lane pairs (r^k, y_k), block scan ----
-  const float xprev0 = t * C == 0 ? ci[4] : sb[posS<SC>(t * C - 1)];  // x before the lane's first sample
+  // x before the lane's first sample: lane 0 of chunk 0 takes the carried x1; lane 0 of a
+  // later chunk the sample before the chunk (with the LP4 that sample's position is a
+  // warm-up sample, which the DC pass skips)
+  float xprev0 = t * C == 0 ? ci[DX] : sb[posS<SC>(t * C - 1)];
+  if constexpr (!LP)
+    if (t == 0 && c > 0) xprev0 = static_cast<const float*>(a.x)[ch * a.x_stride + base - 1];
   double m = 1.0, d = 0.0;
   {
     float xp = xprev0, y = 0.0f;
@@ -624,7 +647,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
         v = closes ? sp_ld64(pr + 4) : sp_ld64(pr);
         mk = closes ? 1.0 : sp_ld64(pr + 2);
       } else {
-        v = static_cast<double>(ci[5]);  // the carried y1
+        v = static_cast<double>(ci[DY]);  // the carried y1
       }
       const unsigned long long bal = __ballot(closes);
       const int first = bal ? __builtin_ctzll(bal) : 64;
@@ -676,15 +699,16 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   }
   if (last && t * C <= cnt - 1 && cnt - 1 < t * C + C) {  // carried state of the next call
     float* co = a.carry_out + ch * kScanCarry;
+    if constexpr (LP)
 #pragma unroll
-    for (int i = 0; i < S; ++i) co[i] = ef[i];  // ef ran to the lane's last valid sample
+      for (int i = 0; i < S; ++i) co[i] = ef[i];  // ef ran to the lane's last valid sample
     const int il = cnt - 1 - t * C;
     float xl = 0.0f;
 #pragma unroll
     for (int i = 0; i < C; ++i)
       if (i == il) xl = sb[posS<SC>(t * C + i)];
-    co[4] = xl;
-    co[5] = y;
+    co[DX] = xl;
+    co[DY] = y;
     co[6] = ci[6];
     co[7] = ci[7];
   }
@@ -974,9 +998,9 @@ long long lpdc_sp_chunks(long long n) {
   return n <= CH ? 1 : 1 + (n - CH + (CH - kSpWarm) - 1) / (CH - kSpWarm);
 }
 
-long long lpdc_sp_demod_chunks(long long n, int sc) {
+long long lpdc_sp_demod_chunks(long long n, int sc, int warm) {
   const long long ch = static_cast<long long>(sc) * NT;
-  return n <= ch ? 1 : 1 + (n - ch + (ch - kSpWarm) - 1) / (ch - kSpWarm);
+  return n <= ch ? 1 : 1 + (n - ch + (ch - warm) - 1) / (ch - warm);
 }
 int lpdc_sp_lane_samples() {
   static const int sc = [] {
@@ -990,7 +1014,7 @@ void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, 
                     hipStream_t s) {
   if (a.n <= 0 || nch <= 0) return;
   const int sc = lpdc_sp_lane_samples();
-  const long long grid = lpdc_sp_demod_chunks(a.n, sc) * nch;
+  const long long grid = lpdc_sp_demod_chunks(a.n, sc, pre == Pre::Real ? 0 : kSpWarm) * nch;
   if (grid > (1LL << 31) - 1) throw HipError("single-pass scan grid too large");
   const int g = static_cast<int>(grid);
   if (pre == Pre::Ssb) {
@@ -999,6 +1023,9 @@ void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, 
   } else if (pre == Pre::AmAbs) {
     if (sc == kSpC) k_lpdc_sp<Pre::AmAbs, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
     else k_lpdc_sp<Pre::AmAbs, kScanC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+  } else if (pre == Pre::Real) {
+    if (sc == kSpC) k_lpdc_sp<Pre::Real, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    else k_lpdc_sp<Pre::Real, kScanC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else if (pre == Pre::AmSqrt) {
     if (sc == kSpC) k_lpdc_sp<Pre::AmSqrt, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
     else k_lpdc_sp<Pre::AmSqrt, kScanC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);

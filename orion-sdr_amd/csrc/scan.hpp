@@ -87,7 +87,7 @@ long long lpdc_sp_chunks(long long n);
 // chunks of kSpCH samples; ORION_SP_C16=1 runs the kScanC form (timing comparisons).
 constexpr int kSpC = 2 * kScanC;
 constexpr int kSpCH = kSpC * kScanNT;
-long long lpdc_sp_demod_chunks(long long n, int sc);
+long long lpdc_sp_demod_chunks(long long n, int sc, int warm);  // warm: kSpWarm, or 0 for the DcBlocker alone
 int lpdc_sp_lane_samples();  // kSpC, or kScanC under ORION_SP_C16=1
 // SsbPhasingMod in one pass (k_ssb_mod_sp): valid when ||A_lp^kSpWarm|| is
 // negligible; mats_lp = the LP4 scan matrices; carry = [I 4][Q 4] floats.

@@ -30,6 +30,12 @@ class ScanStage {
       const char* e = std::getenv("ORION_SCAN_3K");  // timing comparisons: keep the three-kernel scan
       sp1_ok_ = std::sqrt(fro) < 1e-10 && !(e && std::atoi(e) == 1);
     }
+    // DcBlocker alone: k_lpdc_sp's DC look-back without the LP4 (pole ~1: no chunk forgets)
+    if (rec == RecK::DC && pre == Pre::Real && post == Post::Id) {
+      const char* e = std::getenv("ORION_SCAN_3K");
+      sp_ok_ = !(e && std::atoi(e) == 1);
+      dc_only_ = true;
+    }
     if (rec == RecK::LPDC && (pre == Pre::Ssb || pre == Pre::AmAbs || pre == Pre::AmSqrt)) {
       const StateSpace lp = lp_cascade_ss(BiquadCoeffs{c.b0, c.b1, c.b2, c.a1, c.a2});
       const auto m = mat_pow(lp.A, 4, kSpWarm);
@@ -102,7 +108,8 @@ class ScanStage {
     a.c = c_;
     if ((sp_ok_ || sp1_ok_) && mode_ == 0) {
       const size_t words = sp1_ok_ ? static_cast<size_t>(scan_sp_chunks(n)) * nch_ * 16
-                                   : static_cast<size_t>(lpdc_sp_demod_chunks(n, lpdc_sp_lane_samples())) * nch_ * 8;
+                                   : static_cast<size_t>(lpdc_sp_demod_chunks(n, lpdc_sp_lane_samples(),
+                                                                              dc_only_ ? 0 : kSpWarm)) * nch_ * 8;
       if (words * 4 > rec_buf_.size()) {
         rec_buf_.resize(words * 4);
         rec_buf_.zero(s);
@@ -132,6 +139,7 @@ class ScanStage {
   int cur_ = 0;
   bool sp_ok_ = false;   // k_lpdc_sp (LpDcCascade after SSB / AM-abs)
   bool sp1_ok_ = false;  // k_scan_sp (stages that forget within one chunk)
+  bool dc_only_ = false;  // k_lpdc_sp<Real>: the DcBlocker alone
   int mode_ = 0;
   uint32_t epoch_ = 0;
 };

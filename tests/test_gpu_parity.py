@@ -249,6 +249,14 @@ def test_single_pass_lpdc_geometry(gpu_lib, oracle):
                                                      ref[:n]), 1e-4)
     got = stream(gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0), iq, 7937)
     report("ssb single-pass streamed 7937 nrmse", nrmse(got, ref), 1e-4)
+    # the DcBlocker alone (k_lpdc_sp<Real>: DC look-back, no LP4, abutting 8192-sample chunks)
+    xd = (RNG.standard_normal(60_000) + 0.3).astype(np.float32)
+    dref = lambda v: oracle.dc_blocker(v, FS, 2.0)  # noqa: E731
+    td = floor_tol(1e-6, dref, xd)
+    rd = dref(xd)
+    for n in (8192, 8193, 3 * 8192 + 5):
+        report(f"dc_blocker single-pass n={n} nrmse", nrmse(gpu_lib.DcBlocker(FS, 2.0).process(xd[:n]), rd[:n]), td)
+    report("dc_blocker single-pass streamed 10007 nrmse", nrmse(stream(gpu_lib.DcBlocker(FS, 2.0), xd, 10007), rd), td)
     am = oracle.am_mod(real_tone(FS, 1000.0, 100_000, 0.5), FS, 0.0, 0.8, 0.5)
     got = stream(gpu_lib.AmEnvelopeDemod(FS, 5000, abs_approx=True), am, 33_333)
     report("am abs single-pass streamed nrmse",
