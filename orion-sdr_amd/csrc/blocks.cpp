@@ -155,6 +155,24 @@ class FmModBlock final : public Block {
     const size_t n = std::min(n_in, out_cap);  // fm.rs:47
     if (n == 0) return {0, 0};
     const float kf = kTauF * dev_ / fs_;  // fm.rs:48, f32 as in the reference
+    const long long nn = static_cast<long long>(n);
+    if (single_pass_) {
+      const size_t bytes = static_cast<size_t>(fm_mod_chunks(nn)) * 8 * sizeof(uint32_t);
+      if (bytes > rec_.size()) {
+        rec_.resize(bytes);
+        rec_.zero(s);
+        epoch_ = 0;
+      }
+      if (++epoch_ == 0xFFFFFFFFu) {  // never reuse a tag that may sit in a record
+        rec_.zero(s);
+        epoch_ = 1;
+      }
+      launch_fm_mod_sp(static_cast<const float*>(in), static_cast<f2*>(out), nn, kf, g_, rec_.as<uint32_t>(), epoch_,
+                       carry_[cur_].as<double>(), carry_[cur_ ^ 1].as<double>(), k_, osc_.step_q64, rtab_.as<f2>(), s);
+      cur_ ^= 1;
+      k_ += n;
+      return {n, n};
+    }
     sums_.resize(static_cast<size_t>(fm_mod_chunks(static_cast<long long>(n))) * sizeof(double));
     launch_fm_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), kf, g_,
                   sums_.as<double>(), carry_[cur_].as<double>(), carry_[cur_ ^ 1].as<double>(), k_, osc_.step_q64,
@@ -176,9 +194,15 @@ class FmModBlock final : public Block {
  private:
   float fs_, dev_, g_ = 1.0f;
   Oscillator osc_;
-  DevBuf carry_[2], sums_, rtab_;
+  DevBuf carry_[2], sums_, rtab_, rec_;
   int cur_ = 0;
   uint64_t k_ = 0;
+  uint32_t epoch_ = 0;
+  // single-pass phase scan (k_fm_mod_sp); ORION_FM_MOD_3P=1 keeps the three passes
+  bool single_pass_ = [] {
+    const char* e = std::getenv("ORION_FM_MOD_3P");
+    return !(e && std::atoi(e) == 1);
+  }();
 };
 
 // --------------------------------------------------------- FirDecimator ----

@@ -192,6 +192,127 @@ __global__ __launch_bounds__(NT) void k_fm_mod_apply(const float* __restrict__ x
   }
 }
 
+// Single pass (default; the three passes above stay behind ORION_FM_MOD_3P=1): each
+// chunk computes its increments once, publishes its f64 aggregate, and takes the
+// phase entering it by decoupled look-back over its predecessors (wave 0: lane i
+// looks at chunk c-1-i; the nearest chunk with a published inclusive prefix, or the
+// carried phase before chunk 0, closes the sum), then publishes its own inclusive
+// prefix. Chunk-major grid: every predecessor was dispatched earlier and publishes
+// its aggregate before it waits, so the walk always ends. Records: 8 u32 per chunk,
+// [0, 2) aggregate, [2, 4) inclusive prefix (f64), 6 / 7 their flags (launch epoch).
+__device__ __forceinline__ void fm_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t fm_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fm_st64(uint32_t* p, double v) {
+  const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
+  fm_st(p, static_cast<uint32_t>(b));
+  fm_st(p + 1, static_cast<uint32_t>(b >> 32));
+}
+__device__ __forceinline__ double fm_ld64(const uint32_t* p) {
+  const unsigned long long lo = fm_ld(p), hi = fm_ld(p + 1);
+  return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
+}
+
+__global__ __launch_bounds__(NT) void k_fm_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
+                                                  float kf, float gain, uint32_t* __restrict__ rec, uint32_t epoch,
+                                                  const double* __restrict__ carry_in, double* __restrict__ carry_out,
+                                                  uint64_t k0, uint64_t step, const f2* __restrict__ rtab) {
+  __shared__ double tot[NT / 64];
+  __shared__ double excl_sh;
+  __shared__ float xs[kFmCH + kFmCH / 16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int c = static_cast<int>(blockIdx.x);
+  const int nchunk = static_cast<int>((n + kFmCH - 1) / kFmCH);
+  const bool last = c == nchunk - 1;
+  const long long base = static_cast<long long>(c) * kFmCH;
+  for (int k = 0; k < kFmC; ++k) {
+    const int e = t + k * NT;
+    const long long i = base + e;
+    xs[e + (e >> 4)] = i < n ? x[i] : 0.0f;
+  }
+  __syncthreads();
+  double d[kFmC];
+  double run = 0.0;
+#pragma unroll
+  for (int k = 0; k < kFmC; ++k) {
+    const int e = t * kFmC + k;
+    d[k] = base + e < n ? fm_inc(kf, xs[e + (e >> 4)]) : 0.0;
+    run += d[k];
+  }
+  double inc = run;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const double o = __shfl_up(inc, dd, 64);
+    if (lane >= dd) inc += o;
+  }
+  if (lane == 63) tot[w] = inc;
+  __syncthreads();
+  if (w == 0) {
+    double agg = 0.0;
+    for (int v = 0; v < NT / 64; ++v) agg += tot[v];
+    uint32_t* my = rec + static_cast<long long>(c) * 8;
+    if (!last) {
+      if (lane == 0) fm_st64(my, agg);
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the aggregate is visible before its flag
+      if (lane == 0) fm_st(my + 6, epoch);
+    }
+    double excl = 0.0;
+    for (int b = c - 1;; b -= 64) {
+      const int k = b - lane;
+      double v = 0.0;
+      bool closes = true;
+      if (k >= 0) {
+        const uint32_t* pr = rec + static_cast<long long>(k) * 8;
+        int it = 0;
+        while (fm_ld(pr + 6) != epoch && fm_ld(pr + 7) != epoch && ++it < (1 << 22)) __builtin_amdgcn_s_sleep(2);
+        closes = fm_ld(pr + 7) == epoch;
+        v = closes ? fm_ld64(pr + 2) : fm_ld64(pr);
+      } else {
+        v = k == -1 ? carry_in[0] : 0.0;  // the carried phase before chunk 0
+      }
+      const unsigned long long bal = __ballot(closes);
+      const int first = bal ? __builtin_ctzll(bal) : 64;
+      double term = lane <= first ? v : 0.0;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) term += __shfl_xor(term, off, 64);
+      excl += term;
+      if (first < 64) break;
+    }
+    if (lane == 0) {
+      if (!last) {
+        fm_st64(my + 2, excl + agg);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        fm_st(my + 7, epoch);
+      } else {
+        const double end = excl + agg;  // the carried phase of the next call (reduced mod 2 pi)
+        carry_out[0] = end - 6.283185307179586 * rint(end * 0.15915494309189535);
+      }
+      excl_sh = excl;
+    }
+  }
+  __syncthreads();
+  double phi = excl_sh + inc - run;
+  for (int k = 0; k < w; ++k) phi += tot[k];
+  const long long i0 = base + t * kFmC;
+  const f2 R0 = phasor_q64(k0 + static_cast<uint64_t>(i0) + 1, step);
+#pragma unroll
+  for (int k = 0; k < kFmC; ++k) {
+    const long long i = i0 + k;
+    phi += d[k];
+    if (i < n) {
+      const double red = phi - 6.283185307179586 * rint(phi * 0.15915494309189535);
+      float sn, cs;
+      sincosf(static_cast<float>(red), &sn, &cs);
+      const f2 bz = f2{cs * gain, sn * gain};  // fm.rs:66 base = z * gain
+      const f2 r = cmul(R0, rtab[k]);
+      y[i] = f2{bz.x * r.x - bz.y * r.y, bz.x * r.y + bz.y * r.x};  // nco.rs:65 (no FMA)
+    }
+  }
+}
+
 }  // namespace
 
 void launch_am_mod(const float* x, f2* y, long long n, uint64_t k0, uint64_t step, float cl, float mi, float g,
@@ -214,6 +335,17 @@ void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, uint64
 }
 
 long long fm_mod_chunks(long long n) { return (n + kFmCH - 1) / kFmCH; }
+
+void launch_fm_mod_sp(const float* x, f2* y, long long n, float kf, float gain, uint32_t* rec, uint32_t epoch,
+                      const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
+                      hipStream_t s) {
+  if (n <= 0) return;
+  const long long nchunk = fm_mod_chunks(n);
+  if (nchunk > (1LL << 30)) throw HipError("FM modulator: input too long");
+  k_fm_mod_sp<<<static_cast<int>(nchunk), NT, 0, s>>>(x, y, n, kf, gain, rec, epoch, carry_in, carry_out, k0, step,
+                                                     rtab);
+  ORION_LAUNCH_CHECK();
+}
 int fm_mod_rtab_len() { return kFmC; }
 
 void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, double* sums,

@@ -26,6 +26,11 @@ void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, uint64
 // carry_out: the running phase (one double each, ping-pong between calls)
 // rtab: e^{j theta k}, k < fm_mod_rtab_len(), of the RF oscillator
 long long fm_mod_chunks(long long n);
+// Single-pass form: rec = fm_mod_chunks(n) * 8 u32 look-back records (zeroed when
+// allocated), epoch = this launch's tag (never reused while a record may hold it).
+void launch_fm_mod_sp(const float* x, f2* y, long long n, float kf, float gain, uint32_t* rec, uint32_t epoch,
+                      const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
+                      hipStream_t s);
 int fm_mod_rtab_len();
 void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, double* sums,
                    const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
