@@ -13,6 +13,9 @@ namespace orion {
 namespace {
 
 constexpr int NT = 256;
+#ifndef ORION_FIR8_UNROLL
+#define ORION_FIR8_UNROLL 1  // 16-tap blocks unrolled in k_fir_iq8 / k_fir_real8 (timing experiments)
+#endif
 constexpr int kMaxGrid = 2048;  // memory-bound: cap and grid-stride (2048 = 8 WG per CU)
 #ifndef ORION_FIR_HT
 #define ORION_FIR_HT 4
@@ -537,7 +540,7 @@ __global__ __launch_bounds__(NT) void k_fir_real8(const float* __restrict__ x, l
     f2 acc[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) acc[r] = f2{0.0f, 0.0f};
-#pragma unroll 1
+#pragma unroll ORION_FIR8_UNROLL
     for (int kb = 0; kb < KP / 16; ++kb) {
       const int pb = 8 * t + KP - 16 * kb - 16;  // as k_fir_iq8 (off = 0)
       f2 w[24];
@@ -706,7 +709,7 @@ __global__ __launch_bounds__(NT) void k_fir_iq8(const f2* x, long long n,
     f2 acc[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) acc[r] = f2{0.0f, 0.0f};
-#pragma unroll 1
+#pragma unroll ORION_FIR8_UNROLL
     for (int kb = 0; kb < KP / 16; ++kb) {
       // output j0 + r, tap 16 kb + kk reads element j0 + off + r - 16 kb - kk =
       // staged p = pb + 16 + r - kk, pb = 8 t + KP - 16 kb - 16 (even, >= 0)
