@@ -1,0 +1,59 @@
+"""profiles/traffic_<cfg>.json from a scripts/traffic_session.sh run: HBM bytes per
+launch of the config's kernel = FETCH_SIZE (KB; doubled on gfx950 for wide streaming
+reads, MI355X_MICROARCH.md, when the raw figure falls below the input the kernel must
+read) + WRITE_SIZE (KB), mean over the kernel's dispatches.
+  python tools/traffic.py gpurun_out/traffic c3 c4 c5"""
+import csv
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CFG = {  # samples per launch, input bytes, algorithmic bytes per sample, kernel name fragment
+    "c3": (256 << 20, 8 * (256 << 20), 9.0, "k_decim_w4"),
+    "c4": (8 << 24, 8 * (8 << 24), 8.5, "k_wbfm_seg4"),
+    "c5": (128 << 20, 8 * (128 << 20), 12.0, "k_lpdc_sp"),
+}
+
+
+def mean_kb(path, frag):
+    v, name = [], None
+    for r in csv.DictReader(open(path)):
+        if frag in r["Kernel_Name"]:
+            v.append(float(r["Counter_Value"]))
+            name = r["Kernel_Name"]
+    return sum(v) / len(v), name, len(v)
+
+
+def main():
+    src = sys.argv[1]
+    for cfg in sys.argv[2:]:
+        samples, inbytes, bps, frag = CFG[cfg]
+        f_kb, name, nf = mean_kb(os.path.join(src, f"{cfg}_FETCH_SIZE.csv"), frag)
+        w_kb, _, nw = mean_kb(os.path.join(src, f"{cfg}_WRITE_SIZE.csv"), frag)
+        raw = f_kb * 1024
+        doubled = raw < inbytes
+        fetch = 2 * raw if doubled else raw
+        write = w_kb * 1024
+        alg = bps * samples
+        short = name.split("(")[0].replace("void ", "").replace("orion::(anonymous namespace)::", "")
+        out = {
+            "config": cfg, "kernel": short, "samples_per_launch": samples,
+            "algorithmic_bytes_per_launch": alg, "hbm_bytes_per_launch": int(round(fetch + write)),
+            "per_kernel": {short: {"fetch_bytes" + ("_x2" if doubled else ""): int(round(fetch)),
+                                   "write_bytes": int(round(write)), "dispatches": [nf, nw]}},
+            "ratio_to_algorithmic": round((fetch + write) / alg, 4),
+            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (scripts/traffic_session.sh, "
+                      "bench.py --steps 3 --warmup 1, mean per dispatch); FETCH_SIZE "
+                      + ("doubled per MI355X_MICROARCH.md (gfx950 reports half of a wide streaming read; the raw "
+                         "figure was below the input bytes)" if doubled else "as reported")
+                      + "; KB = 1024 B",
+            "source": src,
+        }
+        p = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
+        json.dump(out, open(p, "w"), indent=1)
+        print(cfg, out["hbm_bytes_per_launch"], out["ratio_to_algorithmic"], "doubled" if doubled else "raw")
+
+
+if __name__ == "__main__":
+    main()
