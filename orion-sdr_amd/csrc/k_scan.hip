@@ -19,6 +19,9 @@ constexpr int PADN = CH + CH / 16 + 16;
 #ifndef ORION_SP_MINW
 #define ORION_SP_MINW 4  // waves per SIMD k_lpdc_sp is compiled for at kSpC samples per lane (<= 128 VGPRs)
 #endif
+#ifndef ORION_SP_TRUNC
+#define ORION_SP_TRUNC 1  // k_lpdc_sp: the LP4 lane scan truncated to the forgetting horizon (0: full two-scan form)
+#endif
 #ifndef ORION_SP_TAB2
 #define ORION_SP_TAB2 1  // SSB mixing phasor = (Swg tab[t]) tab[k NT]: one uniform table load per sample, not a per-lane one
 #endif
@@ -531,6 +534,40 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   double q[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) q[i] = s0[i];
+  double e[S];
+#if ORION_SP_TRUNC
+  // Truncated scan: the LP4 forgets its state within kSpWarm samples (the host checks
+  // ||A^kSpWarm|| < 1e-10, the warm-up's own criterion), i.e. within NL lane runs, so
+  // the state entering lane L is sum_{i = 1..NL} A^{C(i-1)} s0[L - i] to that bound:
+  // a log2(NL)-step scan over the wave (not 6 steps twice), the previous wave's last
+  // inclusive sum Q (lane 63) carried into lanes L < NL as A^{CL} Q, and in chunk 0 the
+  // carried state as A^{CL} carry (kLane holds A^{16 m}).
+  constexpr int NL = kSpWarm / SC;
+  constexpr int STEPS = NL == 8 ? 3 : NL == 16 ? 4 : 5;
+  static_assert(NL == (1 << STEPS) && NL * SC / kScanC < 64, "truncated scan geometry");
+#pragma unroll 1
+  for (int st = 0; st < STEPS; ++st) {
+    double o[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) o[i] = __shfl_up(q[i], 1 << st, 64);
+    if (lane >= (1 << st)) matvec_acc<S>(mlp + (kPw + st) * S * S, o, q);
+  }
+  if (lane == 63)
+#pragma unroll
+    for (int i = 0; i < S; ++i) tot[wave][i] = q[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const double o = __shfl_up(q[i], 1, 64);
+    e[i] = lane == 0 ? 0.0 : o;
+  }
+  if (lane < NL && (wave > 0 || c == 0)) {
+    double v[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) v[i] = wave > 0 ? tot[wave - 1][i] : static_cast<double>(ci[i]);
+    matvec_acc<S>(mlp + (ScanMatsLayout::kLane + lane * (SC / kScanC)) * S * S, v, e);
+  }
+#else
   wave_scan_inclusive<S>(q, mlp + kPw * S * S, lane);
   if (lane == 63)
 #pragma unroll
@@ -549,7 +586,6 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   }
   // the wave's entering state folded into lane 0 and the wave re-scanned (a
   // per-lane transition matrix would be 128 B of global reads per lane)
-  double e[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) q[i] = s0[i];
   if (lane == 0) matvec_acc<S>(mlp + kPw * S * S, cw, q);  // pw[0] = A^C
@@ -559,6 +595,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
     const double o = __shfl_up(q[i], 1, 64);
     e[i] = lane == 0 ? cw[i] : o;
   }
+#endif
 #pragma unroll
   for (int i = 0; i < S; ++i) ef[i] = static_cast<float>(e[i]);
 #pragma unroll
