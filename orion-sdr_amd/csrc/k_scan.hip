@@ -939,6 +939,11 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_sp(const float* __restrict__ x, 
   __syncthreads();
   float xs[2][C];
   float s0[2][S];
+#if ORION_SP_TRUNC
+  double qt[2][S];  // truncated scan (k_lpdc_sp): NL = kSpWarm / C lane runs span the horizon
+  constexpr int NL = kSpWarm / C, STEPS = NL == 16 ? 4 : NL == 8 ? 3 : 5;
+  static_assert(NL == (1 << STEPS) && NL * C / kScanC < 64, "truncated scan geometry");
+#endif
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
 #pragma unroll
@@ -951,7 +956,19 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_sp(const float* __restrict__ x, 
     double q[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) q[k] = s0[b][k];
+#if ORION_SP_TRUNC
+#pragma unroll 1
+    for (int st = 0; st < STEPS; ++st) {
+      double o[S];
+#pragma unroll
+      for (int k = 0; k < S; ++k) o[k] = __shfl_up(q[k], 1 << st, 64);
+      if (lane >= (1 << st)) matvec_acc<S>(mlp + (ScanMatsLayout::kPwc + st) * S * S, o, q);
+    }
+#pragma unroll
+    for (int k = 0; k < S; ++k) qt[b][k] = q[k];
+#else
     wave_scan_inclusive<S>(q, mlp + ScanMatsLayout::kPwc * S * S, lane);
+#endif
     if (lane == 63)
 #pragma unroll
       for (int k = 0; k < S; ++k) tot[b][wave][k] = q[k];
@@ -959,6 +976,23 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_sp(const float* __restrict__ x, 
   __syncthreads();
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
+#if ORION_SP_TRUNC
+    double e[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const double o = __shfl_up(qt[b][k], 1, 64);
+      e[k] = lane == 0 ? 0.0 : o;
+    }
+    if (lane < NL && (wave > 0 || c == 0)) {
+      double v[S];
+#pragma unroll
+      for (int k = 0; k < S; ++k) v[k] = wave > 0 ? tot[b][wave - 1][k] : static_cast<double>(carry_in[4 * b + k]);
+      matvec_acc<S>(mlp + (ScanMatsLayout::kLane + lane * (C / kScanC)) * S * S, v, e);
+    }
+    float ef[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) ef[k] = static_cast<float>(e[k]);
+#else
     double cw[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) cw[k] = c == 0 ? static_cast<double>(carry_in[4 * b + k]) : 0.0;
@@ -982,6 +1016,7 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_sp(const float* __restrict__ x, 
       const double o = __shfl_up(q[k], 1, 64);
       ef[k] = static_cast<float>(lane == 0 ? cw[k] : o);
     }
+#endif
 #pragma unroll
     for (int i = 0; i < C; ++i)
       if (t * C + i < cnt) xs[b][i] = lp.step(ef, xs[b][i]);  // ssb.rs:53-54 LpCascade outputs
