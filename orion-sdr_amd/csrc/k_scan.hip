@@ -768,7 +768,9 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
 // scan this drops the carry pass and the second read of the input. kSpC samples per
 // lane as k_lpdc_sp. Records: 16 u32 per (channel, chunk), [0, 2S) the aggregate
 // (f64), 15 the flag (launch epoch).
-template <RecK RK, Pre PR, Post PO>
+// TR: the stage also forgets within kSpWarm samples (the host checks ||A^kSpWarm||):
+// the lane scan truncated to NL = kSpWarm / C lane runs, as in k_lpdc_sp.
+template <RecK RK, Pre PR, Post PO, bool TR>
 __global__ __launch_bounds__(NT, 4) void k_scan_sp(const ScanArgs a, int nch, uint32_t* __restrict__ rec,
                                                    uint32_t epoch) {
   using R = typename RecSel<RK>::T;
@@ -816,7 +818,18 @@ __global__ __launch_bounds__(NT, 4) void k_scan_sp(const ScanArgs a, int nch, ui
   double q[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) q[i] = s0[i];
-  wave_scan_inclusive<S>(q, a.mats + kPw * S * S, lane);
+  constexpr int NL = kSpWarm / SC;
+  if constexpr (TR) {
+#pragma unroll 1
+    for (int st = 0; st < 3; ++st) {  // NL = 8 lane runs: 3 steps
+      double o[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) o[i] = __shfl_up(q[i], 1 << st, 64);
+      if (lane >= (1 << st)) matvec_acc<S>(a.mats + (kPw + st) * S * S, o, q);
+    }
+  } else {
+    wave_scan_inclusive<S>(q, a.mats + kPw * S * S, lane);
+  }
   if (lane == 63)
 #pragma unroll
     for (int i = 0; i < S; ++i) tot[wave][i] = q[i];
@@ -825,7 +838,8 @@ __global__ __launch_bounds__(NT, 4) void k_scan_sp(const ScanArgs a, int nch, ui
     double agg[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) agg[i] = 0.0;
-    for (int w = 0; w < 4; ++w) {
+    // truncated: the chunk's last lane already holds its zero-state end state
+    for (int w = TR ? 3 : 0; w < 4; ++w) {
       double v[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) v[i] = tot[w][i];
@@ -852,6 +866,23 @@ __global__ __launch_bounds__(NT, 4) void k_scan_sp(const ScanArgs a, int nch, ui
     }
   }
   __syncthreads();
+  float ef[S];
+  if constexpr (TR) {
+    double e[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const double o = __shfl_up(q[i], 1, 64);
+      e[i] = lane == 0 ? 0.0 : o;
+    }
+    if (lane < NL) {  // the previous wave's sum, or the state entering the chunk, as A^{C lane} v
+      double v[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) v[i] = wave > 0 ? tot[wave - 1][i] : cin_sh[i];
+      matvec_acc<S>(a.mats + (ScanMatsLayout::kLane + lane * (SC / kScanC)) * S * S, v, e);
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) ef[i] = static_cast<float>(e[i]);
+  } else {
   double cw[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) cw[i] = cin_sh[i];
@@ -868,12 +899,12 @@ __global__ __launch_bounds__(NT, 4) void k_scan_sp(const ScanArgs a, int nch, ui
   for (int i = 0; i < S; ++i) q[i] = s0[i];
   if (lane == 0) matvec_acc<S>(a.mats + kPw * S * S, cw, q);
   wave_scan_inclusive<S>(q, a.mats + kPw * S * S, lane);
-  float ef[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     const double o = __shfl_up(q[i], 1, 64);
     ef[i] = static_cast<float>(lane == 0 ? cw[i] : o);
   }
+  }  // TR
 #pragma unroll
   for (int i = 0; i < C; ++i)
     if (t * C + i < cnt) xs[i] = postmap<PO>(a, rr.step(ef, xs[i]));  // the reference's f32 update
@@ -1116,14 +1147,15 @@ bool scan_sp_supported(RecK rec, Pre pre, Post post) {
 }
 
 void launch_scan_sp(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, uint32_t* recs, uint32_t epoch,
-                    hipStream_t s) {
+                    bool trunc, hipStream_t s) {
   if (a.n <= 0 || nch <= 0) return;
   const long long grid = scan_sp_chunks(a.n) * nch;
   if (grid > (1LL << 31) - 1) throw HipError("single-pass scan grid too large");
   const int g = static_cast<int>(grid);
 #define ORION_SP(RK, PR, PO)                                                                         \
   if (rec == RecK::RK && pre == Pre::PR && post == Post::PO) {                                       \
-    k_scan_sp<RecK::RK, Pre::PR, Post::PO><<<g, NT, 0, s>>>(a, nch, recs, epoch);                    \
+    if (trunc) k_scan_sp<RecK::RK, Pre::PR, Post::PO, true><<<g, NT, 0, s>>>(a, nch, recs, epoch);   \
+    else k_scan_sp<RecK::RK, Pre::PR, Post::PO, false><<<g, NT, 0, s>>>(a, nch, recs, epoch);        \
     ORION_LAUNCH_CHECK();                                                                            \
     return;                                                                                          \
   }

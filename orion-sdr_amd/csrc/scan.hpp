@@ -103,7 +103,9 @@ int scan_state_dim(RecK rec);
 // recs: scan_sp_chunks(n) * nch * 16 u32 records; epoch: this launch's tag.
 bool scan_sp_supported(RecK rec, Pre pre, Post post);
 long long scan_sp_chunks(long long n);
+// trunc: the stage also forgets within kSpWarm samples (||A^kSpWarm|| < 1e-10): the
+// lane scan is truncated to that horizon.
 void launch_scan_sp(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, uint32_t* recs, uint32_t epoch,
-                    hipStream_t s);
+                    bool trunc, hipStream_t s);
 
 }  // namespace orion
