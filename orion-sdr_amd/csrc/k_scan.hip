@@ -768,9 +768,10 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
 // scan this drops the carry pass and the second read of the input. kSpC samples per
 // lane as k_lpdc_sp. Records: 16 u32 per (channel, chunk), [0, 2S) the aggregate
 // (f64), 15 the flag (launch epoch).
-// TR: the stage also forgets within kSpWarm samples (the host checks ||A^kSpWarm||):
-// the lane scan truncated to NL = kSpWarm / C lane runs, as in k_lpdc_sp.
-template <RecK RK, Pre PR, Post PO, bool TR>
+// TRS > 0: the stage also forgets within H = 2^TRS lane runs (H C samples; the host
+// picks the smallest H in {256, 512, 1024} samples with ||A^H|| < 1e-10): the lane scan
+// truncated to TRS steps, as in k_lpdc_sp. TRS = 0: the full scan and re-scan.
+template <RecK RK, Pre PR, Post PO, int TRS>
 __global__ __launch_bounds__(NT, 4) void k_scan_sp(const ScanArgs a, int nch, uint32_t* __restrict__ rec,
                                                    uint32_t epoch) {
   using R = typename RecSel<RK>::T;
@@ -818,10 +819,12 @@ __global__ __launch_bounds__(NT, 4) void k_scan_sp(const ScanArgs a, int nch, ui
   double q[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) q[i] = s0[i];
-  constexpr int NL = kSpWarm / SC;
+  constexpr bool TR = TRS > 0;
+  constexpr int NL = 1 << TRS;
+  static_assert(TRS <= 5 && NL * (SC / kScanC) <= 64, "truncation horizon within the kLane table");
   if constexpr (TR) {
 #pragma unroll 1
-    for (int st = 0; st < 3; ++st) {  // NL = 8 lane runs: 3 steps
+    for (int st = 0; st < TRS; ++st) {
       double o[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) o[i] = __shfl_up(q[i], 1 << st, 64);
@@ -1147,15 +1150,17 @@ bool scan_sp_supported(RecK rec, Pre pre, Post post) {
 }
 
 void launch_scan_sp(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, uint32_t* recs, uint32_t epoch,
-                    bool trunc, hipStream_t s) {
+                    int trs, hipStream_t s) {
   if (a.n <= 0 || nch <= 0) return;
   const long long grid = scan_sp_chunks(a.n) * nch;
   if (grid > (1LL << 31) - 1) throw HipError("single-pass scan grid too large");
   const int g = static_cast<int>(grid);
 #define ORION_SP(RK, PR, PO)                                                                         \
   if (rec == RecK::RK && pre == Pre::PR && post == Post::PO) {                                       \
-    if (trunc) k_scan_sp<RecK::RK, Pre::PR, Post::PO, true><<<g, NT, 0, s>>>(a, nch, recs, epoch);   \
-    else k_scan_sp<RecK::RK, Pre::PR, Post::PO, false><<<g, NT, 0, s>>>(a, nch, recs, epoch);        \
+    if (trs == 3) k_scan_sp<RecK::RK, Pre::PR, Post::PO, 3><<<g, NT, 0, s>>>(a, nch, recs, epoch);   \
+    else if (trs == 4) k_scan_sp<RecK::RK, Pre::PR, Post::PO, 4><<<g, NT, 0, s>>>(a, nch, recs, epoch); \
+    else if (trs == 5) k_scan_sp<RecK::RK, Pre::PR, Post::PO, 5><<<g, NT, 0, s>>>(a, nch, recs, epoch); \
+    else k_scan_sp<RecK::RK, Pre::PR, Post::PO, 0><<<g, NT, 0, s>>>(a, nch, recs, epoch);            \
     ORION_LAUNCH_CHECK();                                                                            \
     return;                                                                                          \
   }

@@ -103,9 +103,9 @@ int scan_state_dim(RecK rec);
 // recs: scan_sp_chunks(n) * nch * 16 u32 records; epoch: this launch's tag.
 bool scan_sp_supported(RecK rec, Pre pre, Post post);
 long long scan_sp_chunks(long long n);
-// trunc: the stage also forgets within kSpWarm samples (||A^kSpWarm|| < 1e-10): the
-// lane scan is truncated to that horizon.
+// trs: 3, 4 or 5 when the stage also forgets within 2^trs lane runs of kSpC samples
+// (||A^(2^trs kSpC)|| < 1e-10): the lane scan is truncated to that horizon; 0: full.
 void launch_scan_sp(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, uint32_t* recs, uint32_t epoch,
-                    bool trunc, hipStream_t s);
+                    int trs, hipStream_t s);
 
 }  // namespace orion

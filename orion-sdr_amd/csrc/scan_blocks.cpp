@@ -29,11 +29,17 @@ class ScanStage {
       for (double v : m) fro += v * v;
       const char* e = std::getenv("ORION_SCAN_3K");  // timing comparisons: keep the three-kernel scan
       sp1_ok_ = std::sqrt(fro) < 1e-10 && !(e && std::atoi(e) == 1);
-      const auto mw = mat_pow(ss.A, ss.S, kSpWarm);
-      double fw = 0.0;
-      for (double v : mw) fw += v * v;
+      // the shortest horizon of 2^trs lane runs (kSpC samples each) the stage forgets within
       const char* et = std::getenv("ORION_SCAN_FULL");  // timing comparisons: the untruncated lane scan
-      sp1_trunc_ = std::sqrt(fw) < 1e-10 && !(et && std::atoi(et) == 1);
+      for (int trs = 3; trs <= 5 && !(et && std::atoi(et) == 1); ++trs) {
+        const auto mw = mat_pow(ss.A, ss.S, static_cast<uint64_t>(kSpC) << trs);
+        double fw = 0.0;
+        for (double v : mw) fw += v * v;
+        if (std::sqrt(fw) < 1e-10) {
+          sp1_trs_ = trs;
+          break;
+        }
+      }
     }
     // DcBlocker alone: k_lpdc_sp's DC look-back without the LP4 (pole ~1: no chunk forgets)
     if (rec == RecK::DC && pre == Pre::Real && post == Post::Id) {
@@ -124,7 +130,7 @@ class ScanStage {
         rec_buf_.zero(s);
         epoch_ = 1;
       }
-      if (sp1_ok_) launch_scan_sp(rec_, pre_, post_, a, nch_, rec_buf_.as<uint32_t>(), epoch_, sp1_trunc_, s);
+      if (sp1_ok_) launch_scan_sp(rec_, pre_, post_, a, nch_, rec_buf_.as<uint32_t>(), epoch_, sp1_trs_, s);
       else launch_lpdc_sp(pre_, a, mats_lp_.as<double>(), nch_, rec_buf_.as<uint32_t>(), epoch_, s);
     } else {
       launch_scan(rec_, pre_, post_, a, nch_, s);
@@ -145,7 +151,7 @@ class ScanStage {
   bool sp_ok_ = false;   // k_lpdc_sp (LpDcCascade after SSB / AM-abs)
   bool sp1_ok_ = false;  // k_scan_sp (stages that forget within one chunk)
   bool dc_only_ = false;  // k_lpdc_sp<Real>: the DcBlocker alone
-  bool sp1_trunc_ = false;  // k_scan_sp with the lane scan truncated to kSpWarm samples
+  int sp1_trs_ = 0;  // k_scan_sp lane scan truncated to 2^sp1_trs_ lane runs (0: full)
   int mode_ = 0;
   uint32_t epoch_ = 0;
 };
