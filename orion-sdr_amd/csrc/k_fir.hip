@@ -440,6 +440,47 @@ __global__ __launch_bounds__(64, 2) void k_decim_w4(const f2* __restrict__ x, lo
   }
 }
 
+// k_decim_w4 with four waves per workgroup sharing one tap table (LDS per wave 12.9 KB
+// + 1 KB of taps per workgroup instead of per wave) and ONE tile of inputs in flight
+// per wave (<= 168 VGPRs): three waves per SIMD instead of two. Each wave still walks
+// its own range with no barrier after the tap load. ORION_DECIM_Q4=0 keeps k_decim_w4.
+template <int Q, bool A16, bool CLAMP>
+__global__ __launch_bounds__(256, 3) void k_decim_w4q(const f2* __restrict__ x, long long x_stride, long long n,
+                                                     const f2* __restrict__ hist, int hist_len, f2* __restrict__ out,
+                                                     long long out_stride, long long n_out, const Taps256 g, int wpc,
+                                                     long long L, int nranges) {
+  using D = Dw4<Q>;
+  __shared__ __attribute__((aligned(16))) f2 U4[4][D::LDS_F2];
+  __shared__ __attribute__((aligned(16))) float Gt[8 * Q];
+  for (int k = threadIdx.x; k < 8 * Q; k += 256) Gt[k] = g.g[k];
+  __syncthreads();
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = static_cast<int>(blockIdx.x) * 4 + w;
+  if (r >= nranges) return;
+  f2* __restrict__ U = U4[w];
+  const int ch = r / wpc;
+  const long long A = static_cast<long long>(r - ch * wpc) * L;
+  const long long B = min(A + L, n_out);
+  if (A >= B) return;
+  const int ntiles = static_cast<int>((B - A + D::TW - 1) / D::TW);
+  const f2* __restrict__ xc = x + ch * x_stride;
+  const f2* __restrict__ hc = hist + static_cast<long long>(ch) * hist_len;
+  f2* __restrict__ outc = out + ch * out_stride;
+  const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
+  const int s0 = c0 * D::LRS + D::slot((8 * Q + 2 * l + c0) / 8);
+  const int s1 = c1 * D::LRS + D::slot((8 * Q + 2 * l + 1 + c1) / 8);
+  long long porg = 8LL * (A - Q);
+  f2 va[D::KL][2];
+  dw_load<Q, A16, CLAMP>(xc, n, porg, l, va);
+  const long long dummy = -8LL * Q;
+#pragma unroll 1
+  for (int t = 0; t < ntiles; ++t, porg += D::NEW) {
+    const long long J = A + static_cast<long long>(t) * D::TW;
+    dw4_tile<Q, A16, CLAMP>(U, Gt, l, t, porg, J, xc, n, hc, hist_len, va, t + 1 < ntiles ? porg + D::NEW : dummy,
+                            s0, s1, outc, B);
+  }
+}
+
 __global__ __launch_bounds__(NT) void k_decim_generic(const f2* __restrict__ x, long long x_stride,
                                                       long long n, const f2* __restrict__ hist,
                                                       int hist_len, f2* __restrict__ out,
@@ -836,6 +877,37 @@ void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* 
     const char* e = std::getenv("ORION_DECIM_W2");
     return e && e[0] == '1';
   }();
+  static const bool q4 = [] {  // k_decim_w4q: four waves per workgroup, three per SIMD (ORION_DECIM_Q4=0: off)
+    const char* e = std::getenv("ORION_DECIM_Q4");
+    return !(e && e[0] == '0');
+  }();
+  if (M == 8 && K > 128 && K <= 256 && hist_len >= 8 * 32 && !legacy && !w2 && q4) {
+    static int capq = 0;
+    if (capq == 0) {
+      int per_cu = 0, dev = 0, ncu = 0;
+      ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decim_w4q<32, true, false>, 256, 0));
+      ORION_HIP(hipGetDevice(&dev));
+      ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      capq = std::max(1, per_cu) * 4 * std::max(1, ncu);  // waves
+    }
+    const long long tiles_ch = (n_out + 127) / 128;
+    const long long N = (tiles_ch * nch + capq - 1) / capq;  // tiles per wave
+    const long long L = N * 128;
+    const long long wpc = (n_out + L - 1) / L;
+    const long long nr = wpc * nch;
+    if (nr > (1LL << 31) - 1) throw HipError("decimator grid too large");
+    const bool clamp = n < 2 * 1024;
+    const int gi = static_cast<int>((nr + 3) / 4), wi = static_cast<int>(wpc), ni = static_cast<int>(nr);
+    if (clamp) {
+      if (a16) k_decim_w4q<32, true, true><<<gi, 256, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, ni);
+      else k_decim_w4q<32, false, true><<<gi, 256, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, ni);
+    } else {
+      if (a16) k_decim_w4q<32, true, false><<<gi, 256, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, ni);
+      else k_decim_w4q<32, false, false><<<gi, 256, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, ni);
+    }
+    ORION_LAUNCH_CHECK();
+    return;
+  }
   if (M == 8 && K <= 256 && hist_len >= 8 * (K <= 128 ? 16 : 32) && !legacy) {
     static int caps[2] = {0, 0};
     int& cap = caps[w2 ? 1 : 0];
