@@ -276,7 +276,7 @@ def main():
                                           else f"channel-sharded x{world}, no data-path collective")),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "k_wbfm_seg4" if args.config in ("c2", "c4") else ("k_decim_w4" if args.config == "c3"
+                     "kernel": "k_wbfm_seg4" if args.config in ("c2", "c4") else ("k_decim_w4q" if args.config == "c3"
                                                                                  else "k_lpdc_sp"),
                      "kernel_ms": round(kern_ms, 4), "bytes_per_sample": bps},
         "cpu_baseline": None,
