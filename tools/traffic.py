@@ -36,7 +36,8 @@ def main():
         fetch = 2 * raw if doubled else raw
         write = w_kb * 1024
         alg = bps * samples
-        short = name.replace("void ", "").replace("orion::(anonymous namespace)::", "").split("(")[0]
+        short = name.replace("void ", "").replace("orion::(anonymous namespace)::", "")
+        short = short[: short.rfind(">(") + 1] if ">(" in short else short.split("(")[0]
         out = {
             "config": cfg, "kernel": short, "samples_per_launch": samples,
             "algorithmic_bytes_per_launch": alg, "hbm_bytes_per_launch": int(round(fetch + write)),
