@@ -19,6 +19,9 @@ constexpr int PADN = CH + CH / 16 + 16;
 #ifndef ORION_SP_MINW
 #define ORION_SP_MINW 4  // waves per SIMD k_lpdc_sp is compiled for at kSpC samples per lane (<= 128 VGPRs)
 #endif
+#ifndef ORION_SCAN_SP_MINW
+#define ORION_SCAN_SP_MINW 4  // waves per SIMD k_scan_sp is compiled for (4: <= 128 VGPRs, spills 52-132 B)
+#endif
 #ifndef ORION_SP_TRUNC
 #define ORION_SP_TRUNC 1  // k_lpdc_sp: the LP4 lane scan truncated to the forgetting horizon (0: full two-scan form)
 #endif
@@ -772,7 +775,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
 // picks the smallest H in {256, 512, 1024} samples with ||A^H|| < 1e-10): the lane scan
 // truncated to TRS steps, as in k_lpdc_sp. TRS = 0: the full scan and re-scan.
 template <RecK RK, Pre PR, Post PO, int TRS>
-__global__ __launch_bounds__(NT, 4) void k_scan_sp(const ScanArgs a, int nch, uint32_t* __restrict__ rec,
+__global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanArgs a, int nch, uint32_t* __restrict__ rec,
                                                    uint32_t epoch) {
   using R = typename RecSel<RK>::T;
   constexpr int S = R::S;
