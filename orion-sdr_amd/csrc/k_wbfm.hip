@@ -2029,12 +2029,12 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
 
 // ---- segmented chain, four-group decimator ----------------------------------------
 #ifndef ORION_SEG4_X
-#define ORION_SEG4_X 31  // bits: 1 first phase opens the chains with a product, 2 taps-first read order (fu_tile8),
+#define ORION_SEG4_X 95  // bits: 1 first phase opens the chains with a product, 2 taps-first read order (fu_tile8),
                          // 4 audio FIR in blocks of 16 taps (sg::back), 8 iir16 (16 consecutive samples per lane),
-                         // 16 XCD-contiguous segment runs
+                         // 16 XCD-contiguous segment runs, 64 one tile of inputs in flight (no VGPR spills)
 #endif
 #ifndef ORION_SEG4_XALT
-#define ORION_SEG4_XALT 31  // a second instantiation for in-process A/B (ORION_SEG4_X_LIVE=<bits>)
+#define ORION_SEG4_XALT 95  // a second instantiation for in-process A/B (ORION_SEG4_X_LIVE=<bits>)
 #endif
 constexpr int kSeg4X = ORION_SEG4_X;
 constexpr int kSeg4XAlt = ORION_SEG4_XALT;
@@ -2079,9 +2079,10 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg4(const WbfmArgs a, const Wbf
   fu::trace(a, g.r, 0);
 
   const FuPrefetch org = fu_origin(a, g);
+  constexpr bool PF1 = (X & 64) != 0;  // one tile of inputs in flight instead of two (32 VGPRs)
   f2 va[G::KL][2], vb[G::KL][2];
   front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, l, va);
-  front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, l, vb);
+  if constexpr (!PF1) front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg + G::NEW, l, vb);
   const f2* __restrict__ tabc = a.tab + static_cast<long long>(g.ch) * kWbfmNS;
   const f2* __restrict__ xc = a.x + g.ch * a.x_stride;
   const f2* __restrict__ hc = a.hist_in + g.ch * kWbfmHist;
@@ -2128,6 +2129,21 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg4(const WbfmArgs a, const Wbf
         ph[k][1] = cmul(tb1, ek);
       }
     }
+    if constexpr (PF1) {
+#pragma unroll 1
+      for (int tin = 0; tin < sg::NS; ++tin, ++n, porg += G::NEW) {
+        if (kSegPrio) {
+          if ((16 * n < kSegPrioQ16 * ntiles) == late) __builtin_amdgcn_s_setprio(1);
+          else __builtin_amdgcn_s_setprio(0);
+        }
+        if ((n & 63) == 0)
+          Sv = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1 + static_cast<long long>(l) * G::NEW),
+                          a.step[g.ch]);
+        const long long jd0 = g.A + static_cast<long long>(n) * TW;
+        const FuPrefetch p0 = n + 1 < ntiles ? FuPrefetch{org.xl, org.nl, porg + G::NEW, true} : dummy;
+        fu_tile8<A16, CLAMP, X>(T, n, porg, jd0, ph, va, p0, Sv, carry, Phi + TW * tin, n & 63);
+      }
+    } else {
 #pragma unroll 1
     for (int tin = 0; tin < sg::NS; tin += 2, n += 2, porg += 2 * G::NEW) {
       if (kSegPrio) {  // see k_wbfm_seg
@@ -2144,6 +2160,7 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg4(const WbfmArgs a, const Wbf
       fu_tile8<A16, CLAMP, X>(T, n, porg, jd0, ph, va, p0, Sv, carry, dst, n & 63);
       fu_tile8<A16, CLAMP, X>(T, n + 1, porg + G::NEW, jd0 + TW, ph, vb, p1, Sv, carry, dst + TW, (n + 1) & 63);
     }
+    }  // PF1
     wave_lds_fence();
     if (sub == 0) {
       // keep sub-range 0's phi for the deferred back in the segment's global slot
