@@ -2036,6 +2036,9 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
 #ifndef ORION_SEG4_XALT
 #define ORION_SEG4_XALT 95  // a second instantiation for in-process A/B (ORION_SEG4_X_LIVE=<bits>)
 #endif
+#ifndef ORION_SEG_PRIO_Q16_ALT
+#define ORION_SEG_PRIO_Q16_ALT 9  // X & 128 (experiments): the priority hand-over point of k_wbfm_seg4, in 16ths
+#endif
 constexpr int kSeg4X = ORION_SEG4_X;
 constexpr int kSeg4XAlt = ORION_SEG4_XALT;
 // k_wbfm_seg4: k_wbfm_seg with fu_tile8's front tile. The padded image needs 2.3 KB
@@ -2133,7 +2136,7 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg4(const WbfmArgs a, const Wbf
 #pragma unroll 1
       for (int tin = 0; tin < sg::NS; ++tin, ++n, porg += G::NEW) {
         if (kSegPrio) {
-          if ((16 * n < kSegPrioQ16 * ntiles) == late) __builtin_amdgcn_s_setprio(1);
+          if ((16 * n < ((X & 128) ? ORION_SEG_PRIO_Q16_ALT : kSegPrioQ16) * ntiles) == late) __builtin_amdgcn_s_setprio(1);
           else __builtin_amdgcn_s_setprio(0);
         }
         if ((n & 63) == 0)
@@ -2147,7 +2150,7 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg4(const WbfmArgs a, const Wbf
 #pragma unroll 1
     for (int tin = 0; tin < sg::NS; tin += 2, n += 2, porg += 2 * G::NEW) {
       if (kSegPrio) {  // see k_wbfm_seg
-        if ((16 * n < kSegPrioQ16 * ntiles) == late) __builtin_amdgcn_s_setprio(1);
+        if ((16 * n < ((X & 128) ? ORION_SEG_PRIO_Q16_ALT : kSegPrioQ16) * ntiles) == late) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);
       }
       if ((n & 63) == 0)
