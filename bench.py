@@ -7,7 +7,7 @@ C2-sized channel (2^26 cf32 @ 10 Msps, its own tuning offset; BASELINE.json
 configs[1]). Channels are independent: no collective on the data path
 ("scaling": "weak"); the only collectives are the timing barrier / max.
 
-The roofline object prices the one kernel the chain runs (k_wbfm_seg4) with
+The roofline object prices the one kernel the chain runs (k_wbfm_seg) with
 HIP events on the stream it is launched on (one pair around the K launches, so
 inter-launch gaps count against it): algorithmic bytes per launch
 (8 B cf32 in + 4 B f32 audio out per 8 inputs = 8.5 B per input sample, SURVEY
@@ -17,8 +17,10 @@ single-threaded) timed on this host on a bounded prefix of the same input; the
 multi-channel configs time the oracle on min(channels, 16) host threads, one
 channel per thread, on a bounded prefix of that many channels.
 
-Other workloads (--config c3|c4|c5) are available for DESIGN.md tables; the
-driver's default line is c2.
+Other workloads (--config c1|c3|c4|c5) are available for DESIGN.md tables; the
+driver's default line is c2. C1 (BASELINE configs[0], the reference's CPU block
+graph: 127-tap FirLowpassIq over 2^20 cf32) is compute-bound (508 flop per 16 B),
+so its roofline is priced against packed FP32 (157.3 TFLOP/s), not HBM.
 """
 import argparse
 import json
@@ -35,12 +37,16 @@ import torch  # noqa: E402  (device memory, streams, torch.distributed: plumbing
 import orion_sdr  # noqa: E402  (the HIP engine; raises if the library is missing)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+FP32_PEAK_TFLOPS = 157.3  # MI355X packed FP32 (v_pk_fma_f32) dense peak (MI355X_MICROARCH.md)
 METRIC = "Msamples/s through WBFM demod chain (NCO+decim+FM discrim) at 1/2/4/8 MI355X"
 OFFSETS = [1.5e6, -2.25e6, 0.75e6, -3.5e6, 2.75e6, -0.5e6, 3.75e6, -1.25e6]
 METRICS = {  # the non-default configs name what they measure
+    "c1": "Msamples/s through 127-tap FirLowpassIq (1 channel, 2^20 cf32 per pass) per MI355X",
     "c3": "Msamples/s through batched 255-tap decimating FIR (256 channels, M=8) per MI355X",
     "c5": "Msamples/s through SSB product demod (128 channels @ 48 ksps) per MI355X",
 }
+KERNELS = {"c1": "k_fir_iq8", "c2": "k_wbfm_seg", "c3": "k_decim_w4q", "c4": "k_wbfm_seg", "c5": "k_lpdc_sp"}
+CHANNELS_PER_GPU = {"c3": 256, "c4": 8, "c5": 128}
 
 
 def _sum_sin(w, k):
@@ -69,16 +75,44 @@ def wbfm_iq(n, f_off, dev, seed, fs=10e6, t0=0, noise=0.0025):
 
 
 def channel_plan(cfg, rank, world):
-    """The independent channels rank `rank` of `world` owns: [(f_off_hz, seed)].
+    """The independent channels rank `rank` of `world` owns: [(param, seed)] with
+    param the tuning offset (Hz) for C2/C4 and the global channel index for C3/C5.
     Contiguous channel ranges per rank, disjoint, fixed per-rank work (weak
-    scaling); nothing on the data path crosses ranks."""
+    scaling: C3 256, C4 8, C5 128 channels per GPU; C5's 1024 channels on 8 GPUs);
+    nothing on the data path crosses ranks. Every channel's input is
+    generated from its own seed, so a channel's output does not depend on the
+    rank that runs it."""
     if cfg == "c2":
         return [(OFFSETS[rank % len(OFFSETS)], 0x1234 + rank)]
     if cfg == "c4":
-        nch = 8
+        nch = CHANNELS_PER_GPU["c4"]
         return [(OFFSETS[(rank * nch + c) % len(OFFSETS)] * (1 + 0.01 * c), 0x1234 + rank * nch + c)
                 for c in range(nch)]
+    if cfg in ("c3", "c5"):
+        nch = CHANNELS_PER_GPU[cfg]
+        base = 77 if cfg == "c3" else 99
+        return [(rank * nch + c, (base << 20) ^ (rank * nch + c)) for c in range(nch)]
     raise ValueError(cfg)
+
+
+def channel_input(cfg, n, seed, dev):
+    """One C3 / C5 channel's synthetic input (complex64, on `dev`), from its seed."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    if cfg == "c3":
+        return torch.randn(n, dtype=torch.complex64, device=dev, generator=g)
+    t = torch.arange(n, device=dev, dtype=torch.float64) / 48e3  # C5: USB voice-band tone + noise
+    base = torch.polar(torch.ones_like(t), 2 * np.pi * 2700.0 * t).to(torch.complex64) * 0.4
+    return (base + 0.03 * torch.randn(n, dtype=torch.complex64, device=dev, generator=g)).contiguous()
+
+
+def c1_input(n, dev, seed=0x1234_5678):
+    """C1: complex tone at 0.03 fs plus complex noise of power 0.01."""
+    t = torch.arange(n, device=dev, dtype=torch.float64)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    x = torch.polar(torch.ones_like(t), 2 * np.pi * 0.03 * t).to(torch.complex64)
+    return (x + np.sqrt(0.01) * torch.randn(n, dtype=torch.complex64, device=dev, generator=g)).contiguous()
 
 
 def max_over_ranks(elapsed, dist, device):
@@ -122,25 +156,29 @@ def make_workload(cfg, rank, dev, n_override=None, world=1, shard="stream"):
         desc = dict(workload="C4 WBFM chain, 8 independent channels per GPU", samples_per_step_per_gpu=nch * n,
                     channels_per_gpu=nch)
         return blk, x, nch * n, 8.5, desc
+    if cfg == "c1":
+        n = n_override or (1 << 20)
+        blk = orion_sdr.FirLowpassIq.design(127, 0.2, 60.0)
+        x = c1_input(n, dev)
+        desc = dict(workload="C1 FirLowpassIq::design(127, 0.2, 60 dB) over 2^20 cf32 per pass (the reference's "
+                    "CPU Block-graph config, here on the device path)", samples_per_step_per_gpu=n, channels_per_gpu=1,
+                    flop_per_sample=508)
+        return blk, x, n, 16.0, desc
     if cfg == "c3":
-        nch, n = 256, n_override or (1 << 20)
+        plan = channel_plan(cfg, rank, world)
+        nch, n = len(plan), n_override or (1 << 20)
         blk = orion_sdr.FirDecimator(10e6, 8, 190e3, 39370.0, channels=nch)
-        g = torch.Generator(device=dev)
-        g.manual_seed(77 + rank)
-        x = torch.randn(nch, n, dtype=torch.complex64, device=dev, generator=g)
+        x = torch.stack([channel_input(cfg, n, seed, dev) for _, seed in plan]).contiguous()
         desc = dict(workload="C3 batched FirDecimator, 256 channels x 255 taps, M=8", samples_per_step_per_gpu=nch * n,
-                    channels_per_gpu=nch)
+                    channels_per_gpu=nch, channels=[plan[0][0], plan[-1][0] + 1])
         return blk, x, nch * n, 9.0, desc
     if cfg == "c5":
-        nch, n = 128, n_override or (1 << 20)
+        plan = channel_plan(cfg, rank, world)
+        nch, n = len(plan), n_override or (1 << 20)
         blk = orion_sdr.SsbProductDemod(48e3, 1500.0, 2800.0, channels=nch)
-        g = torch.Generator(device=dev)
-        g.manual_seed(99 + rank)
-        t = torch.arange(n, device=dev, dtype=torch.float64) / 48e3
-        base = torch.polar(torch.ones_like(t), 2 * np.pi * 2700.0 * t).to(torch.complex64) * 0.4
-        x = (base.unsqueeze(0) + 0.03 * torch.randn(nch, n, dtype=torch.complex64, device=dev, generator=g)).contiguous()
-        desc = dict(workload="C5 SsbProductDemod, 128 channels per GPU @ 48 ksps", samples_per_step_per_gpu=nch * n,
-                    channels_per_gpu=nch)
+        x = torch.stack([channel_input(cfg, n, seed, dev) for _, seed in plan]).contiguous()
+        desc = dict(workload="C5 SsbProductDemod, 128 channels per GPU @ 48 ksps (1024 on 8 GPUs)",
+                    samples_per_step_per_gpu=nch * n, channels_per_gpu=nch, channels=[plan[0][0], plan[-1][0] + 1])
         return blk, x, nch * n, 12.0, desc
     raise SystemExit(f"unknown --config {cfg}")
 
@@ -187,6 +225,23 @@ def cpu_baseline(x_dev, cfg, seconds_target, max_samples):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
+    if cfg == "c1":
+        taps = O.kaiser_lowpass_taps(127, 0.2, 60.0)
+        n_all = x_dev.shape[-1]
+        xh_all = x_dev.cpu().numpy()
+        probe = min(n_all, 1 << 16)
+        t0 = time.perf_counter()
+        O.fir_lowpass_iq(xh_all[:probe], taps)
+        rate = probe / (time.perf_counter() - t0)
+        passes = max(1, int(rate * seconds_target / n_all))
+        t0 = time.perf_counter()
+        for _ in range(passes):
+            ref = O.fir_lowpass_iq(xh_all, taps)
+        dt = time.perf_counter() - t0
+        return dict(value=round(passes * n_all / dt / 1e6, 4), unit="Msamples/s", cores=1, kind="port",
+                    sample=f"{passes} passes over the whole 2^{np.log2(n_all):.0f}-sample C1 input, oracle/orion_oracle.c "
+                           f"o_fir_lowpass_iq, 1 thread, {os.uname().nodename}",
+                    seconds=round(dt, 2)), xh_all, ref
     if cfg not in ("c2",):
         return None
     n = min(max_samples, x_dev.shape[-1])
@@ -211,7 +266,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--n", type=int, default=0, help="override samples per channel")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-max-samples", type=int, default=1 << 24)
@@ -237,7 +292,7 @@ def main():
     blk, x, samples, bps, desc = make_workload(args.config, rank, dev, args.n or None, world, args.shard)
     nout = blk.out_len(x.shape[-1])
     out_shape = (nout,) if x.dim() == 1 else (x.shape[0], nout)
-    out_dtype = torch.float32 if args.config != "c3" else torch.complex64
+    out_dtype = torch.complex64 if args.config in ("c1", "c3") else torch.float32
     out = torch.empty(out_shape, dtype=out_dtype, device=dev)
     torch.cuda.synchronize(dev)
 
@@ -275,37 +330,47 @@ def main():
                                           "data-path collective" if "halo_samples" in desc
                                           else f"channel-sharded x{world}, no data-path collective")),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "k_wbfm_seg4" if args.config in ("c2", "c4") else ("k_decim_w4q" if args.config == "c3"
-                                                                                 else "k_lpdc_sp"),
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": KERNELS[args.config],
                      "kernel_ms": round(kern_ms, 4), "bytes_per_sample": bps},
         "cpu_baseline": None,
     }
+    if args.config == "c1":  # compute-bound: packed FP32 is the roof (31.75 flop/B > the ~19.7 flop/B ridge)
+        tflops = samples * desc["flop_per_sample"] / (kern_ms * 1e-3) / 1e12
+        line["roofline"].update(bound="fp32", achieved=round(tflops, 2), peak=FP32_PEAK_TFLOPS, unit="TFLOP/s",
+                                frac=round(tflops / FP32_PEAK_TFLOPS, 4), hbm_gbs=round(achieved, 1),
+                                hbm_frac=round(achieved / HBM_PEAK_GBS, 4))
     # on-box read ceiling (after the timed region): the library's streaming-read probe
-    # over this rank's input, 10 launches between events
-    nb = orion_sdr.diag_stream_read(x, stream.cuda_stream)
-    p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    p0.record(stream)
-    for _ in range(10):
-        orion_sdr.diag_stream_read(x, stream.cuda_stream)
-    p1.record(stream)
-    torch.cuda.synchronize(dev)
-    peak_meas = nb / (p0.elapsed_time(p1) / 10 * 1e-3) / 1e9
-    line["roofline"]["peak_measured"] = round(peak_meas, 1)
-    line["roofline"]["frac_measured"] = round(achieved / peak_meas, 4)
+    # over this rank's input, 10 launches between events. Diagnostic
+    # only: a probe that cannot run (input below one tile per wave) leaves it null.
+    try:
+        nb = orion_sdr.diag_stream_read(x, stream.cuda_stream) if args.config != "c1" else 0
+        if nb > 0:
+            p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            p0.record(stream)
+            for _ in range(10):
+                orion_sdr.diag_stream_read(x, stream.cuda_stream)
+            p1.record(stream)
+            torch.cuda.synchronize(dev)
+            peak_meas = nb / (p0.elapsed_time(p1) / 10 * 1e-3) / 1e9
+            line["roofline"]["peak_measured"] = round(peak_meas, 1)
+            line["roofline"]["frac_measured"] = round(achieved / peak_meas, 4)
+    except Exception as e:  # noqa: BLE001  (the bench line must still print)
+        line["roofline"]["peak_measured"] = None
+        line["roofline"]["probe_error"] = str(e)[:120]
     traffic_file = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(traffic_file):
         tr = json.load(open(traffic_file))
         if tr.get("samples_per_launch") == samples:
             line["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
-    if rank == 0 and world == 1 and not args.no_cpu and args.config == "c2":
+    if rank == 0 and world == 1 and not args.no_cpu and args.config in ("c1", "c2"):
         res = cpu_baseline(x, args.config, args.cpu_seconds, args.cpu_max_samples)
         if res:
             cb, xh, ref = res
-            fresh = orion_sdr.WbfmChain(f_off=OFFSETS[0])
+            fresh = (orion_sdr.WbfmChain(f_off=OFFSETS[0]) if args.config == "c2"
+                     else orion_sdr.FirLowpassIq.design(127, 0.2, 60.0))
             got = fresh.process(xh)
-            den = float(np.sqrt(np.mean(ref.astype(np.float64) ** 2)))
-            cb["gpu_vs_cpu_nrmse"] = float(np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2)) / den)
+            den = float(np.sqrt(np.mean(np.abs(ref.astype(np.complex128)) ** 2)))
+            cb["gpu_vs_cpu_nrmse"] = float(np.sqrt(np.mean(np.abs(got.astype(np.complex128) - ref) ** 2)) / den)
             line["cpu_baseline"] = cb
     elif rank == 0 and world == 1 and not args.no_cpu:
         f_offs = [f for f, _ in channel_plan("c4", 0, 1)] if args.config == "c4" else None

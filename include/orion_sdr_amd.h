@@ -61,8 +61,35 @@ size_t orion_diag_stream_read_bytes(size_t bytes);
 int orion_diag_stream_read(const void* dev, size_t bytes, void* stream);
 
 /* ---- constructors (one per reference constructor) ---------------------- */
-/* dsp/rotator.rs:16-26 Rotator::new(freq_hz, fs); Block-like rotate_block (:74-85). cf32->cf32 */
+/* dsp/rotator.rs:16-26 Rotator::new(freq_hz, fs); Block-like rotate_block (:74-85). cf32->cf32
+ * The oscillator is closed-form and phase-exact: the phasor after k steps is
+ * e^{j theta k} with theta the exact angle of the reference's f32 step phasor w
+ * (the reference's f32 recurrence drifts from it by its own rounding). */
 orion_block* orion_rotator_new(float freq_hz, float fs);
+/* dsp/rotator.rs:35-39 Rotator::set_freq(freq_hz, fs): a new step phasor; the phase
+ * continues from where it is (the reference keeps z). Synchronizes the device
+ * (kernels in flight read the oscillator table). */
+int orion_rotator_set_freq(orion_block* b, float freq_hz, float fs);
+/* dsp/rotator.rs:28-31 Rotator::reset_phase: phasor back to 1 + j0 (the step stays);
+ * the same as orion_block_reset on a Rotator. */
+int orion_rotator_reset_phase(orion_block* b);
+/* dsp/rotator.rs:88-94 Rotator::mix_usb_block(input, out): out[i] = fma(I, cos, Q*sin)
+ * with the phasor of the next step, on the same oscillator as rotate_block; n =
+ * min(n_in, out_cap). cf32 -> f32. Host buffers (synchronous) / device buffers. */
+int orion_rotator_mix_usb_block(orion_block* b, const void* in, size_t n_in, float* out, size_t out_cap,
+                                orion_work_report* wr);
+int orion_rotator_mix_usb_block_device(orion_block* b, const void* in_dev, size_t n_in, float* out_dev, size_t out_cap,
+                                       void* stream, orion_work_report* wr);
+/* dsp/nco.rs:20-31 Nco::new(freq_hz, fs) as a block: process = mix_with_nco per sample
+ * (nco.rs:63-66, the non-FMA product (x.re c - x.im s, x.re s + x.im c)). cf32->cf32 */
+orion_block* orion_nco_new(float freq_hz, float fs);
+/* dsp/nco.rs:33-38 Nco::set_freq(freq_hz) (fs from orion_nco_new): the phase continues.
+ * Synchronizes the device. */
+int orion_nco_set_freq(orion_block* b, float freq_hz);
+/* dsp/nco.rs:42-58 next_cs, n times: out[i] = (cos, sin) of the phasor after each step
+ * (cf32 pairs). Host buffer (synchronous) / device buffer. */
+int orion_nco_next_cs_block(orion_block* b, void* out, size_t n);
+int orion_nco_next_cs_block_device(orion_block* b, void* out_dev, size_t n, void* stream);
 /* dsp/decim.rs:24-37 FirDecimator::new(fs, m, cutoff_hz, trans_hz). cf32->cf32 */
 orion_block* orion_fir_decimator_new(float fs, size_t m, float cutoff_hz, float trans_hz);
 /* Batched FirDecimator: nch independent channels sharing one design. */
@@ -80,6 +107,17 @@ int orion_fir_lowpass_iq_filter_aligned_device(orion_block* b, void* io_dev, siz
 int orion_fir_lowpass_iq_filter_aligned(orion_block* b, void* io, size_t n);
 /* dsp/iir.rs:49-71 LpCascade::design(fs, fc) as a f32->f32 block (:79-83). */
 orion_block* orion_lp_cascade_new(float fs, float fc);
+/* dsp/iir.rs:15-41 Biquad::new(b0, b1, b2, a1, a2) (TDF-II, process :34-40) as an f32->f32
+ * block; orion_block_reset = Biquad::reset. Any coefficients: a design whose state
+ * decays within 8192 samples runs one pass, any other (a pole near the unit circle)
+ * the three-kernel state-carry scan with f64 carries. */
+orion_block* orion_biquad_new(float b0, float b1, float b2, float a1, float a2);
+/* dsp/iir.rs:111-137 LpDcCascade::design(fs, lp_fc, dc_cut_hz); process :151-165 (LP4 then
+ * the DC blocker). f32->f32 */
+orion_block* orion_lp_dc_cascade_new(float fs, float lp_fc, float dc_cut_hz);
+/* on = 1: process_mapped(x, f32::sqrt) (iir.rs:170-186: sqrt between the LP4 and the DC
+ * blocker, the AM-PowerSqrt use) instead of process; set before the first call. */
+int orion_lp_dc_cascade_set_sqrt_map(orion_block* b, int on);
 /* dsp/dc.rs:15-21 DcBlocker::new(fs, cut_hz); Block impl :40-58. f32->f32 */
 orion_block* orion_dc_blocker_new(float fs, float cut_hz);
 /* demodulate/fm.rs:22-32 FmQuadratureDemod::new(fs, dev_hz, audio_bw_hz). cf32->f32 */
@@ -116,6 +154,17 @@ int orion_am_dsb_mod_set_clamp(orion_block* b, int on);
 orion_block* orion_fm_phase_accum_mod_new(float fs, float deviation_hz, float rf_hz);
 int orion_fm_phase_accum_mod_set_deviation(orion_block* b, float deviation_hz);
 int orion_fm_phase_accum_mod_set_gain(orion_block* b, float g);
+/* modulate/pm.rs:17-29 PmDirectPhaseMod::new(sample_rate, kp_rad_per_unit, rf_hz); set_gain,
+ * set_sensitivity. process :36-47: (cos kp x, sin kp x) * gain, mixed with the RF Nco. */
+orion_block* orion_pm_direct_phase_mod_new(float fs, float kp_rad_per_unit, float rf_hz);
+int orion_pm_direct_phase_mod_set_gain(orion_block* b, float g);
+int orion_pm_direct_phase_mod_set_sensitivity(orion_block* b, float kp_rad_per_unit);
+/* modulate/cw.rs:21-41 CwKeyedMod::new(sample_rate, tone_hz, rise_ms, fall_ms); set_gain.
+ * process :45-87: keying input clamped to [0, 1], rise/fall one-pole envelope, mixed with
+ * the tone Nco. The envelope is a data-dependent recurrence: chunked warm-ups whose
+ * exactness is checked bitwise, in-order re-runs where it fails (as AgcRms). */
+orion_block* orion_cw_keyed_mod_new(float fs, float tone_hz, float rise_ms, float fall_ms);
+int orion_cw_keyed_mod_set_gain(orion_block* b, float g);
 /* modulate/ssb.rs:22-35 SsbPhasingMod::new(fs, audio_bw_hz, audio_if_hz, rf_hz, usb). */
 orion_block* orion_ssb_phasing_mod_new(float fs, float audio_bw_hz, float audio_if_hz, float rf_hz, int usb);
 
@@ -137,15 +186,16 @@ orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float*
  * LpCascade decays fast enough for it (the WBFM defaults), else two kernels;
  * max_segments > 0 caps the segmented kernel's waves (0 = the resident
  * capacity). ORION_E_TYPE if b is not a WBFM chain, ORION_E_ARG if the design
- * cannot run on that path. */
+ * cannot run on that path.
+ * Residency: the segmented kernel launches one round of waves (at most the
+ * device's resident capacity) and each segment waits, bounded, for the end state
+ * its predecessor publishes. Predecessors are dispatched earlier except at the
+ * seven XCD run boundaries, so a wait outlasts its bound only if other work holds
+ * the CUs for longer than ~0.5 s; the handle then reports ORION_E_HIP (see
+ * orion_block_status) instead of returning the audio as valid. */
 #define ORION_WBFM_AUTO 0
-#define ORION_WBFM_SEGMENTED 1  /* one kernel, one round of segments, FIR spread over tiles */
-#define ORION_WBFM_RANGES 2     /* one kernel, one wave per 2048-output range */
+#define ORION_WBFM_SEGMENTED 1  /* one kernel, one round of segments (k_wbfm_seg) */
 #define ORION_WBFM_SPLIT 3      /* two kernels (front, back), any IIR design */
-#define ORION_WBFM_SEGMENTED_V1 4
-#define ORION_WBFM_SPECIALIZED 5  /* one kernel, streaming and back waves per CU */
-#define ORION_WBFM_SEGMENTED3 6   /* one kernel, three waves per SIMD, burst back */
-#define ORION_WBFM_SEGMENTED4 7   /* k_wbfm_seg with the four-group decimator tile */
 int orion_wbfm_chain_configure(orion_block* b, int path, int max_segments);
 /* Time-sharded streams (no reference counterpart): the absolute
  * index of the next input sample, i.e. the NCO phase origin (rotator.rs:44-62
@@ -163,6 +213,20 @@ int orion_block_process(orion_block* b, const void* in, size_t n_in, void* out, 
  * internal copy of the input). */
 int orion_block_process_device(orion_block* b, const void* in_dev, size_t n_in, void* out_dev,
                                size_t out_cap, void* stream, orion_work_report* wr);
+/* Device-side failures (no reference counterpart; the reference never fails on the
+ * path, core.rs:12-22): kernels that wait on other workgroups (the WBFM segment
+ * hand-off, the single-pass scans' decoupled look-back, FmPhaseAccumMod's phase
+ * look-back) bound every wait and flag a timeout in the handle's host-visible
+ * error word instead of hanging. orion_block_status returns ORION_E_HIP once if a
+ * kernel of this handle flagged one since the last check (non-blocking; it sees
+ * every kernel that has finished: orion_synchronize(stream) first to cover all).
+ * orion_block_process checks after its own sync; orion_block_process_device
+ * checks at entry, so an error of call k fails call k+1 at the latest. */
+int orion_block_status(orion_block* b);
+/* Test-only: polls a cross-workgroup wait makes before it times out (process-wide;
+ * default 1 << 22; 0 makes every such wait time out at once). */
+void orion_debug_set_spin_limit(uint32_t polls);
+uint32_t orion_debug_spin_limit(void);
 int orion_block_reset(orion_block* b);
 void orion_block_free(orion_block* b);
 int orion_block_in_type(const orion_block* b);
@@ -170,6 +234,13 @@ int orion_block_out_type(const orion_block* b);
 size_t orion_block_out_len(const orion_block* b, size_t n_in);
 size_t orion_block_channels(const orion_block* b);
 const char* orion_block_name(const orion_block* b);
+/* Engine options (no reference counterpart; tests and timing comparisons).
+ * ORION_E_TYPE if the block has no such option, ORION_E_ARG for a bad value. */
+#define ORION_OPT_SCAN_PATH 1   /* IIR-based blocks (LpCascade, DcBlocker, Biquad, LpDcCascade, the FM/PM/SSB/
+                                   AM/CW demods): 0 single pass where the design allows (default), 1 the
+                                   three-kernel scan */
+#define ORION_OPT_MOD_PASSES 2  /* FmPhaseAccumMod, SsbPhasingMod: 0 single pass (default), 3 three passes */
+int orion_block_configure(orion_block* b, int option, long long value);
 /* Designed coefficients, for parity tests: which = 0 primary taps, 1 audio taps. */
 int orion_block_taps(const orion_block* b, int which, float* out, size_t cap, size_t* n);
 

@@ -54,6 +54,10 @@ def lib():
         "o_kaiser_beta": (_f, [_f]),
         "o_bessel_i0": (_f, [_f]),
         "o_run_rotator": (_sz, [_f, _f, _c64p, _c64p, _sz, _sz]),
+        "o_run_rotator_retune": (_sz, [_f, _f, C.c_int, _c64p, C.c_void_p, _sz, _sz, _f, _f, C.c_int]),
+        "o_run_nco": (_sz, [_f, _f, C.c_int, _c64p, _c64p, _sz, _sz, _f]),
+        "o_run_biquad": (_sz, [_f, _f, _f, _f, _f, _f32p, _f32p, _sz]),
+        "o_run_lpdc": (_sz, [_f, _f, _f, C.c_int, _f32p, _f32p, _sz]),
         "o_run_fir": (_sz, [_f, _f, _f, _f32p, _f32p, _sz, _sz]),
         "o_run_firiq": (_sz, [_f32p, _sz, _c64p, _c64p, _sz, _sz]),
         "o_run_firiq_aligned": (None, [_f32p, _sz, _c64p, _sz]),
@@ -140,6 +144,39 @@ def rotator(x, freq_hz, fs, chunk=0):
     y = np.empty_like(x)
     lib().o_run_rotator(freq_hz, fs, x, y, len(x), chunk)
     return y
+
+
+def rotator_retune(x, f1, fs, n_switch, f2, fs2=None, usb=False, reset=False):
+    """Rotator(f1, fs): rotate_block (usb: mix_usb_block, f32 out) over x with
+    set_freq(f2, fs2) (reset: reset_phase) after the first n_switch samples."""
+    x = _c64(x)
+    out = np.zeros(len(x), np.float32 if usb else np.complex64)
+    lib().o_run_rotator_retune(f1, fs, 1 if usb else 0, x, out.ctypes.data, len(x), n_switch, f2,
+                               fs if fs2 is None else fs2, 1 if reset else 0)
+    return out
+
+
+def nco(x, f1, fs, n_switch=None, f2=0.0, gen=False):
+    """Nco(f1, fs): mix_with_nco per sample (gen: next_cs pairs; x gives the length),
+    set_freq(f2) after n_switch samples."""
+    x = _c64(x)
+    out = np.zeros(len(x), np.complex64)
+    lib().o_run_nco(f1, fs, 1 if gen else 0, x, out, len(x), len(x) if n_switch is None else n_switch, f2)
+    return out
+
+
+def biquad(x, b0, b1, b2, a1, a2):
+    x = _f32(x)
+    out = np.zeros_like(x)
+    lib().o_run_biquad(b0, b1, b2, a1, a2, x, out, len(x))
+    return out
+
+
+def lp_dc_cascade(x, fs, lp_fc, dc_cut, sqrt_map=False):
+    x = _f32(x)
+    out = np.zeros_like(x)
+    lib().o_run_lpdc(fs, lp_fc, dc_cut, 1 if sqrt_map else 0, x, out, len(x))
+    return out
 
 
 def fir_lowpass(x, fs, pass_hz, trans_hz, chunk=0):

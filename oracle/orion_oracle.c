@@ -44,6 +44,11 @@ void o_rotator_init(o_rotator *r, float freq_hz, float fs) {
     r->w.re = cosf(phi); r->w.im = sinf(phi);
     r->renorm_ctr = 0;
 }
+/* rotator.rs:35-39 set_freq: recompute w only (z and the renorm counter stay). */
+void o_rotator_set_freq(o_rotator *r, float freq_hz, float fs) {
+    float phi = O_TAU * freq_hz / fs;
+    r->w.re = cosf(phi); r->w.im = sinf(phi);
+}
 oc32 o_rotator_next(o_rotator *r) {
     float zr = fmaf(r->z.re, r->w.re, -(r->z.im * r->w.im));
     float zi = fmaf(r->z.im, r->w.re, r->z.re * r->w.im);
@@ -650,6 +655,49 @@ static inline size_t o_step(size_t chunk, size_t left) { return (chunk == 0 || c
 size_t o_run_rotator(float freq_hz, float fs, const oc32 *in, oc32 *out, size_t n, size_t chunk) {
     o_rotator r; o_rotator_init(&r, freq_hz, fs);
     for (size_t i = 0; i < n;) { size_t c = o_step(chunk, n - i); o_rotator_rotate_block(&r, in + i, out + i, c); i += c; }
+    return n;
+}
+/* Rotator with a retune mid-stream (rotator.rs:35-39: w changes, z stays): mode 0
+ * rotate_block (out: cf32), 1 mix_usb_block (out: f32, rotator.rs:88-94); set_freq(f2,
+ * fs2) after the first n_switch samples; reset_phase (rotator.rs:28-31) instead when
+ * reset_at_switch. */
+size_t o_run_rotator_retune(float f1, float fs, int mode, const oc32 *in, void *out, size_t n, size_t n_switch,
+                            float f2, float fs2, int reset_at_switch) {
+    o_rotator r; o_rotator_init(&r, f1, fs);
+    for (int part = 0; part < 2; part++) {
+        size_t a = part ? n_switch : 0, b = part ? n : (n_switch < n ? n_switch : n);
+        if (part) {
+            if (reset_at_switch) { r.z.re = 1.0f; r.z.im = 0.0f; r.renorm_ctr = 0; }
+            else o_rotator_set_freq(&r, f2, fs2);
+        }
+        if (b <= a) continue;
+        if (mode == 0) o_rotator_rotate_block(&r, in + a, (oc32 *)out + a, b - a);
+        else o_rotator_mix_usb_block(&r, in + a, (float *)out + a, b - a);
+    }
+    return n;
+}
+/* Nco (nco.rs): mode 0 mix_with_nco per sample (nco.rs:63-66), 1 next_cs (nco.rs:42-58)
+ * as (cos, sin) pairs (in unused); set_freq(f2) after n_switch samples. */
+size_t o_run_nco(float f1, float fs, int mode, const oc32 *in, oc32 *out, size_t n, size_t n_switch, float f2) {
+    o_nco q; o_nco_init(&q, f1, fs);
+    for (size_t i = 0; i < n; i++) {
+        if (i == n_switch) o_nco_set_freq(&q, f2);
+        if (mode == 0) out[i] = o_mix_with_nco(in[i], &q);
+        else { float cc, ss; o_nco_next_cs(&q, &cc, &ss); out[i].re = cc; out[i].im = ss; }
+    }
+    return n;
+}
+/* Biquad::new(b0, b1, b2, a1, a2) (iir.rs:15-41) over a stream. */
+size_t o_run_biquad(float b0, float b1, float b2, float a1, float a2, const float *in, float *out, size_t n) {
+    o_biquad b = {b0, b1, b2, a1, a2, 0.0f, 0.0f};
+    for (size_t i = 0; i < n; i++) out[i] = o_biquad_process(&b, in[i]);
+    return n;
+}
+/* LpDcCascade::design(fs, lp_fc, dc_cut) (iir.rs:111-137): process (:151-165), or
+ * process_mapped(x, f32::sqrt) (:170-186) when sqrt_map. */
+size_t o_run_lpdc(float fs, float lp_fc, float dc_cut, int sqrt_map, const float *in, float *out, size_t n) {
+    o_lpdc c; o_lpdc_design(&c, fs, lp_fc, dc_cut);
+    for (size_t i = 0; i < n; i++) out[i] = sqrt_map ? o_lpdc_process_mapped_sqrt(&c, in[i]) : o_lpdc_process(&c, in[i]);
     return n;
 }
 size_t o_run_fir(float fs, float pass_hz, float trans_hz, const float *in, float *out, size_t n, size_t chunk) {

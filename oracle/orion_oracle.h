@@ -40,6 +40,7 @@ float o_atan2_approx(float y, float x);
 typedef struct { oc32 z, w; uint32_t renorm_ctr; } o_rotator;
 void o_rotator_init(o_rotator *r, float freq_hz, float fs);
 oc32 o_rotator_next(o_rotator *r);
+void o_rotator_set_freq(o_rotator *r, float freq_hz, float fs);
 void o_rotator_rotate_block(o_rotator *r, const oc32 *in, oc32 *out, size_t n);
 void o_rotator_mix_usb_block(o_rotator *r, const oc32 *in, float *out, size_t n);
 
@@ -160,6 +161,11 @@ void o_add_awgn(oc32 *iq, size_t n, float noise_power, uint64_t seed);
  * exactly like repeated Block::process calls on one Rust instance.
  * ====================================================================== */
 size_t o_run_rotator(float freq_hz, float fs, const oc32 *in, oc32 *out, size_t n, size_t chunk);
+size_t o_run_rotator_retune(float f1, float fs, int mode, const oc32 *in, void *out, size_t n, size_t n_switch,
+                            float f2, float fs2, int reset_at_switch);
+size_t o_run_nco(float f1, float fs, int mode, const oc32 *in, oc32 *out, size_t n, size_t n_switch, float f2);
+size_t o_run_biquad(float b0, float b1, float b2, float a1, float a2, const float *in, float *out, size_t n);
+size_t o_run_lpdc(float fs, float lp_fc, float dc_cut, int sqrt_map, const float *in, float *out, size_t n);
 size_t o_run_fir(float fs, float pass_hz, float trans_hz, const float *in, float *out, size_t n, size_t chunk);
 size_t o_run_firiq(const float *taps, size_t ntaps, const oc32 *in, oc32 *out, size_t n, size_t chunk);
 void   o_run_firiq_aligned(const float *taps, size_t ntaps, oc32 *io, size_t n);

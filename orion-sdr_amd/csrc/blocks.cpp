@@ -33,11 +33,32 @@ void DevBuf::upload(const void* h, size_t bytes, hipStream_t s) {
 // ------------------------------------------------------------------- Block --
 Block::~Block() {
   if (hs_) (void)hipStreamDestroy(hs_);
+  if (err_) (void)hipHostFree(err_);
 }
 hipStream_t Block::host_stream() {
   if (!hs_) ORION_HIP(hipStreamCreateWithFlags(&hs_, hipStreamNonBlocking));
   return hs_;
 }
+int* Block::dev_err() {
+  if (!err_) {
+    void* p = nullptr;
+    ORION_HIP(hipHostMalloc(&p, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+    err_ = static_cast<int*>(p);
+    __atomic_store_n(err_, 0, __ATOMIC_RELAXED);
+  }
+  return err_;
+}
+void Block::check_device_errors() {
+  if (err_ && __atomic_exchange_n(err_, 0, __ATOMIC_ACQ_REL) != 0)
+    throw HipError(std::string(name()) +
+                   ": a cross-workgroup wait of an earlier kernel of this handle timed out; its output is invalid");
+}
+
+namespace {
+uint32_t g_spin = kSpinDefault;
+}
+uint32_t spin_limit() { return __atomic_load_n(&g_spin, __ATOMIC_RELAXED); }
+void set_spin_limit(uint32_t polls) { __atomic_store_n(&g_spin, polls, __ATOMIC_RELAXED); }
 
 WorkReport Block::process_host(const void* in, size_t n_in, void* out, size_t out_cap) {
   hipStream_t s = host_stream();
@@ -84,30 +105,74 @@ int padded_hist(int K) {
   return K;
 }
 
-// -------------------------------------------------------------- Rotator ----
-class RotatorBlock final : public Block {
+// ------------------------------------------------------ Rotator / Nco ----
+// The oscillator in closed form: after k steps the phasor is e^{j 2 pi ph(k) / 2^64},
+// ph(k) = base + k step (Q0.64, exact integer arithmetic), step = the exact angle of
+// the reference's f32 step phasor w (design.cpp oscillator). Retuning keeps the
+// phase (the reference keeps z and replaces w): base += k (step_old - step_new).
+class OscBlock : public Block {
  public:
-  RotatorBlock(float f, float fs) : osc_(oscillator(f, fs)) {
+  OscBlock(float f, float fs) : fs_(fs) { tune(f, fs); }
+  void reset() override {  // phasor back to 1 + 0j (Rotator::reset_phase, rotator.rs:28-31)
+    k_ = 0;
+    base_ = 0;
+  }
+  std::vector<float> taps(int) const override { return {osc_.w_re, osc_.w_im}; }
+  void set_freq(float f, float fs) {
+    const Oscillator o = oscillator(f, fs);
+    base_ += k_ * (osc_.step_q64 - o.step_q64);
+    ORION_HIP(hipDeviceSynchronize());  // kernels in flight may read the old table
+    tune(f, fs);
+  }
+  float fs() const { return fs_; }
+  // One oscillator pass (launch_osc mode) over n samples, advancing the phase.
+  void run(int mode, const void* in, void* out, size_t n, hipStream_t s) {
+    launch_osc(mode, static_cast<const f2*>(in), out, static_cast<long long>(n), k_, osc_.step_q64, base_,
+               tab_.as<f2>(), s);
+    k_ += n;
+  }
+
+ private:
+  void tune(float f, float fs) {
+    osc_ = oscillator(f, fs);
+    fs_ = fs;
     const auto tab = phasor_table(osc_.theta, kRotTile);
     tab_.upload(tab.data(), tab.size() * sizeof(float));
   }
+  float fs_;
+  Oscillator osc_{};
+  DevBuf tab_;
+  uint64_t k_ = 0, base_ = 0;
+};
+
+// dsp/rotator.rs:8-95: process = rotate_block (cf32 -> cf32); mix_usb_block on the
+// same phasor (osc_mix_usb).
+class RotatorBlock final : public OscBlock {
+ public:
+  RotatorBlock(float f, float fs) : OscBlock(f, fs) {}
   const char* name() const override { return "Rotator"; }
   Dt in_type() const override { return Dt::C32; }
   Dt out_type() const override { return Dt::C32; }
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const size_t n = std::min(n_in, out_cap);  // rotator.rs:76
-    launch_rotator(static_cast<const f2*>(in), static_cast<f2*>(out), static_cast<long long>(n), k_,
-                   osc_.step_q64, tab_.as<f2>(), s);
-    k_ += n;
+    run(0, in, out, n, s);
     return {n, n};
   }
-  void reset() override { k_ = 0; }  // Rotator::reset_phase (rotator.rs:29-32)
-  std::vector<float> taps(int) const override { return {osc_.w_re, osc_.w_im}; }
+};
 
- private:
-  Oscillator osc_;
-  DevBuf tab_;
-  uint64_t k_ = 0;
+// dsp/nco.rs:11-66: process = mix_with_nco per sample (cf32 -> cf32, the non-FMA
+// product); next_cs as a block of phasors (osc_next_cs).
+class NcoBlock final : public OscBlock {
+ public:
+  NcoBlock(float f, float fs) : OscBlock(f, fs) {}
+  const char* name() const override { return "Nco"; }
+  Dt in_type() const override { return Dt::C32; }
+  Dt out_type() const override { return Dt::C32; }
+  WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
+    const size_t n = std::min(n_in, out_cap);
+    run(2, in, out, n, s);
+    return {n, n};
+  }
 };
 
 // ------------------------------------------------------ analog modulators --
@@ -135,6 +200,31 @@ class AmModBlock final : public Block {
   Oscillator osc_;
   float cl_, mi_, g_ = 1.0f;
   bool clamp_ = false;
+  uint64_t k_ = 0;
+};
+
+// modulate/pm.rs:9-47 PmDirectPhaseMod. F32 audio -> C32 IQ.
+class PmModBlock final : public Block {
+ public:
+  PmModBlock(float fs, float kp, float rf_hz) : osc_(oscillator(rf_hz, fs)), kp_(kp) {}
+  const char* name() const override { return "PmDirectPhaseMod"; }
+  Dt in_type() const override { return Dt::F32; }
+  Dt out_type() const override { return Dt::C32; }
+  WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
+    const size_t n = std::min(n_in, out_cap);  // pm.rs:37
+    launch_pm_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), k_, osc_.step_q64,
+                  kp_, g_, s);
+    k_ += n;
+    return {n, n};
+  }
+  void reset() override { k_ = 0; }
+  void set_gain(float g) { g_ = g; }          // pm.rs:24-26
+  void set_sensitivity(float kp) { kp_ = kp; }  // pm.rs:27-29
+  std::vector<float> taps(int) const override { return {kp_, osc_.w_re, osc_.w_im}; }
+
+ private:
+  Oscillator osc_;
+  float kp_, g_ = 1.0f;
   uint64_t k_ = 0;
 };
 
@@ -168,7 +258,8 @@ class FmModBlock final : public Block {
         epoch_ = 1;
       }
       launch_fm_mod_sp(static_cast<const float*>(in), static_cast<f2*>(out), nn, kf, g_, rec_.as<uint32_t>(), epoch_,
-                       carry_[cur_].as<double>(), carry_[cur_ ^ 1].as<double>(), k_, osc_.step_q64, rtab_.as<f2>(), s);
+                       carry_[cur_].as<double>(), carry_[cur_ ^ 1].as<double>(), k_, osc_.step_q64, rtab_.as<f2>(),
+                       dev_err(), s);
       cur_ ^= 1;
       k_ += n;
       return {n, n};
@@ -189,6 +280,12 @@ class FmModBlock final : public Block {
   }
   void set_gain(float g) { g_ = g; }           // fm.rs:37-39
   void set_deviation(float d) { dev_ = d; }    // fm.rs:34-36
+  int configure(int option, long long value) override {
+    if (option != kOptModPasses) return -4;
+    if (value != 0 && value != 1 && value != 3) return -3;
+    single_pass_ = value != 3;
+    return 0;
+  }
   std::vector<float> taps(int) const override { return {kTauF * dev_ / fs_, osc_.w_re, osc_.w_im}; }
 
  private:
@@ -198,11 +295,7 @@ class FmModBlock final : public Block {
   int cur_ = 0;
   uint64_t k_ = 0;
   uint32_t epoch_ = 0;
-  // single-pass phase scan (k_fm_mod_sp); ORION_FM_MOD_3P=1 keeps the three passes
-  bool single_pass_ = [] {
-    const char* e = std::getenv("ORION_FM_MOD_3P");
-    return !(e && std::atoi(e) == 1);
-  }();
+  bool single_pass_ = true;  // k_fm_mod_sp, or the three passes (orion_block_configure)
 };
 
 // --------------------------------------------------------- FirDecimator ----
@@ -418,24 +511,7 @@ class WbfmBlock final : public Block {
       std::copy(m.begin(), m.end(), lm.begin() + L * 16);
     }
     lanemats_.upload(lm.data(), lm.size() * sizeof(double));
-    // fused chain constants: chunks of kFuC per lane, halves of kFuL/2
-    std::memset(&cu_, 0, sizeof(cu_));
-    for (size_t k = 0; k < a.size(); ++k) cu_.a[k] = a[k];
-    cu_.b0 = bq.b0; cu_.b1 = bq.b1; cu_.b2 = bq.b2; cu_.a1 = bq.a1; cu_.a2 = bq.a2;
-    auto pf = mat_pow(ss.A, 4, kFuC);
-    for (int s = 0; s < 6; ++s) {
-      for (int i = 0; i < 16; ++i) cu_.pw[s * 16 + i] = pf[i];
-      pf = mat_mul(pf, pf, 4);
-    }
-    const auto mh = mat_pow(ss.A, 4, kFuL / 2);
-    for (int i = 0; i < 16; ++i) cu_.mh[i] = mh[i];
-    std::vector<double> lf(64 * 16);
-    for (int L = 0; L < 64; ++L) {
-      const auto m = mat_pow(ss.A, 4, static_cast<uint64_t>(kFuC) * L);
-      std::copy(m.begin(), m.end(), lf.begin() + L * 16);
-    }
-    lanemats_fu_.upload(lf.data(), lf.size() * sizeof(double));
-    // segmented chain constants: chunks of kSgC per lane, halves of kSgL/2
+    // segmented chain constants: steps A^(kSgC 2^s), and A^(kSgL/2)
     std::memset(&cs_, 0, sizeof(cs_));
     for (size_t k = 0; k < a.size(); ++k) cs_.a[k] = a[k];
     cs_.b0 = bq.b0; cs_.b1 = bq.b1; cs_.b2 = bq.b2; cs_.a1 = bq.a1; cs_.a2 = bq.a2;
@@ -446,12 +522,6 @@ class WbfmBlock final : public Block {
     }
     const auto msh = mat_pow(ss.A, 4, kSgL / 2);
     for (int i = 0; i < 16; ++i) cs_.mh[i] = msh[i];
-    std::vector<double> ls(64 * 16);
-    for (int L = 0; L < 64; ++L) {
-      const auto m = mat_pow(ss.A, 4, static_cast<uint64_t>(kSgC) * L);
-      std::copy(m.begin(), m.end(), ls.begin() + L * 16);
-    }
-    lanemats_sg_.upload(ls.data(), ls.size() * sizeof(double));
     // The segmented chain starts every segment's first sub-range from a zero
     // state and hands the next sub-range that sub-range's zero-state end state
     // and last 128 outputs: exact when A^(kSgL - 128) is below f32 resolution
@@ -462,19 +532,6 @@ class WbfmBlock final : public Block {
       for (double v : m) fro += v * v;
       seg_ok_ = std::sqrt(fro) < 1e-10;
     }
-    // The fused chain hands each range only its predecessor's zero-state IIR
-    // aggregate, exact when A^kFuL (the state carried across one whole range)
-    // is below f32 resolution relative to A^0 = I; the 4th-order Butterworth at
-    // fc/fs2 = 0.0108 (the WBFM defaults) has ||A^1024|| ~ 1e-19. Otherwise the
-    // two-kernel path (510-sample warm-up per 2048) is used; see DESIGN.md.
-    {
-      const auto m = mat_pow(ss.A, 4, kFuL);
-      double fro = 0.0;
-      for (double v : m) fro += v * v;
-      fused_ok_ = std::sqrt(fro) < 1e-12;
-    }
-    err_.resize(sizeof(int));
-    err_.zero();
     std::vector<uint64_t> steps(nch_);
     std::vector<float> tabs;
     tabs.reserve(static_cast<size_t>(nch_) * kWbfmNS * 2);
@@ -508,13 +565,10 @@ class WbfmBlock final : public Block {
       ORION_HIP(hipMemcpyAsync(carry_[nxt].as<void>(), carry_[cur_].as<void>(), carry_[cur_].size(),
                                hipMemcpyDeviceToDevice, s));
     } else {
-      phi_.resize(static_cast<size_t>(nch_) * n_dec * sizeof(float) + 64);
       WbfmArgs a{};
       a.x = static_cast<const f2*>(in);
       a.x_stride = static_cast<long long>(n);
       a.n = static_cast<long long>(n);
-      a.phi = phi_.as<float>();
-      a.phi_stride = static_cast<long long>(n_dec);
       a.y = static_cast<float*>(out);
       a.y_stride = static_cast<long long>(out_cap);
       a.n_dec = static_cast<long long>(n_dec);
@@ -526,42 +580,20 @@ class WbfmBlock final : public Block {
       a.hist_in = hist_[cur_].as<f2>();
       a.hist_out = hist_[nxt].as<f2>();
       a.lanemats = lanemats_.as<double>();
-      int path = path_;
-      if (path == kPathAuto) {
-        static const char* env = std::getenv("ORION_WBFM_PATH");  // timing experiments
-        path = seg_ok_ ? kPathSeg4 : kPathSplit;
-        if (env && std::strcmp(env, "seg2") == 0 && seg_ok_) path = kPathSeg2;
-        if (env && std::strcmp(env, "split") == 0) path = kPathSplit;
-        if (env && std::strcmp(env, "fused") == 0 && fused_ok_) path = kPathRange;
-        if (env && std::strcmp(env, "seg") == 0 && seg_ok_) path = kPathSeg;
-        if (env && std::strcmp(env, "ws") == 0 && seg_ok_) path = kPathWs;
-        if (env && std::strcmp(env, "seg3") == 0 && seg_ok_) path = kPathSeg3;
-        if (env && std::strcmp(env, "seg4") == 0 && seg_ok_) path = kPathSeg4;
-      }
-      const bool seg = path == kPathSeg || path == kPathSeg2 || path == kPathSeg3 || path == kPathSeg4 || path == kPathWs;
-      const bool fused = seg || path == kPathRange;
-      if (fused) {
-        const long long slots = seg ? wbfm_seg_slots(static_cast<long long>(n_dec), nch_)
-                                    : wbfm_fused_slots(static_cast<long long>(n_dec), nch_);
-        const size_t words = path == kPathSeg4 ? kSeg4Slot
-                            : (path == kPathSeg2 || path == kPathSeg3 || path == kPathWs) ? kSg2Slot : kFuSlot;
-        if (static_cast<size_t>(slots) * words * 4 > hand_.size()) hand_.resize(static_cast<size_t>(slots) * words * 4);
+      const int path = path_ == kPathAuto ? (seg_ok_ ? kPathSeg : kPathSplit) : path_;
+      if (path == kPathSeg) {
+        const long long slots = wbfm_seg_slots(static_cast<long long>(n_dec), nch_);
+        if (static_cast<size_t>(slots) * kSeg4Slot * 4 > hand_.size()) hand_.resize(static_cast<size_t>(slots) * kSeg4Slot * 4);
         if (static_cast<size_t>(slots) * 3 * 4 > flags_.size()) {
           flags_.resize(static_cast<size_t>(slots) * 3 * 4);
           flags_.zero(s);  // epochs start at 1: a zeroed flag never matches
         }
-        a.lanemats_fu = lanemats_fu_.as<double>();
-        a.lanemats_sg = lanemats_sg_.as<double>();
         a.hand = hand_.as<uint32_t>();
         a.flags = flags_.as<uint32_t>();
-        a.err = err_.as<int>();
+        a.err = dev_err();
+        a.spin = spin_limit();
         a.epoch = ++epoch_;
-        static const int fu_abl = [] {
-          const char* e = std::getenv("ORION_WBFM_FUABL");  // timing ablations only
-          return e ? std::atoi(e) : 0;
-        }();
-        a.fu_abl = fu_abl;
-        static const char* trace_path = std::getenv("ORION_WBFM_TRACE");  // debug: phase timestamps
+        static const char* trace_path = std::getenv("ORION_WBFM_TRACE");  // debug only: per-wave phase timestamps
         if (trace_path) {
           trace_.resize(static_cast<size_t>(slots) * kFuTracePoints * 8);
           trace_.zero(s);
@@ -571,11 +603,7 @@ class WbfmBlock final : public Block {
           flags_.zero(s);
           epoch_ = 0;
         }
-        if (path == kPathWs) launch_wbfm_ws(a, cf_, cs_, nch_, max_seg_, s);
-        else if (seg)
-          launch_wbfm_seg(a, cf_, cs_, nch_, max_seg_,
-                          path == kPathSeg4 ? 3 : path == kPathSeg3 ? 2 : path == kPathSeg2 ? 1 : 0, s);
-        else launch_wbfm_fused(a, cf_, cu_, nch_, s);
+        launch_wbfm_seg(a, cf_, cs_, nch_, max_seg_, s);
         if (trace_path) {  // debug: dump this launch's timestamps (overwrites: last launch wins)
           std::vector<long long> h(static_cast<size_t>(slots) * kFuTracePoints);
           ORION_HIP(hipMemcpyAsync(h.data(), trace_.as<void>(), h.size() * 8, hipMemcpyDeviceToHost, s));
@@ -586,6 +614,9 @@ class WbfmBlock final : public Block {
           }
         }
       } else {
+        phi_.resize(static_cast<size_t>(nch_) * n_dec * sizeof(float) + 64);
+        a.phi = phi_.as<float>();
+        a.phi_stride = static_cast<long long>(n_dec);
         launch_wbfm(a, cf_, cb_, nch_, s);
       }
     }
@@ -606,22 +637,12 @@ class WbfmBlock final : public Block {
   }
   std::vector<float> taps(int which) const override { return which == 0 ? h_dec_ : h_aud_; }
   void seek(uint64_t index) { k0_ = index; }
-  int configure(int path, int max_seg) {
-    if (path < kPathAuto || path > kPathSeg4 || max_seg < 0) return -3;
-    if ((path == kPathSeg2 || path == kPathSeg || path == kPathWs || path == kPathSeg3 || path == kPathSeg4) && !seg_ok_)
-      return -3;
-    if (path == kPathRange && !fused_ok_) return -3;
+  int set_path(int path, int max_seg) {
+    if ((path != kPathAuto && path != kPathSeg && path != kPathSplit) || max_seg < 0) return -3;
+    if (path == kPathSeg && !seg_ok_) return -3;
     path_ = path;
     max_seg_ = max_seg;
     return 0;
-  }
-  void check_device_errors() override {
-    int e = 0;
-    ORION_HIP(hipMemcpy(&e, err_.as<void>(), sizeof(int), hipMemcpyDeviceToHost));
-    if (e) {
-      err_.zero();
-      throw HipError("WBFM fused chain: a range hand-off wait timed out");
-    }
   }
 
  private:
@@ -630,11 +651,11 @@ class WbfmBlock final : public Block {
   std::vector<float> h_dec_, h_aud_;
   WbfmFrontConst cf_;
   WbfmBackConst cb_;
-  WbfmFusedConst cu_, cs_;
-  bool fused_ok_ = false, seg_ok_ = false;
+  WbfmFusedConst cs_;
+  bool seg_ok_ = false;
   int path_ = kPathAuto, max_seg_ = 0;
   uint32_t epoch_ = 0;
-  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, lanemats_fu_, lanemats_sg_, hand_, flags_, err_, trace_;
+  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, hand_, flags_, trace_;
   int cur_ = 0;
   uint64_t k0_ = 0;
 };
@@ -642,6 +663,31 @@ class WbfmBlock final : public Block {
 }  // namespace
 
 std::unique_ptr<Block> make_rotator(float f, float fs) { return std::make_unique<RotatorBlock>(f, fs); }
+std::unique_ptr<Block> make_nco(float f, float fs) { return std::make_unique<NcoBlock>(f, fs); }
+int osc_set_freq(Block* b, const char* kind, float f, float fs) {
+  auto* o = dynamic_cast<OscBlock*>(b);
+  if (!o || std::strcmp(b->name(), kind) != 0) return -4;
+  o->set_freq(f, fs > 0.0f ? fs : o->fs());
+  return 0;
+}
+int osc_reset_phase(Block* b) {
+  auto* o = dynamic_cast<RotatorBlock*>(b);
+  if (!o) return -4;
+  o->reset();
+  return 0;
+}
+int osc_mix_usb(Block* b, const void* in, size_t n, float* out, hipStream_t s) {
+  auto* o = dynamic_cast<RotatorBlock*>(b);
+  if (!o) return -4;
+  o->run(1, in, out, n, s);
+  return 0;
+}
+int osc_next_cs(Block* b, void* out, size_t n, hipStream_t s) {
+  auto* o = dynamic_cast<NcoBlock*>(b);
+  if (!o) return -4;
+  o->run(3, nullptr, out, n, s);
+  return 0;
+}
 std::unique_ptr<Block> make_am_mod(float fs, float rf_hz, float cl, float mi) {
   return std::make_unique<AmModBlock>(fs, rf_hz, cl, mi);
 }
@@ -651,7 +697,15 @@ std::unique_ptr<Block> make_fm_mod(float fs, float dev_hz, float rf_hz) {
 int mod_set_gain(Block* b, float g) {
   if (auto* a = dynamic_cast<AmModBlock*>(b)) { a->set_gain(g); return 0; }
   if (auto* f = dynamic_cast<FmModBlock*>(b)) { f->set_gain(g); return 0; }
-  return -4;
+  if (auto* p = dynamic_cast<PmModBlock*>(b)) { p->set_gain(g); return 0; }
+  return cw_mod_set_gain(b, g);
+}
+std::unique_ptr<Block> make_pm_mod(float fs, float kp, float rf_hz) { return std::make_unique<PmModBlock>(fs, kp, rf_hz); }
+int pm_mod_set_sensitivity(Block* b, float kp) {
+  auto* p = dynamic_cast<PmModBlock*>(b);
+  if (!p) return -4;
+  p->set_sensitivity(kp);
+  return 0;
 }
 int am_mod_set_clamp(Block* b, bool on) {
   auto* a = dynamic_cast<AmModBlock*>(b);
@@ -686,7 +740,7 @@ std::unique_ptr<Block> make_wbfm_chain(const WbfmParams& p, const std::vector<fl
 int wbfm_chain_configure(Block* b, int path, int max_segments) {
   auto* w = dynamic_cast<WbfmBlock*>(b);
   if (!w) return -4;
-  return w->configure(path, max_segments);
+  return w->set_path(path, max_segments);
 }
 
 int wbfm_chain_seek(Block* b, unsigned long long index) {

@@ -20,6 +20,8 @@
 namespace orion {
 
 enum class Dt : int { C32 = 0, F32 = 1 };
+// orion_block_configure options (include/orion_sdr_amd.h ORION_OPT_*).
+enum : int { kOptScanPath = 1, kOptModPasses = 2 };
 inline size_t dt_size(Dt d) { return d == Dt::C32 ? 8 : 4; }
 
 struct WorkReport {
@@ -61,8 +63,11 @@ class Block {
                                     hipStream_t s) = 0;
   // Host buffers: stage through device memory, synchronous.
   WorkReport process_host(const void* in, size_t n_in, void* out, size_t out_cap);
-  // Errors a kernel could only flag in device memory (read after a sync).
-  virtual void check_device_errors() {}
+  // Errors a kernel flagged in the handle's device error word (a cross-workgroup
+  // wait that timed out): throws HipError and clears the word if one is set. The
+  // word is host-visible (pinned, coherent), so this needs no sync; it sees every
+  // kernel of the handle that has finished (orion_block_status).
+  void check_device_errors();
   virtual void reset() = 0;
   virtual int channels() const { return 1; }
   // process_device may be given overlapping in/out ranges (the block stages its
@@ -70,17 +75,34 @@ class Block {
   virtual bool alias_ok() const { return false; }
   // Designed coefficients (for tests): which = 0 primary taps, 1 secondary.
   virtual std::vector<float> taps(int which) const { (void)which; return {}; }
+  // Engine options (include/orion_sdr_amd.h orion_block_configure): 0 set, -3 bad
+  // value, -4 option not known to this block.
+  virtual int configure(int option, long long value) { (void)option; (void)value; return -4; }
 
  protected:
   hipStream_t host_stream();
+  // The handle's device error word (host-pinned, coherent; allocated on first use):
+  // kernels set it with system-scope stores, the host reads it without a sync.
+  int* dev_err();
   DevBuf stage_in_, stage_out_;
 
  private:
   hipStream_t hs_ = nullptr;
+  int* err_ = nullptr;
 };
 
 // dsp/rotator.rs:8-95 (rotate_block). C32 -> C32.
 std::unique_ptr<Block> make_rotator(float freq_hz, float fs);
+// dsp/nco.rs:11-66 (mix_with_nco per sample). C32 -> C32.
+std::unique_ptr<Block> make_nco(float freq_hz, float fs);
+// Oscillator controls (-4 if b is not of that kind): set_freq (Rotator: rotator.rs:35-39,
+// kind "Rotator"; Nco: nco.rs:33-38, kind "Nco", fs <= 0 keeps the block's fs), reset_phase
+// (rotator.rs:28-31), mix_usb_block (rotator.rs:88-94, C32 -> F32 on device buffers) and
+// next_cs n times (nco.rs:42-58, C32 phasors on device buffers), asynchronous on s.
+int osc_set_freq(Block* b, const char* kind, float freq_hz, float fs);
+int osc_reset_phase(Block* b);
+int osc_mix_usb(Block* b, const void* in_dev, size_t n, float* out_dev, hipStream_t s);
+int osc_next_cs(Block* b, void* out_dev, size_t n, hipStream_t s);
 // dsp/decim.rs:10-77. C32 -> C32, out = ceil(n/m) (decimation phase restarts
 // every call, decim.rs:66-71 — reproduced).
 std::unique_ptr<Block> make_fir_decimator(float fs, size_t m, float cutoff_hz, float trans_hz,
@@ -96,7 +118,11 @@ int fir_lowpass_iq_filter_aligned(Block* b, void* io_dev, size_t n, hipStream_t 
 // Analog modulators. F32 audio -> C32 IQ.
 std::unique_ptr<Block> make_am_mod(float fs, float rf_hz, float carrier_level, float modulation_index);  // am.rs
 std::unique_ptr<Block> make_fm_mod(float fs, float deviation_hz, float rf_hz);                         // fm.rs
-int mod_set_gain(Block* b, float g);             // AmDsbMod / FmPhaseAccumMod set_gain; -4 other blocks
+std::unique_ptr<Block> make_pm_mod(float fs, float kp, float rf_hz);                                   // pm.rs
+std::unique_ptr<Block> make_cw_mod(float fs, float tone_hz, float rise_ms, float fall_ms);             // cw.rs
+int mod_set_gain(Block* b, float g);             // Am / Fm / Pm / Cw modulator set_gain; -4 other blocks
+int cw_mod_set_gain(Block* b, float g);          // -4 if not a CwKeyedMod
+int pm_mod_set_sensitivity(Block* b, float kp);  // -4 if not a PmDirectPhaseMod
 int am_mod_set_clamp(Block* b, bool on);         // -4 if not an AmDsbMod
 int fm_mod_set_deviation(Block* b, float d);     // -4 if not an FmPhaseAccumMod
 std::unique_ptr<Block> make_agc(bool iq, float fs, float attack_ms, float release_ms, float target_rms);  // agc.rs
@@ -110,10 +136,10 @@ struct WbfmParams {
 };
 std::unique_ptr<Block> make_wbfm_chain(const WbfmParams& p, const std::vector<float>& f_off);
 // Kernel path of a WBFM chain (tests and timing; include/orion_sdr_amd.h
-// orion_wbfm_chain_configure). max_segments > 0 caps the segmented kernels'
+// orion_wbfm_chain_configure). max_segments > 0 caps the segmented kernel's
 // waves (default: the resident capacity). Returns -4 if b is not a WBFM chain,
 // -3 if this design cannot run on that path.
-enum : int { kPathAuto = 0, kPathSeg2 = 1, kPathRange = 2, kPathSplit = 3, kPathSeg = 4, kPathWs = 5, kPathSeg3 = 6, kPathSeg4 = 7 };
+enum : int { kPathAuto = 0, kPathSeg = 1, kPathSplit = 3 };
 int wbfm_chain_configure(Block* b, int path, int max_segments);
 // Absolute index of the next input sample (the NCO phase origin) of a WBFM
 // chain: a time-sharded stream starts each shard's handle at its halo start

@@ -1,6 +1,7 @@
 // capi.cpp — extern "C" boundary (include/orion_sdr_amd.h) over the Block layer.
 #include "../../include/orion_sdr_amd.h"
 
+#include <algorithm>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -90,6 +91,78 @@ int orion_synchronize(void* stream) {
 orion_block* orion_rotator_new(float freq_hz, float fs) {
   return make([&] { return orion::make_rotator(freq_hz, fs); });
 }
+orion_block* orion_nco_new(float freq_hz, float fs) {
+  return make([&] { return orion::make_nco(freq_hz, fs); });
+}
+int orion_rotator_set_freq(orion_block* b, float freq_hz, float fs) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    if (orion::osc_set_freq(b->impl.get(), "Rotator", freq_hz, fs)) return fail(ORION_E_TYPE, "not a Rotator");
+    return ORION_OK;
+  });
+}
+int orion_rotator_reset_phase(orion_block* b) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    if (orion::osc_reset_phase(b->impl.get())) return fail(ORION_E_TYPE, "not a Rotator");
+    return ORION_OK;
+  });
+}
+int orion_rotator_mix_usb_block_device(orion_block* b, const void* in, size_t n_in, float* out, size_t out_cap,
+                                       void* stream, orion_work_report* wr) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  if ((!in && n_in) || (!out && out_cap)) return fail(ORION_E_NULL, "null buffer");
+  return guarded([&] {
+    b->impl->check_device_errors();
+    const size_t n = std::min(n_in, out_cap);  // rotator.rs:89
+    if (orion::osc_mix_usb(b->impl.get(), in, n, out, static_cast<hipStream_t>(stream)))
+      return fail(ORION_E_TYPE, "not a Rotator");
+    if (wr) { wr->in_read = n; wr->out_written = n; }
+    return ORION_OK;
+  });
+}
+int orion_rotator_mix_usb_block(orion_block* b, const void* in, size_t n_in, float* out, size_t out_cap,
+                                orion_work_report* wr) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  if ((!in && n_in) || (!out && out_cap)) return fail(ORION_E_NULL, "null buffer");
+  return guarded([&] {
+    const size_t n = std::min(n_in, out_cap);
+    orion::DevBuf di(n * 8 + 16), dout(n * 4 + 16);
+    if (n) ORION_HIP(hipMemcpy(di.as<void>(), in, n * 8, hipMemcpyHostToDevice));
+    if (orion::osc_mix_usb(b->impl.get(), di.as<void>(), n, dout.as<float>(), nullptr))
+      return fail(ORION_E_TYPE, "not a Rotator");
+    if (n) ORION_HIP(hipMemcpy(out, dout.as<void>(), n * 4, hipMemcpyDeviceToHost));
+    ORION_HIP(hipDeviceSynchronize());
+    if (wr) { wr->in_read = n; wr->out_written = n; }
+    return ORION_OK;
+  });
+}
+int orion_nco_set_freq(orion_block* b, float freq_hz) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    if (orion::osc_set_freq(b->impl.get(), "Nco", freq_hz, 0.0f)) return fail(ORION_E_TYPE, "not an Nco");
+    return ORION_OK;
+  });
+}
+int orion_nco_next_cs_block_device(orion_block* b, void* out, size_t n, void* stream) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  if (!out && n) return fail(ORION_E_NULL, "null buffer");
+  return guarded([&] {
+    if (orion::osc_next_cs(b->impl.get(), out, n, static_cast<hipStream_t>(stream))) return fail(ORION_E_TYPE, "not an Nco");
+    return ORION_OK;
+  });
+}
+int orion_nco_next_cs_block(orion_block* b, void* out, size_t n) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  if (!out && n) return fail(ORION_E_NULL, "null buffer");
+  return guarded([&] {
+    orion::DevBuf d(n * 8 + 16);
+    if (orion::osc_next_cs(b->impl.get(), d.as<void>(), n, nullptr)) return fail(ORION_E_TYPE, "not an Nco");
+    if (n) ORION_HIP(hipMemcpy(out, d.as<void>(), n * 8, hipMemcpyDeviceToHost));
+    ORION_HIP(hipDeviceSynchronize());
+    return ORION_OK;
+  });
+}
 orion_block* orion_fir_decimator_new(float fs, size_t m, float cutoff_hz, float trans_hz) {
   return make([&] { return orion::make_fir_decimator(fs, m, cutoff_hz, trans_hz, 1); });
 }
@@ -157,11 +230,49 @@ int orion_fm_phase_accum_mod_set_gain(orion_block* b, float g) {
   if (std::strcmp(b->impl->name(), "FmPhaseAccumMod") != 0) return fail(ORION_E_TYPE, "not an FmPhaseAccumMod");
   return guarded([&] { return orion::mod_set_gain(b->impl.get(), g); });
 }
+orion_block* orion_pm_direct_phase_mod_new(float fs, float kp_rad_per_unit, float rf_hz) {
+  return make([&] { return orion::make_pm_mod(fs, kp_rad_per_unit, rf_hz); });
+}
+int orion_pm_direct_phase_mod_set_gain(orion_block* b, float g) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  if (std::strcmp(b->impl->name(), "PmDirectPhaseMod") != 0) return fail(ORION_E_TYPE, "not a PmDirectPhaseMod");
+  return guarded([&] { return orion::mod_set_gain(b->impl.get(), g); });
+}
+int orion_pm_direct_phase_mod_set_sensitivity(orion_block* b, float kp_rad_per_unit) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    if (orion::pm_mod_set_sensitivity(b->impl.get(), kp_rad_per_unit)) return fail(ORION_E_TYPE, "not a PmDirectPhaseMod");
+    return ORION_OK;
+  });
+}
+orion_block* orion_cw_keyed_mod_new(float fs, float tone_hz, float rise_ms, float fall_ms) {
+  return make([&] { return orion::make_cw_mod(fs, tone_hz, rise_ms, fall_ms); });
+}
+int orion_cw_keyed_mod_set_gain(orion_block* b, float g) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    if (orion::cw_mod_set_gain(b->impl.get(), g)) return fail(ORION_E_TYPE, "not a CwKeyedMod");
+    return ORION_OK;
+  });
+}
 orion_block* orion_ssb_phasing_mod_new(float fs, float audio_bw_hz, float audio_if_hz, float rf_hz, int usb) {
   return make([&] { return orion::make_ssb_mod(fs, audio_bw_hz, audio_if_hz, rf_hz, usb != 0); });
 }
 orion_block* orion_lp_cascade_new(float fs, float fc) {
   return make([&] { return orion::make_lp_cascade(fs, fc); });
+}
+orion_block* orion_biquad_new(float b0, float b1, float b2, float a1, float a2) {
+  return make([&] { return orion::make_biquad(b0, b1, b2, a1, a2); });
+}
+orion_block* orion_lp_dc_cascade_new(float fs, float lp_fc, float dc_cut_hz) {
+  return make([&] { return orion::make_lp_dc_cascade(fs, lp_fc, dc_cut_hz); });
+}
+int orion_lp_dc_cascade_set_sqrt_map(orion_block* b, int on) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    if (orion::lp_dc_cascade_set_sqrt(b->impl.get(), on != 0)) return fail(ORION_E_TYPE, "not an LpDcCascade");
+    return ORION_OK;
+  });
 }
 orion_block* orion_dc_blocker_new(float fs, float cut_hz) {
   return make([&] { return orion::make_dc_blocker(fs, cut_hz); });
@@ -248,11 +359,30 @@ int orion_block_process_device(orion_block* b, const void* in, size_t n_in, void
     const char *ip = static_cast<const char*>(in), *op = static_cast<const char*>(out);
     if (ib && ob && ip < op + ob && op < ip + ib && !blk.alias_ok())
       return fail(ORION_E_ARG, "input and output device ranges overlap (not supported by this block)");
+    b->impl->check_device_errors();  // a wait that timed out in an earlier call of this handle
     const orion::WorkReport w = b->impl->process_device(in, n_in, out, out_cap, static_cast<hipStream_t>(stream));
     if (wr) { wr->in_read = w.in_read; wr->out_written = w.out_written; }
     return ORION_OK;
   });
 }
+int orion_block_configure(orion_block* b, int option, long long value) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    const int rc = b->impl->configure(option, value);
+    if (rc == -4) return fail(ORION_E_TYPE, "option not supported by this block");
+    if (rc != 0) return fail(ORION_E_ARG, "bad option value");
+    return ORION_OK;
+  });
+}
+int orion_block_status(orion_block* b) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  return guarded([&] {
+    b->impl->check_device_errors();
+    return ORION_OK;
+  });
+}
+void orion_debug_set_spin_limit(uint32_t polls) { orion::set_spin_limit(polls); }
+uint32_t orion_debug_spin_limit(void) { return orion::spin_limit(); }
 int orion_block_reset(orion_block* b) {
   if (!b) return fail(ORION_E_NULL, "null handle");
   return guarded([&] {

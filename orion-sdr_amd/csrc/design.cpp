@@ -182,6 +182,14 @@ StateSpace lp_cascade_ss(const BiquadCoeffs& c) {
   return ss;
 }
 
+StateSpace biquad_ss(const BiquadCoeffs& c) {  // iir.rs:34-40, state (z1, z2)
+  StateSpace ss;
+  ss.S = 2;
+  ss.A = extract_A(2, [&](double* s, double x) { biquad_step(s, x, c); });
+  ss.D = 0;
+  return ss;
+}
+
 StateSpace lpdc_ss(const LpDcCoeffs& c) {  // iir.rs:151-165, state (z0_1,z0_2,z1_1,z1_2,dc_x1,dc_y1)
   StateSpace ss;
   ss.S = 6;

@@ -55,6 +55,7 @@ struct StateSpace {
   double D;
 };
 StateSpace lp_cascade_ss(const BiquadCoeffs& c);           // S = 4
+StateSpace biquad_ss(const BiquadCoeffs& c);               // S = 2 (one TDF-II biquad)
 StateSpace lpdc_ss(const LpDcCoeffs& c);                   // S = 6 (LP4 + DC blocker)
 StateSpace dc_ss(float r);                                 // S = 2 (x1, y1)
 StateSpace onepole_ss(float a);                            // S = 1 (cw)

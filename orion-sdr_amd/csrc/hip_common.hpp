@@ -71,8 +71,10 @@ __device__ __forceinline__ f2 cmul(f2 a, f2 b) {
 // the top 24 bits give an exactly representable f32 turn count for
 // sincospif, the remaining 40 bits a first-order correction (< 3.8e-7 rad, so
 // the neglected second-order term is < 1e-13).
-__device__ __forceinline__ f2 phasor_q64(uint64_t k, uint64_t step_q64) {
-  const uint64_t ph = k * step_q64;
+__device__ __forceinline__ f2 phasor_at(uint64_t ph);
+__device__ __forceinline__ f2 phasor_q64(uint64_t k, uint64_t step_q64) { return phasor_at(k * step_q64); }
+// The phasor of a Q0.64 phase (a fraction of a turn): e^{j 2 pi ph / 2^64}.
+__device__ __forceinline__ f2 phasor_at(uint64_t ph) {
   const uint32_t hi24 = static_cast<uint32_t>(ph >> 40);
   const uint64_t lo40 = ph & ((1ull << 40) - 1);
   const float t2 = static_cast<float>(hi24) * (1.0f / 8388608.0f);  // 2*turns in [0,2)
@@ -155,5 +157,13 @@ __device__ __forceinline__ float pm_disc(f2 z, f2 p, float k) {
 }
 
 inline int div_up(long long a, long long b) { return static_cast<int>((a + b - 1) / b); }
+
+// Cross-workgroup waits (WBFM segment hand-offs, decoupled look-backs) poll a flag
+// at most spin_limit() times before they give up and set the handle's device error
+// word (blocks.hpp Block::dev_err). Process-wide; orion_debug_set_spin_limit sets
+// it (0: every wait times out at once — a test-only setting).
+constexpr uint32_t kSpinDefault = 1u << 22;
+uint32_t spin_limit();
+void set_spin_limit(uint32_t polls);
 
 }  // namespace orion

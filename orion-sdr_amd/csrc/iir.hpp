@@ -24,6 +24,13 @@ struct BiquadK {
   }
 };
 
+// dsp/iir.rs:15-41 Biquad::process — one TDF-II biquad; state (z1, z2) = design.cpp biquad_ss.
+struct RecBQ {
+  static constexpr int S = 2;
+  BiquadK bq;
+  __device__ __forceinline__ float step(float (&s)[S], float x) const { return bq.step(s[0], s[1], x); }
+};
+
 // dsp/iir.rs:79-83 LpCascade::process — two identical biquads. State order
 // (z0_1, z0_2, z1_1, z1_2) matches design.cpp lp_cascade_ss.
 struct RecLP4 {

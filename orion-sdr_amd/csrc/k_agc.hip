@@ -1,4 +1,5 @@
-// k_agc.hip — AgcRms / AgcRmsIq (dsp/agc.rs:7-150) on the device.
+// k_agc.hip — AgcRms / AgcRmsIq (dsp/agc.rs:7-150) and CwKeyedMod (modulate/cw.rs:9-87)
+// on the device: both are the same switched one-pole envelope recurrence.
 //
 // The reference's envelope is a data-dependent recurrence
 //   env <- a(x2 > env) * env + (1 - a) * x2,  a in {attack_a, release_a}
@@ -44,31 +45,59 @@ struct AgcK {
   float att, rel, tgt, gmin, gmax;
 };
 
+// The switched one-pole envelope, env <- a * env + (1 - a) * d with a = att when
+// up(d, env) else rel, as a policy over the per-sample ops (the walks and the
+// exactness machinery below are shared):
+//   AgcPol<IQ> — dsp/agc.rs:33-75 / :124-150: d = |x|^2, up = d > env, seed env = max(d0,
+//     1e-12) when the carried env is 0 (agc.rs:57-60), out = clamp(tgt / max(sqrt(env),
+//     1e-6), gmin, gmax) * x.
+//   CwPol — modulate/cw.rs:45-87 CwKeyedMod: d = clamp(x, 0, 1), up = d >= env, no
+//     reseed, out = mix_with_nco((env * gain, 0), nco) (the non-FMA product, nco.rs:63-66)
+//     with the oscillator phasor of the sample's absolute index (closed form, as Rotator).
 template <bool IQ>
-__device__ __forceinline__ float agc_x2(const float* in, long long i) {
-  if constexpr (IQ) {
-    const float2 v = reinterpret_cast<const float2*>(in)[i];
-    return v.x * v.x + v.y * v.y;
-  } else {
-    const float v = in[i];
-    return v * v;
+struct AgcPol {
+  using In = typename std::conditional<IQ, float2, float>::type;
+  using Out = In;
+  AgcK k;
+  float att, rel, oma, omr;
+  __device__ __forceinline__ float drive(In v) const {
+    if constexpr (IQ) return v.x * v.x + v.y * v.y;
+    else return v * v;
   }
-}
-
-template <bool IQ>
-struct AgcSample {
-  using T = typename std::conditional<IQ, float2, float>::type;
+  __device__ __forceinline__ bool up(float d, float env) const { return d > env; }
+  __device__ __forceinline__ float seed(float env, float d0) const { return env == 0.0f ? fmaxf(d0, 1e-12f) : env; }
+  __device__ __forceinline__ float warm_seed(float d) const { return fmaxf(d, 1e-12f); }
+  __device__ __forceinline__ Out out(In v, float env, long long) const {
+    const float rms = fmaxf(sqrtf(env), 1e-6f);
+    const float g = fminf(fmaxf(k.tgt / rms, k.gmin), k.gmax);
+    if constexpr (IQ) return make_float2(g * v.x, g * v.y);
+    else return g * v;
+  }
+};
+struct CwPol {
+  using In = float;
+  using Out = float2;
+  float att, rel, oma, omr, gain;
+  uint64_t k0, step;  // sample i of the call: the phasor after k0 + i + 1 steps
+  __device__ __forceinline__ float drive(In v) const { return fminf(fmaxf(v, 0.0f), 1.0f); }  // f32::clamp(0, 1)
+  __device__ __forceinline__ bool up(float d, float env) const { return d >= env; }
+  __device__ __forceinline__ float seed(float env, float) const { return env; }
+  __device__ __forceinline__ float warm_seed(float d) const { return d; }
+  __device__ __forceinline__ Out out(In, float env, long long i) const {
+    const float m = env * gain;
+    const f2 p = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
+    return make_float2(m * p.x - 0.0f * p.y, m * p.y + 0.0f * p.x);
+  }
 };
 
 constexpr int kB = 16;
 
 // Walks samples [s, e) of one lane in batches of kB, the next batch's loads issued
 // before the current batch's recurrence. OUT = false: envelope only (the warm-up).
-template <bool IQ, bool OUT>
-__device__ __forceinline__ float agc_walk(const typename AgcSample<IQ>::T* __restrict__ x,
-                                          typename AgcSample<IQ>::T* __restrict__ y, long long s, long long e,
-                                          float env, const AgcK& k, float oma, float omr) {
-  using T = typename AgcSample<IQ>::T;
+template <class Pol, bool OUT>
+__device__ __forceinline__ float agc_walk(const typename Pol::In* __restrict__ x, typename Pol::Out* __restrict__ y,
+                                          long long s, long long e, float env, const Pol& P) {
+  using T = typename Pol::In;
   T cur[kB], nxt[kB];
 #pragma unroll
   for (int j = 0; j < kB; ++j) cur[j] = s + j < e ? x[s + j] : T{};
@@ -79,29 +108,12 @@ __device__ __forceinline__ float agc_walk(const typename AgcSample<IQ>::T* __res
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       const long long i = base + j;
-      float re, im = 0.0f, x2;
-      if constexpr (IQ) {
-        re = cur[j].x; im = cur[j].y;
-        x2 = re * re + im * im;
-      } else {
-        re = cur[j];
-        x2 = re * re;
-      }
-      const bool up = x2 > env;
-      const float a = up ? k.att : k.rel;
-      const float om = up ? oma : omr;
-      const float ne = a * env + om * x2;  // agc.rs:40
+      const float d = P.drive(cur[j]);
+      const bool up = P.up(d, env);
+      const float ne = (up ? P.att : P.rel) * env + (up ? P.oma : P.omr) * d;  // agc.rs:40, cw.rs:58-62
       if (i < e) {
         env = ne;
-        if constexpr (OUT) {
-          const float rms = fmaxf(sqrtf(env), 1e-6f);
-          const float g = fminf(fmaxf(k.tgt / rms, k.gmin), k.gmax);
-          if constexpr (IQ) {
-            y[i] = make_float2(g * re, g * im);
-          } else {
-            y[i] = g * re;
-          }
-        }
+        if constexpr (OUT) y[i] = P.out(cur[j], env, i);
       }
     }
 #pragma unroll
@@ -111,89 +123,69 @@ __device__ __forceinline__ float agc_walk(const typename AgcSample<IQ>::T* __res
 }
 
 // One wave walks samples [s, e) in order from env (the re-runs of k_agc_fix and the
-// sequential path). The 64 lanes load 64 samples and form x2 and both candidate
-// (1 - a) * x2 products; the envelope chain itself is uniform across the wave
-// (x2 and the products read lane by lane into SGPRs: compare, two selects, one
-// multiply, one add per sample), then every lane forms its sample's gain and
-// output. Same f32 ops and roundings as agc.rs:40 and :63-67.
-template <bool IQ>
-__device__ __forceinline__ float agc_wave_walk(const typename AgcSample<IQ>::T* __restrict__ x,
-                                               typename AgcSample<IQ>::T* __restrict__ y, long long s, long long e,
-                                               float env, const AgcK& k, float oma, float omr) {
-  using T = typename AgcSample<IQ>::T;
+// sequential path). The 64 lanes load 64 samples and form d and both candidate
+// (1 - a) * d products; the envelope chain itself is uniform across the wave
+// (d and the products read lane by lane into SGPRs: compare, two selects, one
+// multiply, one add per sample), then every lane forms its sample's output. Same
+// f32 ops and roundings as the reference's per-sample update.
+template <class Pol>
+__device__ __forceinline__ float agc_wave_walk(const typename Pol::In* __restrict__ x,
+                                               typename Pol::Out* __restrict__ y, long long s, long long e, float env,
+                                               const Pol& P) {
+  using T = typename Pol::In;
   const int lane = threadIdx.x & 63;
   T cur = s + lane < e ? x[s + lane] : T{};
   for (long long base = s; base < e; base += 64) {
     const long long i = base + lane;
     const T nxt = i + 64 < e ? x[i + 64] : T{};
-    float re, im = 0.0f, x2;
-    if constexpr (IQ) {
-      re = cur.x; im = cur.y;
-      x2 = re * re + im * im;
-    } else {
-      re = cur;
-      x2 = re * re;
-    }
-    const float pa = oma * x2, pr = omr * x2;
+    const float d = P.drive(cur);
+    const float pa = P.oma * d, pr = P.omr * d;
     const int cnt = e - base < 64 ? static_cast<int>(e - base) : 64;
     float mine = 0.0f;
     if (cnt == 64) {
 #pragma unroll
       for (int j = 0; j < 64; ++j) {
-        const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x2), j));
+        const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), j));
         const float aj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pa), j));
         const float rj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pr), j));
-        const bool up = xj > env;
-        env = (up ? k.att : k.rel) * env + (up ? aj : rj);
+        const bool up = P.up(xj, env);
+        env = (up ? P.att : P.rel) * env + (up ? aj : rj);
         mine = lane == j ? env : mine;
       }
     } else {
       for (int j = 0; j < cnt; ++j) {
-        const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x2), j));
+        const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), j));
         const float aj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pa), j));
         const float rj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pr), j));
-        const bool up = xj > env;
-        env = (up ? k.att : k.rel) * env + (up ? aj : rj);
+        const bool up = P.up(xj, env);
+        env = (up ? P.att : P.rel) * env + (up ? aj : rj);
         mine = lane == j ? env : mine;
       }
     }
-    if (i < e) {
-      const float rms = fmaxf(sqrtf(mine), 1e-6f);
-      const float g = fminf(fmaxf(k.tgt / rms, k.gmin), k.gmax);
-      if constexpr (IQ) {
-        y[i] = make_float2(g * re, g * im);
-      } else {
-        y[i] = g * re;
-      }
-    }
+    if (i < e) y[i] = P.out(cur, mine, i);
     cur = nxt;
   }
   return env;
 }
 
 // The whole call in order by one wave (warm-ups as long as the call itself).
-template <bool IQ>
-__global__ __launch_bounds__(64) void k_agc_seq(const float* __restrict__ in, float* __restrict__ out, long long n,
-                                                AgcK k, const float* __restrict__ env_in,
-                                                float* __restrict__ env_out) {
-  using T = typename AgcSample<IQ>::T;
-  float env = env_in[0];
-  if (env == 0.0f) env = fmaxf(agc_x2<IQ>(in, 0), 1e-12f);  // agc.rs:57-60
-  const float oma = 1.0f - k.att, omr = 1.0f - k.rel;
-  env = agc_wave_walk<IQ>(reinterpret_cast<const T*>(in), reinterpret_cast<T*>(out), 0, n, env, k, oma, omr);
+template <class Pol>
+__global__ __launch_bounds__(64) void k_agc_seq(const void* __restrict__ in, void* __restrict__ out, long long n,
+                                                Pol P, const float* __restrict__ env_in, float* __restrict__ env_out) {
+  const auto* x = static_cast<const typename Pol::In*>(in);
+  float env = P.seed(env_in[0], P.drive(x[0]));
+  env = agc_wave_walk<Pol>(x, static_cast<typename Pol::Out*>(out), 0, n, env, P);
   if (threadIdx.x == 0) env_out[0] = env;
 }
 
 // Pass 1: chunk c = [c*L, min(c*L+L, n)), warm-up from max(c*L - W, 0).
-template <bool IQ>
-__global__ __launch_bounds__(256) void k_agc(const float* __restrict__ in, float* __restrict__ out,
-                                             long long n, long long L, long long W, AgcK k,
-                                             const float* __restrict__ env_in, float* __restrict__ env_out,
-                                             float* __restrict__ ent, float* __restrict__ ext,
-                                             long long* __restrict__ first_bad) {
-  using T = typename AgcSample<IQ>::T;
-  const T* x = reinterpret_cast<const T*>(in);
-  T* y = reinterpret_cast<T*>(out);
+template <class Pol>
+__global__ __launch_bounds__(256) void k_agc(const void* __restrict__ in, void* __restrict__ out, long long n,
+                                             long long L, long long W, Pol P, const float* __restrict__ env_in,
+                                             float* __restrict__ env_out, float* __restrict__ ent,
+                                             float* __restrict__ ext, long long* __restrict__ first_bad) {
+  const auto* x = static_cast<const typename Pol::In*>(in);
+  auto* y = static_cast<typename Pol::Out*>(out);
   const long long c = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
   const long long b = c * L;
   if (b >= n) return;
@@ -202,17 +194,10 @@ __global__ __launch_bounds__(256) void k_agc(const float* __restrict__ in, float
   // A warm-up that would reach back past the call's first sample starts there, from
   // the carried envelope, exactly as chunk 0 does (such chunks are exact).
   const long long s0 = b - W > 0 ? b - W : 0;
-  float env;
-  if (s0 == 0) {
-    env = env_in[0];
-    if (env == 0.0f) env = fmaxf(agc_x2<IQ>(in, 0), 1e-12f);  // agc.rs:57-60
-  } else {
-    env = fmaxf(agc_x2<IQ>(in, s0), 1e-12f);
-  }
-  const float oma = 1.0f - k.att, omr = 1.0f - k.rel;  // (1 - a) as agc.rs:40 forms it
-  env = agc_walk<IQ, false>(x, y, s0, b, env, k, oma, omr);
+  float env = s0 == 0 ? P.seed(env_in[0], P.drive(x[0])) : P.warm_seed(P.drive(x[s0]));
+  env = agc_walk<Pol, false>(x, y, s0, b, env, P);
   ent[c] = env;
-  env = agc_walk<IQ, true>(x, y, b, e, env, k, oma, omr);
+  env = agc_walk<Pol, true>(x, y, b, e, env, P);
   ext[c] = env;
   if (e == n) env_out[0] = env;
 }
@@ -229,24 +214,22 @@ __global__ __launch_bounds__(256) void k_agc_check(const float* __restrict__ ent
 
 // Pass 3 (one wave): re-run disagreeing chunks in order from the true exit of
 // their predecessor. Exits immediately when pass 2 found nothing.
-template <bool IQ>
-__global__ __launch_bounds__(64) void k_agc_fix(const float* __restrict__ in, float* __restrict__ out,
-                                                long long n, long long L, AgcK k, const float* __restrict__ ent,
+template <class Pol>
+__global__ __launch_bounds__(64) void k_agc_fix(const void* __restrict__ in, void* __restrict__ out, long long n,
+                                                long long L, Pol P, const float* __restrict__ ent,
                                                 const float* __restrict__ ext, const long long* __restrict__ first_bad,
                                                 float* __restrict__ env_out) {
-  using T = typename AgcSample<IQ>::T;
-  const T* x = reinterpret_cast<const T*>(in);
-  T* y = reinterpret_cast<T*>(out);
+  const auto* x = static_cast<const typename Pol::In*>(in);
+  auto* y = static_cast<typename Pol::Out*>(out);
   const long long chunks = (n + L - 1) / L;
   long long c = first_bad[0];
   if (c >= chunks) return;
   const int lane = threadIdx.x;
-  const float oma = 1.0f - k.att, omr = 1.0f - k.rel;
   float ex = ext[c - 1];  // chunks < c are consistent, so this exit is the sequential one
   while (c < chunks) {
     // chunk c entered with the wrong envelope: re-run it from ex, in order
     const long long b = c * L, e = b + L < n ? b + L : n;
-    ex = agc_wave_walk<IQ>(x, y, b, e, ex, k, oma, omr);
+    ex = agc_wave_walk<Pol>(x, y, b, e, ex, P);
     ++c;
     // the next chunk whose recorded entry is not the true exit of its predecessor
     long long nxt = chunks;
@@ -273,37 +256,79 @@ __global__ __launch_bounds__(64) void k_agc_fix(const float* __restrict__ in, fl
   if (lane == 0) env_out[0] = ex;
 }
 
+// Host driver of the three passes for one policy. Chunk length: the extra warm-up
+// work per chunk is W/L of a chunk, so L >= W/16 caps the total work at 17 x n; the
+// floor keeps >> 1024 waves busy for short warm-ups. W >= n/4: one wave walks the
+// call in order (k_agc_seq, ~27 ns per sample, faster than lanes whose own walks are
+// that long).
+class EnvelopeRunner {
+ public:
+  explicit EnvelopeRunner(double amax) {
+    // amax^W < 1e-9; amax == 1 (or NaN) never forgets: one sequential lane.
+    warm_ = amax < 1.0 ? static_cast<long long>(std::ceil(std::log(1e-9) / std::log(amax))) : -1;
+    env_.resize(2 * sizeof(float));
+    env_.zero();
+  }
+  long long warm() const { return warm_; }
+  long long chunk_len(long long n) const {
+    if (warm_ < 0 || warm_ >= n / 4) return n;
+    return std::max(256LL, (warm_ + 15) / 16);
+  }
+  template <class Pol>
+  void run(const void* in, void* out, long long n, const Pol& P, hipStream_t s) {
+    const long long L = chunk_len(n);
+    const long long chunks = (n + L - 1) / L;
+    float* e = env_.as<float>();
+    float* ein = e + cur_;
+    float* eout = e + (cur_ ^ 1);
+    cur_ ^= 1;
+    if (chunks == 1) {  // one wave, in order
+      hipLaunchKernelGGL(k_agc_seq<Pol>, dim3(1), dim3(64), 0, s, in, out, n, P, ein, eout);
+      ORION_HIP(hipGetLastError());
+      return;
+    }
+    const size_t need = static_cast<size_t>(chunks) * 2 * sizeof(float) + sizeof(long long);
+    if (chunk_state_.size() < need) chunk_state_.resize(need);
+    long long* first_bad = chunk_state_.as<long long>();
+    float* ent = reinterpret_cast<float*>(first_bad + 1);
+    float* ext = ent + chunks;
+    const unsigned grid = static_cast<unsigned>((chunks + 255) / 256);
+    const long long W = warm_ < 0 ? 0 : warm_;
+    hipLaunchKernelGGL(k_agc<Pol>, dim3(grid), dim3(256), 0, s, in, out, n, L, W, P, ein, eout, ent, ext, first_bad);
+    ORION_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_agc_check, dim3(static_cast<unsigned>((chunks - 1 + 255) / 256)), dim3(256), 0, s, ent, ext,
+                       chunks, first_bad);
+    ORION_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_agc_fix<Pol>, dim3(1), dim3(64), 0, s, in, out, n, L, P, ent, ext, first_bad, eout);
+    ORION_HIP(hipGetLastError());
+  }
+  void reset() {
+    env_.zero();
+    cur_ = 0;
+  }
+
+ private:
+  long long warm_ = 0;
+  DevBuf env_;          // two floats: the carried envelope, ping-ponged per call
+  DevBuf chunk_state_;  // first disagreeing chunk, then ent[chunks], ext[chunks]
+  int cur_ = 0;
+};
+
 class AgcBlock final : public Block {
  public:
-  AgcBlock(bool iq, float fs, float attack_ms, float release_ms, float target_rms) : iq_(iq) {
+  AgcBlock(bool iq, float fs, float attack_ms, float release_ms, float target_rms)
+      : iq_(iq), runner_(amax_of(fs, attack_ms, release_ms)) {
     // agc.rs:21 / :97: a(ms) = exp(-1 / (fs * (max(ms, 1e-3) / 1000)))
-    auto coef = [fs](float ms) { return std::exp(-1.0f / (fs * (std::max(ms, 1e-3f) / 1000.0f))); };
-    k_.att = coef(attack_ms);
-    k_.rel = coef(release_ms);
+    k_.att = coef(fs, attack_ms);
+    k_.rel = coef(fs, release_ms);
     k_.tgt = std::max(target_rms, 1e-6f);
     k_.gmin = 0.05f;
     k_.gmax = 20.0f;
-    const double amax = std::max(k_.att, k_.rel);
-    // amax^W < 1e-9; amax == 1 (or NaN) never forgets: one sequential lane.
-    warm_ = amax < 1.0 ? static_cast<long long>(std::ceil(std::log(1e-9) / std::log(amax))) : -1;
-    if (const char* v = std::getenv("ORION_AGC_WORK_DIV")) work_div_ = std::max(1LL, std::atoll(v));
-    if (const char* v = std::getenv("ORION_AGC_MIN_L")) min_l_ = std::max(1LL, std::atoll(v));
-    if (const char* v = std::getenv("ORION_AGC_SEQ_DIV")) seq_div_ = std::max(1LL, std::atoll(v));
-    env_.resize(2 * sizeof(float));
-    env_.zero();
   }
   const char* name() const override { return iq_ ? "AgcRmsIq" : "AgcRms"; }
   Dt in_type() const override { return iq_ ? Dt::C32 : Dt::F32; }
   Dt out_type() const override { return iq_ ? Dt::C32 : Dt::F32; }
   bool alias_ok() const override { return true; }  // overlapping in/out: staged through a copy
-  // Chunk length: the extra warm-up work per chunk is W/L of a chunk, so L >= W/div
-  // caps the total work at (1 + div) x n; the floor keeps >> 1024 waves busy for
-  // short warm-ups. W >= n/4: one wave walks the call in order (k_agc_seq, ~27 ns
-  // per sample, faster than lanes whose own walks are that long).
-  long long chunk_len(long long n) const {
-    if (warm_ < 0 || warm_ >= n / seq_div_) return n;
-    return std::max(min_l_, (warm_ + work_div_ - 1) / work_div_);
-  }
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const long long n = static_cast<long long>(std::min(n_in, out_cap));  // agc.rs:49
     if (n == 0) return {0, 0};
@@ -316,76 +341,73 @@ class AgcBlock final : public Block {
       ORION_HIP(hipMemcpyAsync(copy_.as<void>(), in, bytes, hipMemcpyDeviceToDevice, s));
       in = copy_.as<void>();
     }
-    const long long L = chunk_len(n);
-    const long long chunks = (n + L - 1) / L;
-    float* e = env_.as<float>();
-    float* ein = e + cur_;
-    float* eout = e + (cur_ ^ 1);
-    if (chunks == 1) {  // one wave, in order
-      if (iq_) {
-        hipLaunchKernelGGL(k_agc_seq<true>, dim3(1), dim3(64), 0, s, static_cast<const float*>(in),
-                           static_cast<float*>(out), n, k_, ein, eout);
-      } else {
-        hipLaunchKernelGGL(k_agc_seq<false>, dim3(1), dim3(64), 0, s, static_cast<const float*>(in),
-                           static_cast<float*>(out), n, k_, ein, eout);
-      }
-      ORION_HIP(hipGetLastError());
-      cur_ ^= 1;
-      return {static_cast<size_t>(n), static_cast<size_t>(n)};
-    }
-    const size_t need = static_cast<size_t>(chunks) * 2 * sizeof(float) + sizeof(long long);
-    if (chunk_state_.size() < need) chunk_state_.resize(need);
-    long long* first_bad = chunk_state_.as<long long>();
-    float* ent = reinterpret_cast<float*>(first_bad + 1);
-    float* ext = ent + chunks;
-    const unsigned grid = static_cast<unsigned>((chunks + 255) / 256);
-    const long long W = warm_ < 0 ? 0 : warm_;
-    const float* x = static_cast<const float*>(in);
-    float* y = static_cast<float*>(out);
-    if (iq_) {
-      hipLaunchKernelGGL(k_agc<true>, dim3(grid), dim3(256), 0, s, x, y, n, L, W, k_, ein, eout, ent, ext, first_bad);
-    } else {
-      hipLaunchKernelGGL(k_agc<false>, dim3(grid), dim3(256), 0, s, x, y, n, L, W, k_, ein, eout, ent, ext, first_bad);
-    }
-    ORION_HIP(hipGetLastError());
-    {
-      hipLaunchKernelGGL(k_agc_check, dim3(static_cast<unsigned>((chunks - 1 + 255) / 256)), dim3(256), 0, s, ent,
-                         ext, chunks, first_bad);
-      ORION_HIP(hipGetLastError());
-      if (iq_) {
-        hipLaunchKernelGGL(k_agc_fix<true>, dim3(1), dim3(64), 0, s, x, y, n, L, k_, ent, ext, first_bad, eout);
-      } else {
-        hipLaunchKernelGGL(k_agc_fix<false>, dim3(1), dim3(64), 0, s, x, y, n, L, k_, ent, ext, first_bad, eout);
-      }
-      ORION_HIP(hipGetLastError());
-    }
-    cur_ ^= 1;
+    const float oma = 1.0f - k_.att, omr = 1.0f - k_.rel;  // (1 - a) as agc.rs:40 forms it
+    if (iq_) runner_.run(in, out, n, AgcPol<true>{k_, k_.att, k_.rel, oma, omr}, s);
+    else runner_.run(in, out, n, AgcPol<false>{k_, k_.att, k_.rel, oma, omr}, s);
     return {static_cast<size_t>(n), static_cast<size_t>(n)};
   }
-  void reset() override {
-    env_.zero();
-    cur_ = 0;
-  }
+  void reset() override { runner_.reset(); }
   std::vector<float> taps(int which) const override {
-    if (which == 1) return {static_cast<float>(chunk_len(1LL << 24))};
-    return {k_.att, k_.rel, k_.tgt, static_cast<float>(warm_)};
+    if (which == 1) return {static_cast<float>(runner_.chunk_len(1LL << 24))};
+    return {k_.att, k_.rel, k_.tgt, static_cast<float>(runner_.warm())};
   }
 
  private:
+  static float coef(float fs, float ms) { return std::exp(-1.0f / (fs * (std::max(ms, 1e-3f) / 1000.0f))); }
+  static double amax_of(float fs, float a, float r) { return std::max(coef(fs, a), coef(fs, r)); }
   bool iq_;
   AgcK k_{};
-  long long warm_ = 0;
-  long long work_div_ = 16, min_l_ = 256, seq_div_ = 4;
-  DevBuf env_;          // two floats: the carried envelope, ping-ponged per call
-  DevBuf chunk_state_;  // first disagreeing chunk, then ent[chunks], ext[chunks]
-  DevBuf copy_;         // input copy for overlapping in/out
-  int cur_ = 0;
+  EnvelopeRunner runner_;
+  DevBuf copy_;  // input copy for overlapping in/out
+};
+
+// modulate/cw.rs:9-87 CwKeyedMod: keying envelope f32 -> cf32 IQ.
+class CwModBlock final : public Block {
+ public:
+  CwModBlock(float fs, float tone_hz, float rise_ms, float fall_ms)
+      : osc_(oscillator(tone_hz, fs)), runner_(std::max(alpha(fs, rise_ms), alpha(fs, fall_ms))) {
+    rise_ = alpha(fs, rise_ms);
+    fall_ = alpha(fs, fall_ms);
+  }
+  const char* name() const override { return "CwKeyedMod"; }
+  Dt in_type() const override { return Dt::F32; }
+  Dt out_type() const override { return Dt::C32; }
+  WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
+    const long long n = static_cast<long long>(std::min(n_in, out_cap));  // cw.rs:47
+    if (n == 0) return {0, 0};
+    runner_.run(in, out, n, CwPol{rise_, fall_, 1.0f - rise_, 1.0f - fall_, g_, k_, osc_.step_q64}, s);
+    k_ += static_cast<uint64_t>(n);
+    return {static_cast<size_t>(n), static_cast<size_t>(n)};
+  }
+  void reset() override {
+    runner_.reset();
+    k_ = 0;
+  }
+  void set_gain(float g) { g_ = g; }  // cw.rs:39-41
+  std::vector<float> taps(int) const override { return {rise_, fall_, osc_.w_re, osc_.w_im}; }
+
+ private:
+  // cw.rs:27-30: tau = (max(ms, 0.1) * 1e-3) * fs; alpha = exp(-1 / tau)
+  static float alpha(float fs, float ms) { return std::exp(-1.0f / ((std::max(ms, 0.1f) * 1e-3f) * fs)); }
+  Oscillator osc_;
+  EnvelopeRunner runner_;
+  float rise_ = 0, fall_ = 0, g_ = 1.0f;
+  uint64_t k_ = 0;
 };
 
 }  // namespace
 
 std::unique_ptr<Block> make_agc(bool iq, float fs, float attack_ms, float release_ms, float target_rms) {
   return std::make_unique<AgcBlock>(iq, fs, attack_ms, release_ms, target_rms);
+}
+std::unique_ptr<Block> make_cw_mod(float fs, float tone_hz, float rise_ms, float fall_ms) {
+  return std::make_unique<CwModBlock>(fs, tone_hz, rise_ms, fall_ms);
+}
+int cw_mod_set_gain(Block* b, float g) {
+  auto* c = dynamic_cast<CwModBlock*>(b);
+  if (!c) return -4;
+  c->set_gain(g);
+  return 0;
 }
 
 }  // namespace orion

@@ -13,19 +13,19 @@ namespace orion {
 namespace {
 
 constexpr int NT = 256;
-#ifndef ORION_FIR8_UNROLL
-#define ORION_FIR8_UNROLL 1  // 16-tap blocks unrolled in k_fir_iq8 / k_fir_real8 (timing experiments)
-#endif
 constexpr int kMaxGrid = 2048;  // memory-bound: cap and grid-stride (2048 = 8 WG per CU)
-#ifndef ORION_FIR_HT
-#define ORION_FIR_HT 4
-#endif
-constexpr int kFirHT = ORION_FIR_HT;  // 512-output halves per complex-FIR tile
 
 // ------------------------------------------------------------------ NCO --
-template <bool A16, bool USB>
+// Output i of a call uses the oscillator phasor after k0 + i + 1 steps (the
+// reference's next() returns the post-multiply phasor, rotator.rs:44-62), of phase
+// base + (k0 + i + 1) step (Q0.64; base moves when the frequency is retuned, so the
+// phase continues). MODE: kRotate rotate_block (FMA form, rotator.rs:80-83), kUsb
+// mix_usb_block (cf32 -> f32, rotator.rs:88-94), kNcoMix mix_with_nco (non-FMA
+// product, nco.rs:63-66), kNcoGen the phasors themselves (nco.rs:42-58, no input).
+enum : int { kRotate = 0, kUsb = 1, kNcoMix = 2, kNcoGen = 3 };
+template <bool A16, int MODE>
 __global__ __launch_bounds__(NT) void k_rotator(const f2* __restrict__ x, void* __restrict__ yv,
-                                                long long n, uint64_t k0, uint64_t step,
+                                                long long n, uint64_t k0, uint64_t step, uint64_t base,
                                                 const f2* __restrict__ tab) {
   constexpr int PER = kRotTile / (2 * NT);  // pairs per thread per tile (8)
   const int t = threadIdx.x;
@@ -36,32 +36,44 @@ __global__ __launch_bounds__(NT) void k_rotator(const f2* __restrict__ x, void* 
     tb[i][0] = f2{v.x, v.y};
     tb[i][1] = f2{v.z, v.w};
   }
-  for (long long base = static_cast<long long>(blockIdx.x) * kRotTile; base < n;
-       base += static_cast<long long>(gridDim.x) * kRotTile) {
-    const f2 S = phasor_q64(k0 + static_cast<uint64_t>(base) + 1, step);
+  for (long long tile = static_cast<long long>(blockIdx.x) * kRotTile; tile < n;
+       tile += static_cast<long long>(gridDim.x) * kRotTile) {
+    const f2 S = phasor_at(base + (k0 + static_cast<uint64_t>(tile) + 1) * step);
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const long long P = base + 2 * t + 2 * NT * i;
+      const long long P = tile + 2 * t + 2 * NT * i;
       if (P >= n) break;
-      f2 v0, v1 = f2{0.0f, 0.0f};
+      f2 v0 = f2{0.0f, 0.0f}, v1 = f2{0.0f, 0.0f};
       const bool full = P + 1 < n;
-      if (A16 && full) {
-        const f4 v = *reinterpret_cast<const f4*>(x + P);
-        v0 = f2{v.x, v.y};
-        v1 = f2{v.z, v.w};
-      } else {
-        v0 = x[P];
-        if (full) v1 = x[P + 1];
+      if constexpr (MODE != kNcoGen) {
+        if (A16 && full) {
+          const f4 v = *reinterpret_cast<const f4*>(x + P);
+          v0 = f2{v.x, v.y};
+          v1 = f2{v.z, v.w};
+        } else {
+          v0 = x[P];
+          if (full) v1 = x[P + 1];
+        }
       }
       const f2 p0 = cmul(S, tb[i][0]);
       const f2 p1 = cmul(S, tb[i][1]);
-      if constexpr (USB) {
+      if constexpr (MODE == kUsb) {
         float* y = static_cast<float*>(yv);
         y[P] = __builtin_fmaf(v0.x, p0.x, v0.y * p0.y);
         if (full) y[P + 1] = __builtin_fmaf(v1.x, p1.x, v1.y * p1.y);
       } else {
         f2* y = static_cast<f2*>(yv);
-        const f2 o0 = cmul_rot(v0, p0), o1 = cmul_rot(v1, p1);
+        f2 o0, o1;
+        if constexpr (MODE == kRotate) {
+          o0 = cmul_rot(v0, p0);
+          o1 = cmul_rot(v1, p1);
+        } else if constexpr (MODE == kNcoMix) {  // (x.re c - x.im s, x.re s + x.im c), no FMA
+          o0 = f2{v0.x * p0.x - v0.y * p0.y, v0.x * p0.y + v0.y * p0.x};
+          o1 = f2{v1.x * p1.x - v1.y * p1.y, v1.x * p1.y + v1.y * p1.x};
+        } else {
+          o0 = p0;
+          o1 = p1;
+        }
         if (A16 && full) {
           *reinterpret_cast<f4*>(y + P) = f4{o0.x, o0.y, o1.x, o1.y};
         } else {
@@ -73,53 +85,15 @@ __global__ __launch_bounds__(NT) void k_rotator(const f2* __restrict__ x, void* 
   }
 }
 
-// -------------------------------------------------- polyphase decimator --
-template <int Q, bool A16>
-__global__ __launch_bounds__(NT) void k_decim8(const f2* __restrict__ x, long long x_stride,
-                                               long long n, const f2* __restrict__ hist,
-                                               int hist_len, f2* __restrict__ out,
-                                               long long out_stride, long long n_out,
-                                               const Taps256 g) {
-  using P = Poly<8, Q, 512, NT>;
-  __shared__ __attribute__((aligned(16))) f2 U[P::LDS_F2];
-  const int t = threadIdx.x;
-  const int ch = blockIdx.y;
-  x += ch * x_stride;
-  hist += static_cast<long long>(ch) * hist_len;
-  out += ch * out_stride;
-  for (long long J = static_cast<long long>(blockIdx.x) * 512; J < n_out;
-       J += static_cast<long long>(gridDim.x) * 512) {
-    const long long porg = 8 * (J - Q);
-    for (int p = 2 * t; p < P::NS; p += 2 * NT) {
-      f2 v0, v1;
-      load_pair<A16>(x, n, hist, hist_len, porg + p, v0, v1);
-      U[P::slot(p)] = v0;
-      U[P::slot(p + 1)] = v1;
-    }
-    __syncthreads();
-    f2 acc[P::R];
-    P::compute(U, t, [&](int c, int q) { return g.g[c * Q + q]; }, acc);
-#pragma unroll
-    for (int r = 0; r < P::R; ++r) {
-      const long long j = J + P::R * t + r;
-      if (j < n_out) out[j] = acc[r];
-    }
-    __syncthreads();
-  }
-}
-
 // ------------------------------------------- wave-independent decimator ---
-// k_decim_w<Q>: FirDecimator with M = 8 and K <= 8Q taps (C3: 255 taps, Q = 32)
-// in the WBFM front's form. One 64-lane wave per contiguous range of decimated
-// outputs of one channel (as many waves as are resident, one round), walked in
-// tiles of TW = 128 outputs / 1024 new inputs. A tile's inputs are prefetched
-// two tiles ahead into registers (16-B nontemporal loads) and scattered into an
-// 8-row polyphase LDS image (pitch TW+Q+2 = 2 mod 16: conflict-free
-// ds_write_b64); the image's Q+2 leading columns are the previous tile's last
-// ones, copied inside LDS. Each lane computes outputs 2l, 2l+1 from (Q+2)/2
-// conflict-free ds_read_b128 and 2Q packed FMAs per phase (taps from SGPRs) and
-// stores them with one 16-B store (a wave writes 1 KB contiguously). No
-// workgroup barriers, so the register prefetch stays in flight.
+// FirDecimator with M = 8 and K <= 8Q taps (C3: 255 taps, Q = 32) in the WBFM
+// front's form. One 64-lane wave per contiguous range of decimated outputs of one
+// channel (as many waves as are resident, one round), walked in tiles of TW = 128
+// outputs / 1024 new inputs. A tile's inputs are prefetched ahead into registers
+// (16-B nontemporal loads, dw_load) and scattered into an 8-row polyphase LDS
+// image; the image's leading columns are the previous tile's last ones, copied
+// inside LDS. No workgroup barriers, so the register prefetch stays in flight.
+// Dw<Q>: the tile geometry shared by the decimator kernels below.
 template <int Q>
 struct Dw {
   static constexpr int TW = 128;         // outputs per tile
@@ -160,114 +134,6 @@ __device__ __forceinline__ void dw_load(const f2* __restrict__ x, long long n, l
       v[k][0] = xb[o];
       v[k][1] = xb[o + 1];
     }
-  }
-}
-
-template <int Q, bool A16, bool CLAMP>
-__device__ __forceinline__ void dw_tile(f2* __restrict__ U, int l, int n, long long porg, long long J,
-                                        const f2* __restrict__ xc, long long nx, const f2* __restrict__ hc,
-                                        int hist_len, f2 (&v)[Dw<Q>::KL][2], const f2* __restrict__ pfx,
-                                        long long pfn, long long pforg, const Taps256& g, int s0, int s1,
-                                        f2* __restrict__ outc, long long n_out) {
-  using D = Dw<Q>;
-  if (n > 0) {  // halo: the previous tile's columns TW .. TW+Q+1 -> 0 .. Q+1
-#pragma unroll
-    for (int r2 = 0; r2 < (8 * D::HALO / 2 + 63) / 64; ++r2) {
-      const int e = l + 64 * r2;
-      if (e < 8 * D::HALO / 2) {
-        const int c = e / (D::HALO / 2), h = e - (D::HALO / 2) * c;
-        const f4 w = *reinterpret_cast<const f4*>(U + c * D::LR + D::TW + 2 * h);
-        *reinterpret_cast<f4*>(U + c * D::LR + 2 * h) = w;
-      }
-    }
-    wave_lds_fence();
-  }
-#pragma unroll
-  for (int k = 0; k < D::KL; ++k) {
-    U[s0 + 16 * k] = v[k][0];
-    U[s1 + 16 * k] = v[k][1];
-  }
-  asm volatile("" ::: "memory");
-  dw_load<Q, A16, CLAMP>(pfx, pfn, pforg, l, v);  // the tile two ahead (unconditional: see fu_tile)
-  const bool bnd = porg < 0 || porg + 8LL * (D::TW + Q) > nx;
-  if (bnd || n == 0) {
-    // a range's first tile stages its halo columns; a tile reaching before x[0]
-    // or past x[n-1] rewrites its new samples exactly (history / zeros)
-    wave_lds_fence();
-#pragma unroll 1
-    for (int p = (n == 0 ? 0 : 8 * Q) + l; p < 8 * (D::TW + Q); p += 64) {
-      const long long P = porg + p;
-      if (p < 8 * Q || !CLAMP || P < 0 || P >= nx) {
-        const int c = (-p) & 7;
-        U[c * D::LR + (p + c) / 8] = load_hist(xc, nx, hc, hist_len, P);
-      }
-    }
-  }
-  wave_lds_fence();
-  f2 d0 = f2{0.0f, 0.0f}, d1 = f2{0.0f, 0.0f};
-#pragma unroll 1
-  for (int c = 0; c < 8; ++c) {
-    const f4* row = reinterpret_cast<const f4*>(U + c * D::LR + 2 * l);
-    f4 w[D::WIN];
-#pragma unroll
-    for (int h = 0; h < D::WIN; ++h) w[h] = row[h];
-    float t[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) t[q] = g.g[c * Q + q];
-    // window entry m -> output r uses tap q = r + Q - m
-#pragma unroll
-    for (int h = 0; h < D::WIN; ++h) {
-      const f2 w0 = f2{w[h].x, w[h].y}, w1 = f2{w[h].z, w[h].w};
-      const int m0 = 2 * h, m1 = 2 * h + 1;
-      if (Q - m0 >= 0 && Q - m0 < Q) d0 = fma2(splat2(t[Q - m0]), w0, d0);
-      if (Q - m1 >= 0 && Q - m1 < Q) d0 = fma2(splat2(t[Q - m1]), w1, d0);
-      if (1 + Q - m0 >= 0 && 1 + Q - m0 < Q) d1 = fma2(splat2(t[1 + Q - m0]), w0, d1);
-      if (1 + Q - m1 >= 0 && 1 + Q - m1 < Q) d1 = fma2(splat2(t[1 + Q - m1]), w1, d1);
-    }
-  }
-  const long long j = J + 2 * l;
-  if (j + 1 < n_out && (reinterpret_cast<uintptr_t>(outc + j) & 15) == 0) {
-    __builtin_nontemporal_store(f4{d0.x, d0.y, d1.x, d1.y}, reinterpret_cast<f4*>(outc + j));
-  } else {
-    if (j < n_out) outc[j] = d0;
-    if (j + 1 < n_out) outc[j + 1] = d1;
-  }
-}
-
-template <int Q, bool A16, bool CLAMP>
-__global__ __launch_bounds__(64, 3) void k_decim_w(const f2* __restrict__ x, long long x_stride, long long n,
-                                                  const f2* __restrict__ hist, int hist_len, f2* __restrict__ out,
-                                                  long long out_stride, long long n_out, const Taps256 g, int wpc,
-                                                  long long L) {
-  using D = Dw<Q>;
-  __shared__ __attribute__((aligned(16))) f2 U[D::LDS_F2];
-  const int l = threadIdx.x & 63;
-  const int ch = blockIdx.x / wpc;
-  const long long A = static_cast<long long>(blockIdx.x - ch * wpc) * L;
-  const long long B = min(A + L, n_out);
-  if (A >= B) return;
-  // an even tile count: the second tile of a pair always runs (a conditional
-  // one would make the compiler drain the other buffer's prefetch); tiles past
-  // B store nothing
-  const int ntiles = (static_cast<int>((B - A + D::TW - 1) / D::TW) + 1) & ~1;
-  const f2* __restrict__ xc = x + ch * x_stride;
-  const f2* __restrict__ hc = hist + static_cast<long long>(ch) * hist_len;
-  f2* __restrict__ outc = out + ch * out_stride;
-  const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
-  const int s0 = c0 * D::LR + (8 * Q + 2 * l + c0) / 8;
-  const int s1 = c1 * D::LR + (8 * Q + 2 * l + 1 + c1) / 8;
-  long long porg = 8LL * (A - Q);  // x index of staged sample 0 of the first tile
-  f2 va[D::KL][2], vb[D::KL][2];
-  dw_load<Q, A16, CLAMP>(xc, n, porg, l, va);
-  dw_load<Q, A16, CLAMP>(xc, n, porg + D::NEW, l, vb);
-  const long long dummy = -8LL * Q;  // past the range: the channel's first tile (an L2 hit)
-#pragma unroll 1
-  for (int t = 0; t < ntiles; t += 2, porg += 2 * D::NEW) {
-    const long long J = A + static_cast<long long>(t) * D::TW;
-    dw_tile<Q, A16, CLAMP>(U, l, t, porg, J, xc, n, hc, hist_len, va, xc, n,
-                           t + 2 < ntiles ? porg + 2 * D::NEW : dummy, g, s0, s1, outc, B);
-    dw_tile<Q, A16, CLAMP>(U, l, t + 1, porg + D::NEW, J + D::TW, xc, n, hc, hist_len, vb, xc, n,
-                           t + 3 < ntiles ? porg + 3 * D::NEW : dummy, g, s0, s1, outc, B);
   }
 }
 
@@ -502,47 +368,6 @@ __global__ __launch_bounds__(NT) void k_decim_generic(const f2* __restrict__ x, 
 // --------------------------------------------------------- real FIR -------
 // y[i] = sum_{k<KP} g[k] x[i-k], 512 outputs per sub-tile, 2 per lane.
 template <int KP>
-__global__ __launch_bounds__(NT) void k_fir_real(const float* __restrict__ x, long long n,
-                                                 const float* __restrict__ hist, int hist_len,
-                                                 float* __restrict__ y, const Taps256 g) {
-  constexpr int TT = 512;
-  static_assert(KP % 16 == 0, "taps padded to 16");
-  __shared__ __attribute__((aligned(16))) float L[TT + KP + 2];
-  const int t = threadIdx.x;
-  for (long long J = static_cast<long long>(blockIdx.x) * TT; J < n;
-       J += static_cast<long long>(gridDim.x) * TT) {
-    const long long org = J - KP;
-    for (int p = t; p < TT + KP + 2; p += NT) {
-      const long long P = org + p;
-      float v = 0.0f;
-      if (P >= 0) v = P < n ? x[P] : 0.0f;
-      else if (P >= -hist_len) v = hist[hist_len + P];
-      L[p] = v;
-    }
-    __syncthreads();
-    float acc0 = 0.0f, acc1 = 0.0f;
-    // element e <-> L[e - org]; outputs j = J + 2t (+1)
-    fir2_blocked<KP>(
-        [&](long long i, float& w0, float& w1) {
-          const f2 w = *reinterpret_cast<const f2*>(L + (i - org));
-          w0 = w.x;
-          w1 = w.y;
-        },
-        J + 2 * t, [&](int k) { return g.g[k]; }, acc0, acc1);
-    const long long j = J + 2 * t;
-    if (j < n) y[j] = acc0;
-    if (j + 1 < n) y[j + 1] = acc1;
-    __syncthreads();
-  }
-}
-
-// Real FIR with sixteen outputs per lane (4096 per workgroup tile) as eight packed
-// pairs: the staged image holds P[p] = (x[org + p], x[org + 2048 + p]), so one
-// v_pk_fma_f32 advances output j of the tile's first half and output j + 2048 of
-// its second with the same tap, and the inner loop is k_fir_iq8's (24-sample
-// window, 12 ds_read_b128 per 16-tap block for 128 packed FMAs, padded image).
-// Two outputs per lane (k_fir_real) stay behind ORION_FIR_REAL2=1.
-template <int KP>
 __global__ __launch_bounds__(NT) void k_fir_real8(const float* __restrict__ x, long long n,
                                                   const float* __restrict__ hist, int hist_len,
                                                   float* __restrict__ y, const Taps256 g) {
@@ -581,7 +406,7 @@ __global__ __launch_bounds__(NT) void k_fir_real8(const float* __restrict__ x, l
     f2 acc[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) acc[r] = f2{0.0f, 0.0f};
-#pragma unroll ORION_FIR8_UNROLL
+#pragma unroll 1
     for (int kb = 0; kb < KP / 16; ++kb) {
       const int pb = 8 * t + KP - 16 * kb - 16;  // as k_fir_iq8 (off = 0)
       f2 w[24];
@@ -639,63 +464,6 @@ __global__ __launch_bounds__(NT) void k_fir_real_generic(const float* __restrict
 // ------------------------------------------------------ complex FIR -------
 // HT halves of 512 outputs per tile: one load round trip (behind one barrier)
 // feeds HT x 512 outputs, so a workgroup keeps HT times the bytes in flight.
-template <int KP, int HT>
-__global__ __launch_bounds__(NT) void k_fir_iq(const f2* __restrict__ x, long long n,
-                                               const f2* __restrict__ hist, int hist_len,
-                                               f2* __restrict__ y, long long n_out, long long off,
-                                               const Taps256 g) {
-  constexpr int TH = 512, TT = TH * HT;
-  __shared__ __attribute__((aligned(16))) f2 L[TT + KP + 2];
-  const int t = threadIdx.x;
-  for (long long J = static_cast<long long>(blockIdx.x) * TT; J < n_out;
-       J += static_cast<long long>(gridDim.x) * TT) {
-    const long long org = J + off - KP;
-    constexpr int W = TT + KP + 2, PER = (W + NT - 1) / NT;
-    if (org >= 0 && org + W <= n) {  // interior tile: every load issued before any is used
-      f2 v[PER];
-#pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const int p = t + k * NT;
-        v[k] = p < W ? x[org + p] : f2{0.0f, 0.0f};
-      }
-#pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const int p = t + k * NT;
-        if (p < W) L[p] = v[k];
-      }
-    } else {
-      for (int p = t; p < W; p += NT) L[p] = load_hist(x, n, hist, hist_len, org + p);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int h = 0; h < HT; ++h) {
-      f2 acc0 = f2{0.0f, 0.0f}, acc1 = f2{0.0f, 0.0f};
-      // element e (= input index i + off) <-> L[e - org]
-      fir2_blocked<KP>(
-          [&](long long i, f2& w0, f2& w1) {
-            const f4 v = *reinterpret_cast<const f4*>(L + (i - org));
-            w0 = f2{v.x, v.y};
-            w1 = f2{v.z, v.w};
-          },
-          J + h * TH + off + 2 * t, [&](int k) { return g.g[k]; }, acc0, acc1);
-      const long long j = J + h * TH + 2 * t;
-      if (j < n_out) y[j] = acc0;
-      if (j + 1 < n_out) y[j + 1] = acc1;
-    }
-    __syncthreads();
-  }
-}
-
-// Eight consecutive outputs per lane (2048 per workgroup tile): per 16-tap block
-// a lane reads a 24-sample window (12 ds_read_b128) for 128 packed FMAs, 3.6x
-// the FMAs per LDS read of two outputs per lane. The staged tile is padded by 2
-// samples per 8 (lane stride 80 B: the 16-lane b128 groups hit distinct bank
-// slots).
-// INPLACE (FirLowpassIq::filter_aligned, fir.rs:260-276, on the caller's buffer):
-// x == y. A tile reads only its own outputs' positions [J, J + TT) from x (all
-// of them before any is written: the barrier), and every sample of its halo
-// from E, the copy k_fir_edges made of each tile boundary before this launch;
-// so no tile reads a sample another tile has overwritten.
 template <int KP, bool INPLACE = false>
 __global__ __launch_bounds__(NT) void k_fir_iq8(const f2* x, long long n,
                                                 const f2* __restrict__ hist, int hist_len,
@@ -750,7 +518,7 @@ __global__ __launch_bounds__(NT) void k_fir_iq8(const f2* x, long long n,
     f2 acc[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) acc[r] = f2{0.0f, 0.0f};
-#pragma unroll ORION_FIR8_UNROLL
+#pragma unroll 1
     for (int kb = 0; kb < KP / 16; ++kb) {
       // output j0 + r, tap 16 kb + kk reads element j0 + off + r - 16 kb - kk =
       // staged p = pb + 16 + r - kk, pb = 8 t + KP - 16 kb - 16 (even, >= 0)
@@ -843,23 +611,26 @@ inline int grid_for(long long work, int per_block) {
 
 }  // namespace
 
-void launch_rotator(const f2* x, f2* y, long long n, uint64_t k0, uint64_t step, const f2* tab,
-                    hipStream_t s) {
+void launch_osc(int mode, const f2* x, void* y, long long n, uint64_t k0, uint64_t step, uint64_t base,
+                const f2* tab, hipStream_t s) {
   if (n <= 0) return;
   const int grid = grid_for(n, kRotTile);
-  const bool a16 = reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(y) % 16 == 0;
-  if (a16) k_rotator<true, false><<<grid, NT, 0, s>>>(x, y, n, k0, step, tab);
-  else k_rotator<false, false><<<grid, NT, 0, s>>>(x, y, n, k0, step, tab);
+  const bool a16 = (mode == kNcoGen || reinterpret_cast<uintptr_t>(x) % 16 == 0) &&
+                   (mode == kUsb || reinterpret_cast<uintptr_t>(y) % 16 == 0);
+#define ORION_OSC(MD)                                                                          \
+  if (a16) k_rotator<true, MD><<<grid, NT, 0, s>>>(x, y, n, k0, step, base, tab);            \
+  else k_rotator<false, MD><<<grid, NT, 0, s>>>(x, y, n, k0, step, base, tab);
+  switch (mode) {
+    case kRotate: ORION_OSC(kRotate) break;
+    case kUsb: ORION_OSC(kUsb) break;
+    case kNcoMix: ORION_OSC(kNcoMix) break;
+    default: ORION_OSC(kNcoGen) break;
+  }
+#undef ORION_OSC
   ORION_LAUNCH_CHECK();
 }
-
-void launch_mix_usb(const f2* x, float* y, long long n, uint64_t k0, uint64_t step, const f2* tab,
-                    hipStream_t s) {
-  if (n <= 0) return;
-  const int grid = grid_for(n, kRotTile);
-  if (reinterpret_cast<uintptr_t>(x) % 16 == 0) k_rotator<true, true><<<grid, NT, 0, s>>>(x, y, n, k0, step, tab);
-  else k_rotator<false, true><<<grid, NT, 0, s>>>(x, y, n, k0, step, tab);
-  ORION_LAUNCH_CHECK();
+void launch_rotator(const f2* x, f2* y, long long n, uint64_t k0, uint64_t step, const f2* tab, hipStream_t s) {
+  launch_osc(kRotate, x, y, n, k0, step, 0, tab, s);
 }
 
 void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* hist, int hist_len,
@@ -867,21 +638,9 @@ void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* 
                         const Taps256& g, const float* g_dev, hipStream_t s) {
   if (n_out <= 0 || nch <= 0) return;
   const bool a16 = reinterpret_cast<uintptr_t>(x) % 16 == 0 && x_stride % 2 == 0;
-  // Fast polyphase path: M = 8 with K <= 128 / 256 taps; grid spread so that the
-  // whole launch has >= 2048 workgroups when channels allow.
-  static const bool legacy = [] {  // experiments: the barrier-form k_decim8
-    const char* e = std::getenv("ORION_DECIM_LEGACY");
-    return e && e[0] == '1';
-  }();
-  static const bool w2 = [] {  // experiments: k_decim_w (two outputs per lane) instead of k_decim_w4
-    const char* e = std::getenv("ORION_DECIM_W2");
-    return e && e[0] == '1';
-  }();
-  static const bool q4 = [] {  // k_decim_w4q: four waves per workgroup, three per SIMD (ORION_DECIM_Q4=0: off)
-    const char* e = std::getenv("ORION_DECIM_Q4");
-    return !(e && e[0] == '0');
-  }();
-  if (M == 8 && K > 128 && K <= 256 && hist_len >= 8 * 32 && !legacy && !w2 && q4) {
+  // M = 8 with 129..256 taps (C3): k_decim_w4q, four waves per workgroup sharing one
+  // tap table (three waves per SIMD); M = 8 with <= 128 taps: k_decim_w4.
+  if (M == 8 && K > 128 && K <= 256 && hist_len >= 8 * 32) {
     static int capq = 0;
     if (capq == 0) {
       int per_cu = 0, dev = 0, ncu = 0;
@@ -908,13 +667,11 @@ void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* 
     ORION_LAUNCH_CHECK();
     return;
   }
-  if (M == 8 && K <= 256 && hist_len >= 8 * (K <= 128 ? 16 : 32) && !legacy) {
-    static int caps[2] = {0, 0};
-    int& cap = caps[w2 ? 1 : 0];
+  if (M == 8 && K <= 256 && hist_len >= 8 * (K <= 128 ? 16 : 32)) {
+    static int cap = 0;
     if (cap == 0) {
       int per_cu = 0, dev = 0, ncu = 0;
-      if (w2) ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decim_w<32, true, false>, 64, 0));
-      else ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decim_w4<32, true, false>, 64, 0));
+      ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decim_w4<32, true, false>, 64, 0));
       ORION_HIP(hipGetDevice(&dev));
       ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
       cap = std::max(4, per_cu & ~3) * std::max(1, ncu);  // a multiple of 4 per CU: balanced SIMDs
@@ -936,25 +693,8 @@ void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* 
     if (a16) KK<QQ, true, false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
     else KK<QQ, false, false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
   }
-    if (w2) {
-      if (K <= 128) { ORION_DW(k_decim_w, 16) } else { ORION_DW(k_decim_w, 32) }
-    } else {
-      if (K <= 128) { ORION_DW(k_decim_w4, 16) } else { ORION_DW(k_decim_w4, 32) }
-    }
+    if (K <= 128) { ORION_DW(k_decim_w4, 16) } else { ORION_DW(k_decim_w4, 32) }
 #undef ORION_DW
-  } else if (M == 8 && K <= 256 && hist_len >= 8 * (K <= 128 ? 16 : 32)) {
-    const long long tiles = (n_out + 511) / 512;
-    long long gx = tiles;
-    const long long cap = (4 * kMaxGrid) / nch > 0 ? (4 * kMaxGrid) / nch : 1;
-    if (gx > cap) gx = cap;
-    const dim3 grid(static_cast<unsigned>(gx), nch);
-    if (K <= 128) {
-      if (a16) k_decim8<16, true><<<grid, NT, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g);
-      else k_decim8<16, false><<<grid, NT, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g);
-    } else {
-      if (a16) k_decim8<32, true><<<grid, NT, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g);
-      else k_decim8<32, false><<<grid, NT, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g);
-    }
   } else {
     const dim3 grid(grid_for(n_out, NT), nch);
     k_decim_generic<<<grid, NT, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, M, K, g_dev);
@@ -970,23 +710,10 @@ void launch_decim(const f2* x, long long n, const f2* hist, int hist_len, f2* ou
 void launch_fir_real(const float* x, long long n, const float* hist, int hist_len, float* y, int K,
                      const Taps256& g, const float* g_dev, hipStream_t s) {
   if (n <= 0) return;
-  static const bool two = [] {
-    const char* e = std::getenv("ORION_FIR_REAL2");  // timing comparisons: two outputs per lane
-    return e && std::atoi(e) == 1;
-  }();
-  if (!two && K <= 256 && hist_len >= K) {
-    const int g16 = static_cast<int>(std::min<long long>(kMaxGrid, (n + 16 * NT - 1) / (16 * NT)));
-    if (K <= 64 && hist_len >= 64) k_fir_real8<64><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g);
-    else if (K <= 128 && hist_len >= 128) k_fir_real8<128><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g);
-    else if (K <= 256 && hist_len >= 256) k_fir_real8<256><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g);
-    else k_fir_real_generic<<<grid_for(n, NT), NT, 0, s>>>(x, n, hist, hist_len, y, K, g_dev);
-    ORION_LAUNCH_CHECK();
-    return;
-  }
-  const int grid = grid_for(n, 512);
-  if (K <= 64 && hist_len >= 64) k_fir_real<64><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, g);
-  else if (K <= 128 && hist_len >= 128) k_fir_real<128><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, g);
-  else if (K <= 256 && hist_len >= 256) k_fir_real<256><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, g);
+  const int g16 = static_cast<int>(std::min<long long>(kMaxGrid, (n + 16 * NT - 1) / (16 * NT)));
+  if (K <= 64 && hist_len >= 64) k_fir_real8<64><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g);
+  else if (K <= 128 && hist_len >= 128) k_fir_real8<128><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g);
+  else if (K <= 256 && hist_len >= 256) k_fir_real8<256><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g);
   else k_fir_real_generic<<<grid_for(n, NT), NT, 0, s>>>(x, n, hist, hist_len, y, K, g_dev);
   ORION_LAUNCH_CHECK();
 }
@@ -994,20 +721,12 @@ void launch_fir_real(const float* x, long long n, const float* hist, int hist_le
 void launch_fir_iq(const f2* x, long long n, const f2* hist, int hist_len, f2* y, long long n_out,
                    long long off, int K, const Taps256& g, const float* g_dev, hipStream_t s) {
   if (n_out <= 0) return;
-  const int grid = grid_for(n_out, 512);
-  static const bool legacy = [] {  // timing comparisons only: two outputs per lane
-    const char* e = std::getenv("ORION_FIR_IQ2");
-    return e && std::atoi(e) != 0;
-  }();
-  if (!legacy && K <= 256 && hist_len >= (K <= 64 ? 64 : K <= 128 ? 128 : 256)) {
+  if (K <= 256 && hist_len >= (K <= 64 ? 64 : K <= 128 ? 128 : 256)) {
     const int g8 = grid_for(n_out, 8 * NT);
     if (K <= 64) k_fir_iq8<64><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
     else if (K <= 128) k_fir_iq8<128><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
     else k_fir_iq8<256><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
-  } else if (K <= 64 && hist_len >= 64) k_fir_iq<64, kFirHT><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
-  else if (K <= 128 && hist_len >= 128) k_fir_iq<128, kFirHT><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
-  else if (K <= 256 && hist_len >= 256) k_fir_iq<256, kFirHT><<<grid, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
-  else k_fir_iq_generic<<<grid_for(n_out, NT), NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, K, g_dev);
+  } else k_fir_iq_generic<<<grid_for(n_out, NT), NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, K, g_dev);
   ORION_LAUNCH_CHECK();
 }
 

@@ -1,5 +1,6 @@
 // k_mod.hip — on-device analog modulators for gfx950.
 //   AmDsbMod::process          modulate/am.rs:44-120
+//   PmDirectPhaseMod::process  modulate/pm.rs:36-47
 //   FmPhaseAccumMod::process   modulate/fm.rs:45-74 (+ mix_with_nco, dsp/nco.rs:62-66)
 //   SsbPhasingMod::process     modulate/ssb.rs:43-114 (front and back of the two
 //                              LpCascade scans, which run on the k_scan kernels)
@@ -32,6 +33,20 @@ __global__ __launch_bounds__(NT) void k_am_mod(const float* __restrict__ x, f2* 
     const float m = v * g;
     const f2 r = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
     y[i] = f2{m * r.x, m * r.y};
+  }
+}
+
+// modulate/pm.rs:36-47 PmDirectPhaseMod: phi = kp x; base = (cos phi, sin phi) * gain
+// (num-complex Complex * f32); out = mix_with_nco(base, rf) (the non-FMA product,
+// nco.rs:63-66) with the RF phasor after k0 + i + 1 steps.
+__global__ __launch_bounds__(NT) void k_pm_mod(const float* __restrict__ x, f2* __restrict__ y, long long n,
+                                               uint64_t k0, uint64_t step, float kp, float g) {
+  for (long long i = blockIdx.x * static_cast<long long>(NT) + threadIdx.x; i < n;
+       i += static_cast<long long>(gridDim.x) * NT) {
+    const float phi = kp * x[i];
+    const float br = cosf(phi) * g, bi = sinf(phi) * g;
+    const f2 r = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
+    y[i] = f2{br * r.x - bi * r.y, br * r.y + bi * r.x};
   }
 }
 
@@ -219,7 +234,8 @@ __device__ __forceinline__ double fm_ld64(const uint32_t* p) {
 __global__ __launch_bounds__(NT) void k_fm_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
                                                   float kf, float gain, uint32_t* __restrict__ rec, uint32_t epoch,
                                                   const double* __restrict__ carry_in, double* __restrict__ carry_out,
-                                                  uint64_t k0, uint64_t step, const f2* __restrict__ rtab) {
+                                                  uint64_t k0, uint64_t step, const f2* __restrict__ rtab,
+                                                  int* __restrict__ err, uint32_t spin) {
   __shared__ double tot[NT / 64];
   __shared__ double excl_sh;
   __shared__ float xs[kFmCH + kFmCH / 16];
@@ -266,8 +282,12 @@ __global__ __launch_bounds__(NT) void k_fm_mod_sp(const float* __restrict__ x, f
       bool closes = true;
       if (k >= 0) {
         const uint32_t* pr = rec + static_cast<long long>(k) * 8;
-        int it = 0;
-        while (fm_ld(pr + 6) != epoch && fm_ld(pr + 7) != epoch && ++it < (1 << 22)) __builtin_amdgcn_s_sleep(2);
+        bool seen = false;  // bounded wait (spin 0: time out at once, test-only)
+        for (uint32_t it = 0; it < spin && !seen; ++it) {
+          seen = fm_ld(pr + 6) == epoch || fm_ld(pr + 7) == epoch;
+          if (!seen) __builtin_amdgcn_s_sleep(2);
+        }
+        if (!seen) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         closes = fm_ld(pr + 7) == epoch;
         v = closes ? fm_ld64(pr + 2) : fm_ld64(pr);
       } else {
@@ -328,6 +348,12 @@ void launch_ssb_mod_front(const float* x, float* u, long long n, uint64_t k0, ui
   ORION_LAUNCH_CHECK();
 }
 
+void launch_pm_mod(const float* x, f2* y, long long n, uint64_t k0, uint64_t step, float kp, float g, hipStream_t s) {
+  if (n <= 0) return;
+  k_pm_mod<<<grid_for(n), NT, 0, s>>>(x, y, n, k0, step, kp, g);
+  ORION_LAUNCH_CHECK();
+}
+
 void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, uint64_t step, float side, hipStream_t s) {
   if (n <= 0) return;
   k_ssb_mod_back<<<grid_for(n), NT, 0, s>>>(v, y, n, k0, step, side);
@@ -338,12 +364,12 @@ long long fm_mod_chunks(long long n) { return (n + kFmCH - 1) / kFmCH; }
 
 void launch_fm_mod_sp(const float* x, f2* y, long long n, float kf, float gain, uint32_t* rec, uint32_t epoch,
                       const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
-                      hipStream_t s) {
+                      int* err, hipStream_t s) {
   if (n <= 0) return;
   const long long nchunk = fm_mod_chunks(n);
   if (nchunk > (1LL << 30)) throw HipError("FM modulator: input too long");
   k_fm_mod_sp<<<static_cast<int>(nchunk), NT, 0, s>>>(x, y, n, kf, gain, rec, epoch, carry_in, carry_out, k0, step,
-                                                     rtab);
+                                                     rtab, err, spin_limit());
   ORION_LAUNCH_CHECK();
 }
 int fm_mod_rtab_len() { return kFmC; }

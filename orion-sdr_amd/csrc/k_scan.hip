@@ -36,6 +36,10 @@ template <> struct RecSel<RecK::LP4> {
   using T = RecLP4;
   __device__ static T make(const ScanCoef& c) { return T{{c.b0, c.b1, c.b2, c.a1, c.a2}}; }
 };
+template <> struct RecSel<RecK::BQ> {
+  using T = RecBQ;
+  __device__ static T make(const ScanCoef& c) { return T{{c.b0, c.b1, c.b2, c.a1, c.a2}}; }
+};
 template <> struct RecSel<RecK::LPDC> {
   using T = RecLpDc;
   __device__ static T make(const ScanCoef& c) { return T{{c.b0, c.b1, c.b2, c.a1, c.a2}, c.r}; }
@@ -431,6 +435,16 @@ __device__ __forceinline__ double sp_ld64(const uint32_t* p) {
   const unsigned long long lo = sp_ld(p), hi = sp_ld(p + 1);
   return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
 }
+// Bounded wait until flag f1 or f2 holds `epoch`: at most `spin` polls (0: give up at
+// once, test-only). false on timeout: the caller flags the handle's error word (the
+// record it then reads may be stale; the host reports the call as failed).
+__device__ __forceinline__ bool sp_wait2(const uint32_t* f1, const uint32_t* f2, uint32_t epoch, uint32_t spin) {
+  for (uint32_t it = 0; it < spin; ++it) {
+    if (sp_ld(f1) == epoch || sp_ld(f2) == epoch) return true;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
 // (m1, d1) then (m2, d2): y -> m2 (m1 y + d1) + d2
 __device__ __forceinline__ void dc_combine(double m1, double d1, double& m2, double& d2) {
   d2 = __builtin_fma(m2, d1, d2);
@@ -446,7 +460,7 @@ __device__ __forceinline__ int posS(int e) { return e + e / SC; }
 template <Pre PR, int SC>
 __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long base, int cnt, float* sb) {
   static_assert(SC * NT <= 2 * kScanCH, "two phasor table spans cover the chunk");
-  if constexpr (PR == Pre::Real) {  // DcBlocker: f32 input
+  if constexpr (PR == Pre::Real || PR == Pre::RealLp || PR == Pre::RealLpSqrt) {  // f32 input
     const float* __restrict__ xr = static_cast<const float*>(a.x) + ch * a.x_stride + base;
     float v[SC];
 #pragma unroll
@@ -498,7 +512,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   // (C = 2 kScanC: the same powers shifted by one; s = 5 is then kM64); A^(64 C) per wave
   static_assert(SC == kScanC || SC == 2 * kScanC, "lane run");
   constexpr int kPw = ScanMatsLayout::kPwc + (SC == kScanC ? 0 : 1);
-  constexpr int kWv = SC == kScanC ? ScanMatsLayout::kM64 : ScanMatsLayout::kM128;
+  [[maybe_unused]] constexpr int kWv = SC == kScanC ? ScanMatsLayout::kM64 : ScanMatsLayout::kM128;
   __shared__ float sb[PADN];
   __shared__ double tot[4][S];
   __shared__ double dtot[4][2];
@@ -605,7 +619,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   for (int i = 0; i < C; ++i)
     if (t * C + i < cnt) {
       xs[i] = lp.step(ef, xs[i]);  // LP output x (f32, reference update)
-      if constexpr (PR == Pre::AmSqrt) xs[i] = sqrtf(xs[i]);  // am.rs:54 process_mapped(.., f32::sqrt)
+      if constexpr (PR == Pre::AmSqrt || PR == Pre::RealLpSqrt) xs[i] = sqrtf(xs[i]);  // process_mapped(.., f32::sqrt)
     }
   __syncthreads();  // every lane has read its sb inputs
 #pragma unroll
@@ -681,8 +695,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
       bool closes = true;
       if (k >= 0) {
         const uint32_t* pr = rec + (static_cast<long long>(ch) * nchunk + k) * 8;
-        int it = 0;
-        while (sp_ld(pr + 6) != epoch && sp_ld(pr + 7) != epoch && ++it < (1 << 22)) __builtin_amdgcn_s_sleep(2);
+        if (!sp_wait2(pr + 6, pr + 7, epoch, a.spin)) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         closes = sp_ld(pr + 7) == epoch;
         v = closes ? sp_ld64(pr + 4) : sp_ld64(pr);
         mk = closes ? 1.0 : sp_ld64(pr + 2);
@@ -865,8 +878,7 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
       for (int i = 0; i < S; ++i) cin_sh[i] = static_cast<double>(ci[i]);
     } else {
       const uint32_t* pr = rec + (static_cast<long long>(ch) * nchunk + c - 1) * 16;
-      int it = 0;
-      while (sp_ld(pr + 15) != epoch && ++it < (1 << 22)) __builtin_amdgcn_s_sleep(2);
+      if (!sp_wait2(pr + 15, pr + 15, epoch, a.spin)) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #pragma unroll
       for (int i = 0; i < S; ++i) cin_sh[i] = sp_ld64(pr + 2 * i);
     }
@@ -1088,6 +1100,7 @@ int scan_state_dim(RecK rec) {
     case RecK::LP4: return 4;
     case RecK::LPDC: return 6;
     case RecK::DC: return 2;
+    case RecK::BQ: return 2;
     default: return 1;
   }
 }
@@ -1111,33 +1124,25 @@ long long lpdc_sp_demod_chunks(long long n, int sc, int warm) {
   const long long ch = static_cast<long long>(sc) * NT;
   return n <= ch ? 1 : 1 + (n - ch + (ch - warm) - 1) / (ch - warm);
 }
-int lpdc_sp_lane_samples() {
-  static const int sc = [] {
-    const char* e = std::getenv("ORION_SP_C16");
-    return e && std::atoi(e) == 1 ? kScanC : kSpC;
-  }();
-  return sc;
-}
 
 void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, uint32_t* rec, uint32_t epoch,
                     hipStream_t s) {
   if (a.n <= 0 || nch <= 0) return;
-  const int sc = lpdc_sp_lane_samples();
-  const long long grid = lpdc_sp_demod_chunks(a.n, sc, pre == Pre::Real ? 0 : kSpWarm) * nch;
+  const long long grid = lpdc_sp_demod_chunks(a.n, kSpC, pre == Pre::Real ? 0 : kSpWarm) * nch;
   if (grid > (1LL << 31) - 1) throw HipError("single-pass scan grid too large");
   const int g = static_cast<int>(grid);
   if (pre == Pre::Ssb) {
-    if (sc == kSpC) k_lpdc_sp<Pre::Ssb, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
-    else k_lpdc_sp<Pre::Ssb, kScanC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    k_lpdc_sp<Pre::Ssb, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else if (pre == Pre::AmAbs) {
-    if (sc == kSpC) k_lpdc_sp<Pre::AmAbs, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
-    else k_lpdc_sp<Pre::AmAbs, kScanC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    k_lpdc_sp<Pre::AmAbs, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else if (pre == Pre::Real) {
-    if (sc == kSpC) k_lpdc_sp<Pre::Real, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
-    else k_lpdc_sp<Pre::Real, kScanC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    k_lpdc_sp<Pre::Real, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else if (pre == Pre::AmSqrt) {
-    if (sc == kSpC) k_lpdc_sp<Pre::AmSqrt, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
-    else k_lpdc_sp<Pre::AmSqrt, kScanC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    k_lpdc_sp<Pre::AmSqrt, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+  } else if (pre == Pre::RealLp) {
+    k_lpdc_sp<Pre::RealLp, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+  } else if (pre == Pre::RealLpSqrt) {
+    k_lpdc_sp<Pre::RealLpSqrt, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else {
     throw std::invalid_argument("single-pass LpDc scan: unsupported front end");
   }
@@ -1148,6 +1153,7 @@ long long scan_sp_chunks(long long n) { return (n + kSpCH - 1) / kSpCH; }
 
 bool scan_sp_supported(RecK rec, Pre pre, Post post) {
   return (rec == RecK::LP4 && post == Post::Id && (pre == Pre::Real || pre == Pre::Fm || pre == Pre::Pm)) ||
+         (rec == RecK::BQ && pre == Pre::Real && post == Post::Id) ||
          (rec == RecK::LP4 && pre == Pre::AmSqrt && post == Post::Sqrt) ||
          (rec == RecK::ONEPOLE && pre == Pre::Cw && post == Post::Gain);
 }
@@ -1168,6 +1174,7 @@ void launch_scan_sp(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, ui
     return;                                                                                          \
   }
   ORION_SP(LP4, Real, Id)
+  ORION_SP(BQ, Real, Id)
   ORION_SP(LP4, Fm, Id)
   ORION_SP(LP4, Pm, Id)
   ORION_SP(LP4, AmSqrt, Sqrt)
@@ -1181,6 +1188,9 @@ void launch_scan(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, hipSt
 #define ORION_SCAN(RK, PR, PO) \
   if (rec == RecK::RK && pre == Pre::PR && post == Post::PO) return run3<RecK::RK, Pre::PR, Post::PO>(a, nch, s);
   ORION_SCAN(LP4, Real, Id)
+  ORION_SCAN(LP4, Real, Sqrt)
+  ORION_SCAN(BQ, Real, Id)
+  ORION_SCAN(LPDC, Real, Id)
   ORION_SCAN(DC, Real, Id)
   ORION_SCAN(LP4, Fm, Id)
   ORION_SCAN(LP4, Pm, Id)

@@ -18,6 +18,8 @@ constexpr int kRotTile = 4096;
 // ---- analog modulators (k_mod.hip; modulate/am.rs, fm.rs, ssb.rs) ----
 void launch_am_mod(const float* x, f2* y, long long n, uint64_t k0, uint64_t step, float cl, float mi, float g,
                    bool clamp, hipStream_t s);
+// pm.rs:36-47: out = mix_with_nco((cos kp x, sin kp x) * g, rf phasor k0 + i + 1)
+void launch_pm_mod(const float* x, f2* y, long long n, uint64_t k0, uint64_t step, float kp, float g, hipStream_t s);
 // u = [x p.re | x p.im] (planar, 2n floats), p = audio NCO phasor k0 + i + 1
 void launch_ssb_mod_front(const float* x, float* u, long long n, uint64_t k0, uint64_t step, hipStream_t s);
 // y = (v[i], side v[n + i]) * rf phasor k0 + i + 1
@@ -28,19 +30,23 @@ void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, uint64
 long long fm_mod_chunks(long long n);
 // Single-pass form: rec = fm_mod_chunks(n) * 8 u32 look-back records (zeroed when
 // allocated), epoch = this launch's tag (never reused while a record may hold it).
+// err: the handle's host-visible error word (a look-back wait that timed out).
 void launch_fm_mod_sp(const float* x, f2* y, long long n, float kf, float gain, uint32_t* rec, uint32_t epoch,
                       const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
-                      hipStream_t s);
+                      int* err, hipStream_t s);
 int fm_mod_rtab_len();
 void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, double* sums,
                    const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
                    hipStream_t s);
 void launch_rotator(const f2* x_dev, f2* y_dev, long long n, uint64_t k0, uint64_t step_q64,
                     const f2* tab_dev, hipStream_t s);
-// SsbProductDemod front end helper / Rotator::mix_usb_block (rotator.rs:88-94):
-// y = fma(x.re, p.re, x.im*p.im).
-void launch_mix_usb(const f2* x_dev, float* y_dev, long long n, uint64_t k0, uint64_t step_q64,
-                    const f2* tab_dev, hipStream_t s);
+// Oscillator blocks (k_fir.hip k_rotator): output i uses the phasor of phase
+// base + (k0 + i + 1) step (Q0.64). mode: 0 Rotator::rotate_block (rotator.rs:74-85,
+// cf32 -> cf32), 1 Rotator::mix_usb_block (rotator.rs:88-94, cf32 -> f32), 2
+// mix_with_nco (nco.rs:63-66, cf32 -> cf32, non-FMA), 3 Nco::next_cs (nco.rs:42-58,
+// no input, cf32 phasors out).
+void launch_osc(int mode, const f2* x_dev, void* y_dev, long long n, uint64_t k0, uint64_t step_q64, uint64_t base,
+                const f2* tab_dev, hipStream_t s);
 
 // ---------------------------------------------------------- FIR family --
 // Decimating FIR at the kept outputs only: out[j] = sum_k g[k] * x[M*j - k],
@@ -75,7 +81,8 @@ void launch_hist_update_r(const float* x_dev, long long n, const float* old_dev,
                           int hist_len, hipStream_t s);
 
 // ------------------------------------------------------------ WBFM chain --
-// Two launches per call (k_wbfm.hip):
+// Default: one launch per call (k_wbfm_seg, see k_wbfm.hip). The two-kernel path
+// (any IIR design):
 //  front: NCO mix -> polyphase decim x8 (<= 128 taps) -> FM discriminator,
 //         writing phi (f32, 1/8 rate) — 8 B in, 0.5 B out per input sample;
 //  back : LpCascade (wave scan, f64 carries, warm-up across workgroups) ->
@@ -102,22 +109,16 @@ struct WbfmBackConst {
   double pw[6 * 16];          // (A^C)^(2^s), s = 0..5 (C = kBackC)
   double mw[16];              // A^(64 C): one wave's span
 };
-// Fused single-kernel chain (k_wbfm_fused): one wave per range of kFuL outputs.
-#ifndef ORION_FU_N
-#define ORION_FU_N 16
-#endif
-constexpr int kFuN = ORION_FU_N;                     // front tiles (128 outputs) per range
-constexpr int kFuL = kFuN * 128;                     // 2048 outputs per wave range
-constexpr int kFuC = kFuL / 128;                     // IIR samples per lane and half (16)
-constexpr int kFuTail = 128;                         // IIR outputs handed to the next range
-constexpr int kFuSlot = 144;                         // u32 words per hand-off slot
-// slot layout (u32 words): [0,2) last decimated sample, [2,10) zero-state IIR
-// aggregate (4 f64), [16,144) last 128 IIR outputs. Flags: 3 u32 per slot.
+// Segmented single-kernel chain (k_wbfm_seg): sub-range backs of kSgL outputs.
+constexpr int kFuTail = 128;                         // IIR outputs handed to the next segment (FIR history)
+constexpr int kFuSlot = 144;                         // u32 words of a segment's end-state record
+// record layout (u32 words): [2,10) end state of the IIR (4 f64), [16,144) last
+// 128 IIR outputs. Flags: 3 u32 per segment (the epoch of the last publish).
 struct WbfmFusedConst {
   float a[128];               // audio taps, quirk-mapped, zero padded
   float b0, b1, b2, a1, a2;   // LpCascade biquad (iir.rs:49-71)
-  double pw[6 * 16];          // (A^kFuC)^(2^s)
-  double mh[16];              // A^(kFuL/2): one half range
+  double pw[6 * 16];          // (A^kSgC)^(2^s)
+  double mh[16];              // A^(kSgL/2): one half sub-range (read by iir16 as pw[6])
 };
 struct WbfmArgs {
   const f2* x;  long long x_stride;  long long n;
@@ -128,40 +129,27 @@ struct WbfmArgs {
   const f2* tab;                                    // [nch][kWbfmNS] e^{j theta p}
   const float* carry_in; float* carry_out;          // [nch][kWbfmCarry]
   const f2* hist_in; f2* hist_out;                  // [nch][kWbfmHist]
-  const double* lanemats;                           // A^(C L), L = 0..63 (16 doubles each)
-  // fused chain only
-  const double* lanemats_fu;                        // A^(kFuC L), L = 0..63
-  const double* lanemats_sg;                        // A^(kSgC L), L = 0..63 (k_wbfm_seg)
-  uint32_t* hand;                                   // [slots][kFuSlot] hand-off data
+  const double* lanemats;                           // A^(C L), L = 0..63 (16 doubles each; k_wbfm_back)
+  // segmented chain only
+  uint32_t* hand;                                   // [slots][kSeg4Slot] hand-off records
   uint32_t* flags;                                  // [slots][3] epoch of the last publish
-  int* err;                                         // set if a hand-off wait timed out
+  int* err;                                         // host-visible error word: a hand-off wait timed out
+  uint32_t spin;                                    // polls before a wait times out (kernels.hpp kSpinDefault)
   uint32_t epoch;                                   // this launch's tag (never 0)
   long long* trace;                                 // debug: per-wave phase timestamps (or null)
-  int fu_abl;                                       // timing ablations of the fused kernel (0)
 };
 constexpr int kFuTracePoints = 16;
 void launch_wbfm(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmBackConst& b, int nch,
                  hipStream_t s);
-// Fused chain: requires ||A^kFuL|| negligible (the block checks it); returns the
-// number of hand-off slots it needs for (n_dec, nch).
-long long wbfm_fused_slots(long long n_dec, int nch);
-// Segmented fused chain (k_wbfm_seg): sub-ranges of kSgL outputs, one round of
-// waves. Requires ||A^(kSgL - 128)|| negligible (the block checks it).
+// Segmented single-kernel chain (k_wbfm_seg): sub-ranges of kSgL outputs, one round
+// of waves. Requires ||A^(kSgL - 128)|| negligible (the block checks it).
 constexpr int kSgL = 1024;                           // outputs per sub-range
 constexpr int kSgC = kSgL / 128;                     // IIR samples per lane and half (8)
-constexpr int kSg2Slot = kSgL;                       // u32 words per k_wbfm_seg2 hand-off slot (phi)
-constexpr int kSeg4Slot = kFuSlot + kSg2Slot;        // k_wbfm_seg4: end-state record, then sub-range 0's phi
+constexpr int kSeg4Slot = kFuSlot + kSgL;            // u32 words per segment: end-state record, then sub-range 0's phi
 long long wbfm_seg_slots(long long n_dec, int nch);
-// spread: k_wbfm_seg2 (FIR spread over the next sub-range's tiles, first sub-range
-// handed to the predecessor); else k_wbfm_seg. max_segments > 0 caps the waves.
+// max_segments > 0 caps the waves (default: the resident capacity).
 void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
-                     int max_segments, int variant, hipStream_t s);
-// Wave-specialised segments (k_wbfm_ws): streaming and back waves in one
-// workgroup per CU; same geometry requirement and hand-off slots as k_wbfm_seg2.
-void launch_wbfm_ws(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
-                    int max_segments, hipStream_t s);
-void launch_wbfm_fused(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
-                       hipStream_t s);
+                     int max_segments, hipStream_t s);
 
 int device_cus();
 // On-box bandwidth probe (k_diag.hip): a streaming read of the first

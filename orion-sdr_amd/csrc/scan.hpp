@@ -36,9 +36,11 @@ enum class Pre : int {
   AmSqrt = 4,  // demodulate/am.rs:201-205, LP stage before the sqrt map
   AmAbs = 5,   // demodulate/am.rs:232-239
   Cw = 6,      // demodulate/cw.rs:38-39
+  RealLp = 7,      // f32 input through the LP4 (+ DC) of LpDcCascade::process (iir.rs:151-165)
+  RealLpSqrt = 8,  // the same with sqrt between LP4 and DC: process_mapped(x, f32::sqrt) (iir.rs:170-186)
 };
 enum class Post : int { Id = 0, Sqrt = 1, Gain = 2 };
-enum class RecK : int { LP4 = 0, LPDC = 1, DC = 2, ONEPOLE = 3 };
+enum class RecK : int { LP4 = 0, LPDC = 1, DC = 2, ONEPOLE = 3, BQ = 4 };
 
 // Matrices of the chunk transition, all S x S row-major f32, in one device buffer.
 struct ScanMatsLayout {
@@ -73,6 +75,8 @@ struct ScanArgs {
   const float* carry_in;               // [ch][kScanCarry]
   float* carry_out;                    // [ch][kScanCarry]
   ScanCoef c;
+  int* err;                            // host-visible error word: a look-back wait timed out (single pass)
+  uint32_t spin;                       // polls before a look-back wait times out (hip_common.hpp)
 };
 
 void launch_scan(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, hipStream_t s);
@@ -84,11 +88,10 @@ constexpr int kSpWarm = 256;
 long long lpdc_sp_chunks(long long n);
 // k_lpdc_sp's own geometry: kSpC samples per lane (2 kScanC: the wave scans and the
 // LP4 state folding cost per lane, not per sample, so longer lane runs amortise them),
-// chunks of kSpCH samples; ORION_SP_C16=1 runs the kScanC form (timing comparisons).
+// chunks of kSpCH samples.
 constexpr int kSpC = 2 * kScanC;
 constexpr int kSpCH = kSpC * kScanNT;
 long long lpdc_sp_demod_chunks(long long n, int sc, int warm);  // warm: kSpWarm, or 0 for the DcBlocker alone
-int lpdc_sp_lane_samples();  // kSpC, or kScanC under ORION_SP_C16=1
 // SsbPhasingMod in one pass (k_ssb_mod_sp): valid when ||A_lp^kSpWarm|| is
 // negligible; mats_lp = the LP4 scan matrices; carry = [I 4][Q 4] floats.
 void launch_ssb_mod_sp(const float* x, f2* y, long long n, uint64_t k0, uint64_t step_aud, uint64_t step_rf,

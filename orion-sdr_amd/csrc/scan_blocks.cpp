@@ -27,11 +27,9 @@ class ScanStage {
       const auto m = mat_pow(ss.A, ss.S, kSpCH);
       double fro = 0.0;
       for (double v : m) fro += v * v;
-      const char* e = std::getenv("ORION_SCAN_3K");  // timing comparisons: keep the three-kernel scan
-      sp1_ok_ = std::sqrt(fro) < 1e-10 && !(e && std::atoi(e) == 1);
+      sp1_ok_ = std::sqrt(fro) < 1e-10;
       // the shortest horizon of 2^trs lane runs (kSpC samples each) the stage forgets within
-      const char* et = std::getenv("ORION_SCAN_FULL");  // timing comparisons: the untruncated lane scan
-      for (int trs = 3; trs <= 5 && !(et && std::atoi(et) == 1); ++trs) {
+      for (int trs = 3; trs <= 5; ++trs) {
         const auto mw = mat_pow(ss.A, ss.S, static_cast<uint64_t>(kSpC) << trs);
         double fw = 0.0;
         for (double v : mw) fw += v * v;
@@ -43,11 +41,11 @@ class ScanStage {
     }
     // DcBlocker alone: k_lpdc_sp's DC look-back without the LP4 (pole ~1: no chunk forgets)
     if (rec == RecK::DC && pre == Pre::Real && post == Post::Id) {
-      const char* e = std::getenv("ORION_SCAN_3K");
-      sp_ok_ = !(e && std::atoi(e) == 1);
+      sp_ok_ = true;
       dc_only_ = true;
     }
-    if (rec == RecK::LPDC && (pre == Pre::Ssb || pre == Pre::AmAbs || pre == Pre::AmSqrt)) {
+    if (rec == RecK::LPDC && (pre == Pre::Ssb || pre == Pre::AmAbs || pre == Pre::AmSqrt || pre == Pre::RealLp ||
+                              pre == Pre::RealLpSqrt)) {
       const StateSpace lp = lp_cascade_ss(BiquadCoeffs{c.b0, c.b1, c.b2, c.a1, c.a2});
       const auto m = mat_pow(lp.A, 4, kSpWarm);
       double fro = 0.0;
@@ -98,7 +96,7 @@ class ScanStage {
   ScanCoef& coef() { return c_; }
   void set_translate(bool on) { translate_ = on; }
   void run(const void* x, long long x_stride, long long n, void* y, long long y_stride, long long k0,
-           hipStream_t s) {
+           int* err, hipStream_t s) {
     const long long nblk = (n + kScanCH - 1) / kScanCH;
     ws_.resize(static_cast<size_t>(2 * nblk * nch_ * S_ + 16) * sizeof(double));
     ScanArgs a{};
@@ -117,10 +115,11 @@ class ScanStage {
     a.carry_in = carry_[cur_].as<float>();
     a.carry_out = carry_[cur_ ^ 1].as<float>();
     a.c = c_;
+    a.err = err;
+    a.spin = spin_limit();
     if ((sp_ok_ || sp1_ok_) && mode_ == 0) {
       const size_t words = sp1_ok_ ? static_cast<size_t>(scan_sp_chunks(n)) * nch_ * 16
-                                   : static_cast<size_t>(lpdc_sp_demod_chunks(n, lpdc_sp_lane_samples(),
-                                                                              dc_only_ ? 0 : kSpWarm)) * nch_ * 8;
+                                   : static_cast<size_t>(lpdc_sp_demod_chunks(n, kSpC, dc_only_ ? 0 : kSpWarm)) * nch_ * 8;
       if (words * 4 > rec_buf_.size()) {
         rec_buf_.resize(words * 4);
         rec_buf_.zero(s);
@@ -200,12 +199,18 @@ class OneStageBlock : public ScanBlock {
   }
   ScanStage& stage() { return *st_; }
   std::vector<float> taps(int) const override { return coef_; }
+  int configure(int option, long long value) override {
+    if (option != kOptScanPath) return -4;
+    if (value != 0 && value != 1) return -3;
+    st_->set_mode(static_cast<int>(value));
+    return 0;
+  }
   std::vector<float> coef_;
 
  protected:
   void run(const void* in, size_t stride, size_t n, void* out, size_t out_stride, hipStream_t s) override {
     st_->run(in, static_cast<long long>(stride), static_cast<long long>(n), out, static_cast<long long>(out_stride),
-             static_cast<long long>(k0_), s);
+             static_cast<long long>(k0_), dev_err(), s);
   }
   void reset_state() override { st_->set_carry(carry0_); }
   std::unique_ptr<ScanStage> st_;
@@ -236,6 +241,13 @@ class AmBlock final : public ScanBlock {
     if (!sq_->lpdc_single_pass()) sq_.reset();
     reset_state();
   }
+  int configure(int option, long long value) override {
+    if (option != kOptScanPath) return -4;
+    if (value != 0 && value != 1) return -3;
+    for (auto* st : {lp_.get(), dc_.get(), lpdc_.get()}) st->set_mode(static_cast<int>(value));
+    three_ = value == 1;
+    return 0;
+  }
   void set_abs(float k1, float k2) {
     abs_ = true;
     lpdc_->coef().k1 = k1;
@@ -249,19 +261,19 @@ class AmBlock final : public ScanBlock {
   void run(const void* in, size_t stride, size_t n, void* out, size_t out_stride, hipStream_t s) override {
     if (abs_) {
       lpdc_->run(in, static_cast<long long>(stride), static_cast<long long>(n), out, static_cast<long long>(out_stride),
-                 static_cast<long long>(k0_), s);
+                 static_cast<long long>(k0_), dev_err(), s);
       return;
     }
-    if (sq_) {
+    if (sq_ && !three_) {
       sq_->run(in, static_cast<long long>(stride), static_cast<long long>(n), out, static_cast<long long>(out_stride),
-               static_cast<long long>(k0_), s);
+               static_cast<long long>(k0_), dev_err(), s);
       return;
     }
     tmp_.resize(n * sizeof(float) + 16);
     lp_->run(in, static_cast<long long>(stride), static_cast<long long>(n), tmp_.as<void>(), static_cast<long long>(n),
-             static_cast<long long>(k0_), s);
+             static_cast<long long>(k0_), dev_err(), s);
     dc_->run(tmp_.as<void>(), static_cast<long long>(n), static_cast<long long>(n), out,
-             static_cast<long long>(out_stride), static_cast<long long>(k0_), s);
+             static_cast<long long>(out_stride), static_cast<long long>(k0_), dev_err(), s);
   }
   void reset_state() override {
     lp_->set_carry(carry_zero());
@@ -272,8 +284,64 @@ class AmBlock final : public ScanBlock {
 
  private:
   LpDcCoeffs d_;
-  bool abs_ = false;
+  bool abs_ = false, three_ = false;
   std::unique_ptr<ScanStage> lp_, dc_, lpdc_, sq_;
+  DevBuf tmp_;
+};
+
+// dsp/iir.rs:86-187 LpDcCascade as an f32 block: process (LP4 -> DC blocker) or, with
+// the sqrt map, process_mapped(x, f32::sqrt) (LP4 -> sqrt -> DC, the AM-PowerSqrt use).
+// One pass (k_lpdc_sp<RealLp / RealLpSqrt>) when the LP4 forgets within the warm-up;
+// otherwise the three-kernel LpDc scan, or (sqrt map) an LP4 scan and a DC scan.
+class LpDcBlock final : public ScanBlock {
+ public:
+  LpDcBlock(float fs, float lp_fc, float dc_cut) : ScanBlock("LpDcCascade", Dt::F32, 1) {
+    d_ = lpdc_design(fs, lp_fc, dc_cut);  // iir.rs:111-137
+    ScanCoef c = coef_lp(d_.bq);
+    c.r = d_.r;
+    sp_ = std::make_unique<ScanStage>(RecK::LPDC, Pre::RealLp, Post::Id, lpdc_ss(d_), c, 1);
+    sq_ = std::make_unique<ScanStage>(RecK::LPDC, Pre::RealLpSqrt, Post::Id, lpdc_ss(d_), c, 1);
+    full_ = std::make_unique<ScanStage>(RecK::LPDC, Pre::Real, Post::Id, lpdc_ss(d_), c, 1);
+    lp_ = std::make_unique<ScanStage>(RecK::LP4, Pre::Real, Post::Sqrt, lp_cascade_ss(d_.bq), c, 1);
+    dc_ = std::make_unique<ScanStage>(RecK::DC, Pre::Real, Post::Id, dc_ss(d_.r), c, 1);
+    reset_state();
+  }
+  // process_mapped with f32::sqrt (iir.rs:170-186) from now on: before the first call.
+  void set_sqrt(bool on) { sqrt_ = on; }
+  int configure(int option, long long value) override {
+    if (option != kOptScanPath) return -4;
+    if (value != 0 && value != 1) return -3;
+    three_ = value == 1;
+    for (auto* st : {lp_.get(), dc_.get(), full_.get()}) st->set_mode(static_cast<int>(value));
+    return 0;
+  }
+  std::vector<float> taps(int) const override { return {d_.bq.b0, d_.bq.b1, d_.bq.b2, d_.bq.a1, d_.bq.a2, d_.r}; }
+
+ protected:
+  void run(const void* in, size_t stride, size_t n, void* out, size_t out_stride, hipStream_t s) override {
+    const long long st = static_cast<long long>(stride), nn = static_cast<long long>(n),
+                    os = static_cast<long long>(out_stride), k0 = static_cast<long long>(k0_);
+    if (!sqrt_) {
+      if (sp_->lpdc_single_pass() && !three_) sp_->run(in, st, nn, out, os, k0, dev_err(), s);
+      else full_->run(in, st, nn, out, os, k0, dev_err(), s);
+      return;
+    }
+    if (sq_->lpdc_single_pass() && !three_) {
+      sq_->run(in, st, nn, out, os, k0, dev_err(), s);
+      return;
+    }
+    tmp_.resize(n * sizeof(float) + 16);
+    lp_->run(in, st, nn, tmp_.as<void>(), nn, k0, dev_err(), s);
+    dc_->run(tmp_.as<void>(), nn, nn, out, os, k0, dev_err(), s);
+  }
+  void reset_state() override {
+    for (auto* st : {sp_.get(), sq_.get(), full_.get(), lp_.get(), dc_.get()}) st->set_carry(carry_zero());
+  }
+
+ private:
+  LpDcCoeffs d_;
+  bool sqrt_ = false, three_ = false;
+  std::unique_ptr<ScanStage> sp_, sq_, full_, lp_, dc_;
   DevBuf tmp_;
 };
 
@@ -315,7 +383,7 @@ class SsbModBlock final : public Block {
       u_.resize(2 * n * sizeof(float));
       v_.resize(2 * n * sizeof(float));
       launch_ssb_mod_front(static_cast<const float*>(in), u_.as<float>(), nn, k_, aud_.step_q64, s);
-      st_->run(u_.as<void>(), nn, nn, v_.as<void>(), nn, static_cast<long long>(k_), s);
+      st_->run(u_.as<void>(), nn, nn, v_.as<void>(), nn, static_cast<long long>(k_), dev_err(), s);
       launch_ssb_mod_back(v_.as<float>(), static_cast<f2*>(out), nn, k_, rf_.step_q64, side_, s);
     }
     k_ += n;
@@ -327,8 +395,12 @@ class SsbModBlock final : public Block {
     reset_sp();
     ORION_HIP(hipDeviceSynchronize());
   }
-  // 0 auto (single pass where valid), 1 the three-pass form (tests)
-  void set_mode(int m) { mode_ = m; }
+  int configure(int option, long long value) override {  // single pass where valid, or the three passes
+    if (option != kOptModPasses) return -4;
+    if (value != 0 && value != 1 && value != 3) return -3;
+    mode_ = value == 3 ? 1 : 0;
+    return 0;
+  }
   std::vector<float> taps(int) const override { return {b_.b0, b_.b1, b_.b2, b_.a1, b_.a2}; }
 
  private:
@@ -360,6 +432,25 @@ std::unique_ptr<Block> make_lp_cascade(float fs, float fc) {
   auto blk = std::make_unique<OneStageBlock>("LpCascade", Dt::F32, 1, std::move(st), carry_zero());
   blk->coef_ = {b.b0, b.b1, b.b2, b.a1, b.a2};
   return blk;
+}
+
+std::unique_ptr<Block> make_biquad(float b0, float b1, float b2, float a1, float a2) {
+  const BiquadCoeffs b{b0, b1, b2, a1, a2};  // iir.rs:17-27
+  auto st = std::make_unique<ScanStage>(RecK::BQ, Pre::Real, Post::Id, biquad_ss(b), coef_lp(b), 1);
+  auto blk = std::make_unique<OneStageBlock>("Biquad", Dt::F32, 1, std::move(st), carry_zero());
+  blk->coef_ = {b0, b1, b2, a1, a2};
+  return blk;
+}
+
+std::unique_ptr<Block> make_lp_dc_cascade(float fs, float lp_fc, float dc_cut_hz) {
+  return std::make_unique<LpDcBlock>(fs, lp_fc, dc_cut_hz);
+}
+
+int lp_dc_cascade_set_sqrt(Block* b, bool on) {
+  auto* l = dynamic_cast<LpDcBlock*>(b);
+  if (!l) return -4;
+  l->set_sqrt(on);
+  return 0;
 }
 
 std::unique_ptr<Block> make_dc_blocker(float fs, float cut_hz) {

@@ -6,9 +6,12 @@
 
 namespace orion {
 
-std::unique_ptr<Block> make_lp_cascade(float fs, float fc);
+std::unique_ptr<Block> make_lp_cascade(float fs, float fc);                  // dsp/iir.rs:49-83
+std::unique_ptr<Block> make_biquad(float b0, float b1, float b2, float a1, float a2);  // dsp/iir.rs:15-41
+std::unique_ptr<Block> make_lp_dc_cascade(float fs, float lp_fc, float dc_cut_hz);     // dsp/iir.rs:86-187
+int lp_dc_cascade_set_sqrt(Block* b, bool on);  // process_mapped(x, f32::sqrt), iir.rs:170-186; -4 other blocks
 // modulate/ssb.rs:9-114 (SsbPhasingMod::new(fs, audio_bw, audio_if, rf, usb)). F32 -> C32.
-std::unique_ptr<Block> make_ssb_mod(float fs, float audio_bw, float audio_if_hz, float rf_hz, bool usb);                  // dsp/iir.rs:49-83
+std::unique_ptr<Block> make_ssb_mod(float fs, float audio_bw, float audio_if_hz, float rf_hz, bool usb);
 std::unique_ptr<Block> make_dc_blocker(float fs, float cut_hz);              // dsp/dc.rs:8-59
 std::unique_ptr<Block> make_fm_demod(float fs, float dev_hz, float audio_bw);  // demodulate/fm.rs
 int fm_demod_with_translate(Block* b, float freq_hz);                        // fm.rs:34-37

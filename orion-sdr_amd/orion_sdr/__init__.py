@@ -101,6 +101,9 @@ def _load():
         "orion_block_process": (i, [vp, vp, sz, vp, sz, C.POINTER(WorkReport)]),
         "orion_block_process_device": (i, [vp, vp, sz, vp, sz, vp, C.POINTER(WorkReport)]),
         "orion_block_reset": (i, [vp]), "orion_block_free": (None, [vp]),
+        "orion_block_configure": (i, [vp, i, C.c_longlong]),
+        "orion_block_status": (i, [vp]),
+        "orion_debug_set_spin_limit": (None, [C.c_uint32]), "orion_debug_spin_limit": (C.c_uint32, []),
         "orion_block_in_type": (i, [vp]), "orion_block_out_type": (i, [vp]),
         "orion_block_out_len": (sz, [vp, sz]), "orion_block_channels": (sz, [vp]),
         "orion_block_name": (C.c_char_p, [vp]),
@@ -238,6 +241,21 @@ class _Block:
 
     def taps(self, which: int = 0) -> np.ndarray:
         return _taps_of(self._h, which)
+
+    _OPTS = {"scan_path": 1, "mod_passes": 2}
+
+    def configure_option(self, option: str, value: int):
+        """Engine options (no reference counterpart; include/orion_sdr_amd.h
+        orion_block_configure): scan_path 0/1 (single pass / three-kernel scan),
+        mod_passes 0/3."""
+        _check(_L.orion_block_configure(self._h, self._OPTS[option], int(value)))
+        return self
+
+    def status(self):
+        """Raise OrionError if a kernel of this handle flagged a device-side failure
+        (a cross-workgroup wait that timed out) since the last check (non-blocking;
+        include/orion_sdr_amd.h orion_block_status)."""
+        _check(_L.orion_block_status(self._h))
 
 
 # ---- DSP primitives (src/dsp) -------------------------------------------------
@@ -426,8 +444,7 @@ class WbfmChain(_Block):
         super().__init__(h)
         self.m = int(m)
 
-    _PATHS = {"auto": 0, "segmented": 1, "ranges": 2, "split": 3, "segmented_v1": 4, "specialized": 5,
-              "segmented3": 6, "segmented4": 7}
+    _PATHS = {"auto": 0, "segmented": 1, "split": 3}
 
     def configure(self, path: str = "auto", max_segments: int = 0):
         """Engine tuning / tests (no reference counterpart): the kernel path and a
@@ -580,6 +597,16 @@ def diag_stream_read(x, stream: int = 0) -> int:
     nb = _L.orion_diag_stream_read_bytes(x.numel() * x.element_size())
     _check(_L.orion_diag_stream_read(C.c_void_p(x.data_ptr()), nb, C.c_void_p(stream)))
     return int(nb)
+
+
+def set_spin_limit(polls: int):
+    """Test-only: polls a cross-workgroup wait makes before it times out (process-wide;
+    0 makes every such wait time out at once). include/orion_sdr_amd.h."""
+    _L.orion_debug_set_spin_limit(int(polls))
+
+
+def spin_limit() -> int:
+    return int(_L.orion_debug_spin_limit())
 
 
 def device_count() -> int:

@@ -228,11 +228,7 @@ def test_single_pass_scan_geometry(gpu_lib, oracle):
         # streamed: also no worse than the three-kernel scan on the same calls (both carry
         # the f32 state across calls, where the f32 rounding of the carried state differs
         # from the reference's by its own sensitivity)
-        os.environ["ORION_SCAN_3K"] = "1"
-        try:
-            e3 = nrmse(stream(mk(), x, 10007), ref)
-        finally:
-            del os.environ["ORION_SCAN_3K"]
+        e3 = nrmse(stream(mk().configure_option("scan_path", 1), x, 10007), ref)
         report(f"{name} three-kernel streamed 10007 nrmse", e3, max(t, e3))
         report(f"{name} single-pass streamed 10007 nrmse", nrmse(stream(mk(), x, 10007), ref), max(t, 1.25 * e3))
 
@@ -342,28 +338,11 @@ def test_wbfm_full_size_windowed(gpu_lib, oracle):
     ("segmented", 1, 600_000),      # one segment, ragged last sub-range
     ("segmented", 7, 4097 * 8 + 5),  # one sub-range per segment, 2-output last segment
     ("segmented", 2, 8 * 1024 + 8),  # second segment of one output
-    ("segmented_v1", 3, 1 << 20),
-    ("specialized", 3, 1 << 20),
-    ("specialized", 1, 600_000),
-    ("specialized", 7, 4097 * 8 + 5),
-    ("specialized", 2, 8 * 1024 + 8),
-    ("specialized", 6, 1 << 16),     # 6 segments in two workgroups, the second part-filled
-    ("specialized", 0, 1 << 20),     # the resident capacity: one sub-range per segment
-    ("segmented3", 3, 1 << 20),
-    ("segmented3", 1, 600_000),
-    ("segmented3", 7, 4097 * 8 + 5),
-    ("segmented3", 2, 8 * 1024 + 8),
-    ("segmented3", 0, 1 << 20),     # the resident capacity: one sub-range per segment
-    ("segmented4", 3, 1 << 20),
-    ("segmented4", 1, 600_000),
-    ("segmented4", 7, 4097 * 8 + 5),
-    ("segmented4", 2, 8 * 1024 + 8),
-    ("segmented4", 0, 1 << 20),     # the resident capacity: one sub-range per segment
-    ("segmented4", 0, 100),         # tiny input: clamped loads, boundary fixups
-    ("segmented_v1", 1, 600_000),
-    ("segmented_v1", 7, 4097 * 8 + 5),
-    ("ranges", 0, 1 << 20),
-    ("split", 0, 1 << 20)])
+    ("segmented", 16, 1 << 20),     # 16 segments: two XCD runs per XCD boundary map
+    ("segmented", 0, 1 << 20),      # the resident capacity: one sub-range per segment
+    ("segmented", 0, 100),          # tiny input: clamped loads, boundary fixups
+    ("split", 0, 1 << 20),
+    ("split", 0, 600_000)])
 def test_wbfm_kernel_paths(gpu_lib, oracle, path, max_seg, n):
     """Every WBFM kernel path and segment geometry against the oracle."""
     x = wbfm_input(n)
@@ -371,9 +350,7 @@ def test_wbfm_kernel_paths(gpu_lib, oracle, path, max_seg, n):
     report(f"wbfm path={path} max_segments={max_seg} n={n} nrmse", nrmse(got, oracle.wbfm(x)), 1e-5)
 
 
-@pytest.mark.parametrize("path,max_seg", [("segmented", 2), ("segmented", 5), ("specialized", 2), ("specialized", 5),
-                                          ("segmented3", 2), ("segmented3", 5), ("segmented4", 2),
-                                          ("segmented4", 5), ("segmented_v1", 2), ("segmented_v1", 5)])
+@pytest.mark.parametrize("path,max_seg", [("segmented", 2), ("segmented", 5), ("segmented", 8), ("split", 0)])
 def test_wbfm_segmented_streaming_and_channels(gpu_lib, oracle, path, max_seg):
     """Carried state across calls and independent channels with several
     multi-sub-range segments per channel."""
@@ -408,8 +385,61 @@ def test_wbfm_stream_shards(gpu_lib, oracle, world):
 def test_wbfm_configure_errors(gpu_lib):
     with pytest.raises(gpu_lib.OrionError):
         gpu_lib.WbfmChain().configure("segmented", -1)
+    W = gpu_lib.WbfmChain()
+    assert gpu_lib._L.orion_wbfm_chain_configure(W._h, 2, 0) == -3  # ORION_E_ARG: no such path
     fm = gpu_lib.FmQuadratureDemod(48e3, 2500, 5000)
     assert gpu_lib._L.orion_wbfm_chain_configure(fm._h, 0, 0) == -4  # ORION_E_TYPE: not a WBFM chain
+    assert gpu_lib._L.orion_block_configure(W._h, 1, 0) == -4       # no scan_path option on the chain
+    assert gpu_lib._L.orion_block_configure(fm._h, 1, 7) == -3      # bad value
+
+
+def test_device_wait_timeouts_are_reported(gpu_lib, oracle):
+    """Every kernel that waits on another workgroup bounds the wait and flags a
+    timeout in the handle's host-visible error word (include/orion_sdr_amd.h
+    orion_block_status): with the test-only spin limit at 0 every such wait times out
+    at once, and the call must be reported as failed, never returned as valid output
+    (core.rs:12-22: a block does not silently corrupt). Host path: the call itself
+    raises. Device path: orion_block_status after a sync, or the next call, raises."""
+    import torch
+
+    default = gpu_lib.spin_limit()
+    assert default > 0
+    x = wbfm_input(1 << 18)
+    a = real_tone(FS, 1000.0, 1 << 17, 0.5)
+    iq = oracle.fm_mod(a, FS, 2500.0)
+    xr = RNG.standard_normal(1 << 17).astype(np.float32)
+    ssb = oracle.ssb_mod(a, FS, 2800.0, 1500.0)
+    makers = [("WBFM segmented", lambda: gpu_lib.WbfmChain().configure("segmented", 8), x),
+              ("LpCascade (k_scan_sp)", lambda: gpu_lib.LpCascade(1.25e6, 13.5e3), xr),
+              ("FmQuadratureDemod (k_scan_sp)", lambda: gpu_lib.FmQuadratureDemod(FS, 2500.0, 5000.0), iq),
+              ("SsbProductDemod (k_lpdc_sp)", lambda: gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0), ssb),
+              ("DcBlocker (k_lpdc_sp)", lambda: gpu_lib.DcBlocker(FS, 2.0), xr),
+              ("FmPhaseAccumMod (k_fm_mod_sp)", lambda: gpu_lib.FmPhaseAccumMod(FS, 2500.0), a)]
+    try:
+        for name, mk, inp in makers:
+            gpu_lib.set_spin_limit(0)
+            with pytest.raises(gpu_lib.OrionError, match="timed out"):
+                mk().process(inp)
+            blk = mk()
+            xd = torch.from_numpy(inp).cuda()
+            blk.process_device(xd)
+            torch.cuda.synchronize()
+            with pytest.raises(gpu_lib.OrionError, match="timed out"):
+                blk.status()
+            blk.status()  # reported once, then clear
+            blk.process_device(xd)  # flags again ...
+            torch.cuda.synchronize()
+            with pytest.raises(gpu_lib.OrionError, match="timed out"):
+                blk.process_device(xd)  # ... and the next call fails on it
+            gpu_lib.set_spin_limit(default)
+            torch.cuda.synchronize()
+            blk2 = mk()
+            blk2.process_device(xd)
+            torch.cuda.synchronize()
+            blk2.status()  # a normal run flags nothing
+            print(f"[parity] {name}: timeout reported on the host and device paths")
+    finally:
+        gpu_lib.set_spin_limit(default)
 
 
 # ---- device-resident path (orion_block_process_device) ---------------------------------
@@ -423,7 +453,7 @@ def test_device_path_alignment_and_capacity(gpu_lib, oracle):
     x = wbfm_input(n + 1)
     xd = torch.from_numpy(x).cuda()
     ref = oracle.wbfm(x[1:])
-    for path in ("segmented", "ranges", "split"):
+    for path in ("segmented", "split"):
         W = gpu_lib.WbfmChain().configure(path)
         got = torch.cat([W.process_device(xd[1 + i: 1 + i + 100_000]) for i in range(0, n, 100_000)])
         report(f"wbfm device path={path} unaligned chained nrmse", nrmse(got.cpu().numpy(), ref), 1e-5)

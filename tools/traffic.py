@@ -10,9 +10,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CFG = {  # samples per launch, input bytes, algorithmic bytes per sample, kernel name fragment
-    "c2": (1 << 26, 8 * (1 << 26), 8.5, "k_wbfm_seg4"),
+    "c2": (1 << 26, 8 * (1 << 26), 8.5, "k_wbfm_seg"),
     "c3": (256 << 20, 8 * (256 << 20), 9.0, "k_decim_w4"),
-    "c4": (8 << 24, 8 * (8 << 24), 8.5, "k_wbfm_seg4"),
+    "c4": (8 << 24, 8 * (8 << 24), 8.5, "k_wbfm_seg"),
     "c5": (128 << 20, 8 * (128 << 20), 12.0, "k_lpdc_sp"),
 }
 

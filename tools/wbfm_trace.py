@@ -1,9 +1,9 @@
-"""Debug: phase timestamps of k_wbfm_seg2 / k_wbfm_seg (ORION_WBFM_TRACE) on the C2 workload.
-Points per wave (s_memrealtime, 100 MHz): 0 start, 1 sub-range loop done,
-2 successor's phi received, 3 end; 3 + s: sub-range s's tiles done, 6 + s: its
-IIR done (s = 1..3).
-IIR done = the whole back (IIR + audio FIR) in k_wbfm_seg.
-  python tools/seg2_trace.py [out.bin] [segmented|segmented_v1]"""
+"""Debug: phase timestamps of k_wbfm_seg (the debug-only ORION_WBFM_TRACE dump) on
+the C2 workload. Points per wave (s_memrealtime, 100 MHz): 0 start, 1 sub-range loop
+done, 2 predecessor's record received, 3 end; 3 + s: sub-range s's tiles done,
+6 + s: its back done (s = 1..3); 10, 11, 12: sub-range 1's zero-state pass + scan,
+states + pass 2, audio FIR done.
+  python tools/wbfm_trace.py [out.bin]"""
 import os
 import sys
 
@@ -12,7 +12,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "orion-sdr_amd"))
-path = sys.argv[1] if len(sys.argv) > 1 else "/tmp/seg2_trace.bin"
+path = sys.argv[1] if len(sys.argv) > 1 else "/tmp/wbfm_trace.bin"
 os.environ["ORION_WBFM_TRACE"] = path
 import orion_sdr  # noqa: E402
 
@@ -20,7 +20,7 @@ dev = torch.device("cuda", 0)
 n = 1 << 26
 x = torch.randn(n, dtype=torch.complex64, device=dev)
 out = torch.empty(n // 8, dtype=torch.float32, device=dev)
-blk = orion_sdr.WbfmChain().configure(sys.argv[2] if len(sys.argv) > 2 else "segmented", 0)
+blk = orion_sdr.WbfmChain().configure("segmented", 0)
 for _ in range(5):  # the last launch's trace is kept
     blk.process_device(x, out, torch.cuda.current_stream(dev).cuda_stream)
 torch.cuda.synchronize()
@@ -40,7 +40,7 @@ ph = {
     "tail (IIR + 2 FIR)": us[:, 3] - us[:, 2],
     "whole": us[:, 3] - us[:, 0],
 }
-if (t[:, 10] > 0).all():  # k_wbfm_seg4: sub-range 1's back split
+if (t[:, 10] > 0).all():  # sub-range 1's back split
     ph["  sub1 zero-state+scan"] = us[:, 10] - us[:, 4]
     ph["  sub1 states+pass2"] = us[:, 11] - us[:, 10]
     ph["  sub1 audio FIR"] = us[:, 12] - us[:, 11]
@@ -68,7 +68,7 @@ print("end p50 by XCD (blockIdx % 8):", " ".join(f"{np.median(end[rr % 8 == x]):
 print("slow waves per XCD:", " ".join(str(int(slow[rr % 8 == x].sum())) for x in range(8)))
 print("slow waves' start p50 / all:", f"{np.median(us[slow, 0]):.2f} / {np.median(us[:, 0]):.2f}")
 raw = np.fromfile(path, dtype=np.int64).reshape(-1, 16)
-if (raw[:, 14] > 0).any():  # k_wbfm_seg4 geometry
+if (raw[:, 14] > 0).any():  # segment geometry
     Lr = raw[r, 14]
     print("segment lengths: min/p50/max", Lr.min(), int(np.median(Lr)), Lr.max(),
           " by XCD (mean):", " ".join(f"{Lr[rr % 8 == x].mean():.0f}" for x in range(8)))
