@@ -252,6 +252,26 @@ float orion_kaiser_transition_norm(size_t num_taps, float stopband_db);         
 size_t orion_kaiser_num_taps(float transition_norm, float stopband_db);                           /* fir.rs:154-157 */
 void orion_lp_cascade_design(float fs, float fc, float out5[5]);                                  /* iir.rs:49-71 */
 
+/* ---- multicarrier/tx_lowpass.rs:88-195 TxLowpass (the TX mask) ----
+ * The spec and its host-side sizing helpers (the reference's f32 arithmetic); the
+ * filter itself is FirLowpassIq::design(num_taps, cutoff_norm, stopband_db), applied
+ * by filter_aligned (TxLowpass::apply = orion_tx_lowpass_filter +
+ * orion_fir_lowpass_iq_filter_aligned[_device]). */
+typedef struct {
+  float cutoff_norm;
+  size_t num_taps;
+  float stopband_db;
+} orion_tx_lowpass;
+orion_tx_lowpass orion_tx_lowpass_for_null_band(size_t n_fft, size_t occupied_half, size_t num_taps,
+                                                float stopband_db);                              /* :118-134 */
+size_t orion_tx_lowpass_taps_for_null_band(size_t n_fft, size_t occupied_half, float stopband_db); /* :141-144 */
+size_t orion_tx_lowpass_group_delay(const orion_tx_lowpass* t);                                  /* :148-150 */
+float orion_tx_lowpass_transition_norm(const orion_tx_lowpass* t);                               /* :154-156 */
+int orion_tx_lowpass_transition_fits(const orion_tx_lowpass* t, size_t n_fft, size_t occupied_half); /* :162-165 */
+float orion_tx_lowpass_stopband_edge_norm(const orion_tx_lowpass* t);                            /* :171-173 */
+int orion_tx_lowpass_fits_guard(const orion_tx_lowpass* t, size_t cp_len, size_t roll_off, size_t backoff); /* :179-182 */
+orion_block* orion_tx_lowpass_filter(const orion_tx_lowpass* t);                                 /* :185-187 */
+
 #ifdef __cplusplus
 }
 #endif

@@ -420,6 +420,31 @@ float orion_kaiser_transition_norm(size_t num_taps, float stopband_db) {
 size_t orion_kaiser_num_taps(float transition_norm, float stopband_db) {
   return orion::kaiser_num_taps(transition_norm, stopband_db);
 }
+static orion::TxLowpassSpec tx_spec(const orion_tx_lowpass* t) { return {t->cutoff_norm, t->num_taps, t->stopband_db}; }
+orion_tx_lowpass orion_tx_lowpass_for_null_band(size_t n_fft, size_t occupied_half, size_t num_taps, float stopband_db) {
+  const auto s = orion::tx_lowpass_for_null_band(n_fft, occupied_half, num_taps, stopband_db);
+  return {s.cutoff_norm, s.num_taps, s.stopband_db};
+}
+size_t orion_tx_lowpass_taps_for_null_band(size_t n_fft, size_t occupied_half, float stopband_db) {
+  return orion::tx_lowpass_taps_for_null_band(n_fft, occupied_half, stopband_db);
+}
+size_t orion_tx_lowpass_group_delay(const orion_tx_lowpass* t) { return t ? orion::tx_lowpass_group_delay(tx_spec(t)) : 0; }
+float orion_tx_lowpass_transition_norm(const orion_tx_lowpass* t) {
+  return t ? orion::tx_lowpass_transition_norm(tx_spec(t)) : 0.0f;
+}
+int orion_tx_lowpass_transition_fits(const orion_tx_lowpass* t, size_t n_fft, size_t occupied_half) {
+  return t && orion::tx_lowpass_transition_fits(tx_spec(t), n_fft, occupied_half) ? 1 : 0;
+}
+float orion_tx_lowpass_stopband_edge_norm(const orion_tx_lowpass* t) {
+  return t ? orion::tx_lowpass_stopband_edge_norm(tx_spec(t)) : 0.0f;
+}
+int orion_tx_lowpass_fits_guard(const orion_tx_lowpass* t, size_t cp_len, size_t roll_off, size_t backoff) {
+  return t && orion::tx_lowpass_fits_guard(tx_spec(t), cp_len, roll_off, backoff) ? 1 : 0;
+}
+orion_block* orion_tx_lowpass_filter(const orion_tx_lowpass* t) {
+  if (!t) { g_err = "null spec"; return nullptr; }
+  return make([&] { return orion::make_fir_lowpass_iq(orion::kaiser_lowpass_taps(t->num_taps, t->cutoff_norm, t->stopband_db)); });
+}
 void orion_lp_cascade_design(float fs, float fc, float out5[5]) {
   const auto c = orion::lp_cascade_design(fs, fc);
   out5[0] = c.b0; out5[1] = c.b1; out5[2] = c.b2; out5[3] = c.a1; out5[4] = c.a2;

@@ -1,6 +1,8 @@
 // design.cpp — built with -ffp-contract=off (see design.hpp). Host only.
 #include "design.hpp"
 
+#include <algorithm>
+
 #include <cfloat>
 #include <cmath>
 
@@ -242,6 +244,31 @@ std::vector<double> mat_pow(const std::vector<double>& A, int S, uint64_t k) {
     k >>= 1;
   }
   return R;
+}
+
+// ---- multicarrier/tx_lowpass.rs:96-185 TxLowpass (host-side sizing helpers) ----
+TxLowpassSpec tx_lowpass_for_null_band(size_t n_fft, size_t occupied_half, size_t num_taps, float stopband_db) {
+  const float occupied_norm = static_cast<float>(occupied_half) / static_cast<float>(std::max<size_t>(n_fft, 1));
+  const float half_transition = 0.5f * kaiser_transition_norm(num_taps, stopband_db);
+  const float earliest = occupied_norm + half_transition;  // tx_lowpass.rs:125-128
+  const float latest = 0.5f - half_transition;
+  const float cutoff = earliest <= latest ? earliest : 0.5f * (occupied_norm + 0.5f);
+  return {cutoff, num_taps, stopband_db};
+}
+size_t tx_lowpass_taps_for_null_band(size_t n_fft, size_t occupied_half, float stopband_db) {  // :141-144
+  const float occupied_norm = static_cast<float>(occupied_half) / static_cast<float>(std::max<size_t>(n_fft, 1));
+  return kaiser_num_taps(0.5f - occupied_norm, stopband_db);
+}
+size_t tx_lowpass_group_delay(const TxLowpassSpec& t) { return (std::max<size_t>(t.num_taps, 3) | 1) / 2; }  // :148-150
+float tx_lowpass_transition_norm(const TxLowpassSpec& t) { return kaiser_transition_norm(t.num_taps, t.stopband_db); }
+bool tx_lowpass_transition_fits(const TxLowpassSpec& t, size_t n_fft, size_t occupied_half) {  // :162-165
+  const float occupied_norm = static_cast<float>(occupied_half) / static_cast<float>(std::max<size_t>(n_fft, 1));
+  return tx_lowpass_transition_norm(t) <= 0.5f - occupied_norm;
+}
+float tx_lowpass_stopband_edge_norm(const TxLowpassSpec& t) { return t.cutoff_norm + 0.5f * tx_lowpass_transition_norm(t); }
+bool tx_lowpass_fits_guard(const TxLowpassSpec& t, size_t cp_len, size_t roll_off, size_t backoff) {  // :179-182
+  const size_t slack = std::min(cp_len > backoff ? cp_len - backoff : 0, backoff);
+  return roll_off + tx_lowpass_group_delay(t) <= slack;
 }
 
 }  // namespace orion

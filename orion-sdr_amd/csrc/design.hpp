@@ -45,6 +45,17 @@ Oscillator oscillator(float freq_hz, float fs);
 // Phasor e^{j*theta*k} for k = 0..n-1, computed in f64 and rounded to f32 pairs.
 std::vector<float> phasor_table(double theta, size_t n);
 
+// multicarrier/tx_lowpass.rs:88-185 TxLowpass: the spec and its sizing helpers (f32
+// arithmetic as the reference). filter() is FirLowpassIq::design(num_taps, cutoff, stopband).
+struct TxLowpassSpec { float cutoff_norm; size_t num_taps; float stopband_db; };
+TxLowpassSpec tx_lowpass_for_null_band(size_t n_fft, size_t occupied_half, size_t num_taps, float stopband_db);
+size_t tx_lowpass_taps_for_null_band(size_t n_fft, size_t occupied_half, float stopband_db);
+size_t tx_lowpass_group_delay(const TxLowpassSpec& t);
+float tx_lowpass_transition_norm(const TxLowpassSpec& t);
+bool tx_lowpass_transition_fits(const TxLowpassSpec& t, size_t n_fft, size_t occupied_half);
+float tx_lowpass_stopband_edge_norm(const TxLowpassSpec& t);
+bool tx_lowpass_fits_guard(const TxLowpassSpec& t, size_t cp_len, size_t roll_off, size_t backoff);
+
 // ---- linear state-space form of the IIR recurrences (for chunked scans) ----
 // A recurrence s' = A s + B x, y = C s + D x with S states. We derive A, B, C, D
 // numerically (f64) from the reference per-sample update so that they match it

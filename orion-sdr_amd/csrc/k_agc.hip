@@ -79,7 +79,7 @@ struct CwPol {
   using Out = float2;
   float att, rel, oma, omr, gain;
   uint64_t k0, step;  // sample i of the call: the phasor after k0 + i + 1 steps
-  __device__ __forceinline__ float drive(In v) const { return fminf(fmaxf(v, 0.0f), 1.0f); }  // f32::clamp(0, 1)
+  __device__ __forceinline__ float drive(In v) const { return v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v); }  // f32::clamp
   __device__ __forceinline__ bool up(float d, float env) const { return d >= env; }
   __device__ __forceinline__ float seed(float env, float) const { return env; }
   __device__ __forceinline__ float warm_seed(float d) const { return d; }

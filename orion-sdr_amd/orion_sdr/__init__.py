@@ -24,7 +24,7 @@ import os
 import numpy as np
 
 __all__ = [
-    "Rotator", "FirDecimator", "FirLowpass", "FirLowpassIq", "LpCascade", "DcBlocker",
+    "Rotator", "Nco", "Biquad", "LpDcCascade", "PmDirectPhaseMod", "CwKeyedMod", "TxLowpass", "FirDecimator", "FirLowpass", "FirLowpassIq", "LpCascade", "DcBlocker",
     "FmQuadratureDemod", "PmQuadratureDemod", "SsbProductDemod", "AmEnvelopeDemod",
     "CwEnvelopeDemod", "WbfmChain", "AgcRms", "AgcRmsIq", "AmDsbMod", "FmPhaseAccumMod", "SsbPhasingMod",
     "fir_lowpass_design", "kaiser_lowpass_taps",
@@ -49,6 +49,10 @@ class WorkReport(C.Structure):
     _fields_ = [("in_read", C.c_size_t), ("out_written", C.c_size_t)]
 
 
+class TxLowpassSpec(C.Structure):
+    _fields_ = [("cutoff_norm", C.c_float), ("num_taps", C.c_size_t), ("stopband_db", C.c_float)]
+
+
 class WbfmParams(C.Structure):
     _fields_ = [("fs", C.c_float), ("f_off", C.c_float), ("dec_cutoff", C.c_float),
                 ("dec_trans", C.c_float), ("dev_hz", C.c_float), ("audio_bw", C.c_float),
@@ -67,6 +71,24 @@ def _load():
         "orion_version": (C.c_char_p, []), "orion_last_error": (C.c_char_p, []),
         "orion_device_count": (i, []), "orion_set_device": (i, [i]), "orion_synchronize": (i, [vp]),
         "orion_rotator_new": (vp, [f, f]),
+        "orion_rotator_set_freq": (i, [vp, f, f]), "orion_rotator_reset_phase": (i, [vp]),
+        "orion_rotator_mix_usb_block": (i, [vp, vp, sz, vp, sz, C.POINTER(WorkReport)]),
+        "orion_rotator_mix_usb_block_device": (i, [vp, vp, sz, vp, sz, vp, C.POINTER(WorkReport)]),
+        "orion_nco_new": (vp, [f, f]), "orion_nco_set_freq": (i, [vp, f]),
+        "orion_nco_next_cs_block": (i, [vp, vp, sz]), "orion_nco_next_cs_block_device": (i, [vp, vp, sz, vp]),
+        "orion_biquad_new": (vp, [f, f, f, f, f]),
+        "orion_lp_dc_cascade_new": (vp, [f, f, f]), "orion_lp_dc_cascade_set_sqrt_map": (i, [vp, i]),
+        "orion_pm_direct_phase_mod_new": (vp, [f, f, f]), "orion_pm_direct_phase_mod_set_gain": (i, [vp, f]),
+        "orion_pm_direct_phase_mod_set_sensitivity": (i, [vp, f]),
+        "orion_cw_keyed_mod_new": (vp, [f, f, f, f]), "orion_cw_keyed_mod_set_gain": (i, [vp, f]),
+        "orion_tx_lowpass_for_null_band": (TxLowpassSpec, [sz, sz, sz, f]),
+        "orion_tx_lowpass_taps_for_null_band": (sz, [sz, sz, f]),
+        "orion_tx_lowpass_group_delay": (sz, [C.POINTER(TxLowpassSpec)]),
+        "orion_tx_lowpass_transition_norm": (f, [C.POINTER(TxLowpassSpec)]),
+        "orion_tx_lowpass_transition_fits": (i, [C.POINTER(TxLowpassSpec), sz, sz]),
+        "orion_tx_lowpass_stopband_edge_norm": (f, [C.POINTER(TxLowpassSpec)]),
+        "orion_tx_lowpass_fits_guard": (i, [C.POINTER(TxLowpassSpec), sz, sz, sz]),
+        "orion_tx_lowpass_filter": (vp, [C.POINTER(TxLowpassSpec)]),
         "orion_fir_decimator_new": (vp, [f, sz, f, f]),
         "orion_fir_decimator_batch_new": (vp, [f, sz, f, f, sz]),
         "orion_fir_lowpass_new": (vp, [f, f, f]),
@@ -260,10 +282,73 @@ class _Block:
 
 # ---- DSP primitives (src/dsp) -------------------------------------------------
 class Rotator(_Block):
-    """dsp/rotator.rs:16 Rotator::new(freq_hz, fs); process = rotate_block."""
+    """dsp/rotator.rs:16 Rotator::new(freq_hz, fs); process = rotate_block (:74-85)."""
 
     def __init__(self, freq_hz: float, fs: float):
         super().__init__(_L.orion_rotator_new(freq_hz, fs))
+
+    def set_freq(self, freq_hz: float, fs: float):
+        """rotator.rs:35-39: a new step; the phase continues (synchronizes the device)."""
+        _check(_L.orion_rotator_set_freq(self._h, freq_hz, fs))
+
+    def reset_phase(self):
+        """rotator.rs:28-31: phasor back to 1 + j0."""
+        _check(_L.orion_rotator_reset_phase(self._h))
+
+    def mix_usb_block(self, x):
+        """rotator.rs:88-94: I*cos + Q*sin on the same oscillator (complex64 -> float32).
+        A torch CUDA tensor runs on the device path (torch's current stream)."""
+        wr = WorkReport()
+        if _is_torch(x):
+            import torch
+
+            if not x.is_cuda or not x.is_contiguous() or x.dtype != torch.complex64:
+                raise ValueError("mix_usb_block needs a contiguous complex64 CUDA tensor")
+            out = torch.empty(x.shape[-1], dtype=torch.float32, device=x.device)
+            s = torch.cuda.current_stream(x.device).cuda_stream
+            _check(_L.orion_rotator_mix_usb_block_device(self._h, x.data_ptr(), x.shape[-1], out.data_ptr(),
+                                                        out.shape[0], s, C.byref(wr)))
+            return out
+        x = self._validate(x)
+        out = np.empty(x.shape[-1], np.float32)
+        _check(_L.orion_rotator_mix_usb_block(self._h, x.ctypes.data, x.shape[-1], out.ctypes.data, out.size,
+                                              C.byref(wr)))
+        return out
+
+
+class Nco(_Block):
+    """dsp/nco.rs:20 Nco::new(freq_hz, fs) as a block: process = mix_with_nco per
+    sample (nco.rs:63-66, the non-FMA product)."""
+
+    def __init__(self, freq_hz: float, fs: float):
+        super().__init__(_L.orion_nco_new(freq_hz, fs))
+
+    def set_freq(self, freq_hz: float):
+        """nco.rs:33-38 (fs from the constructor); the phase continues."""
+        _check(_L.orion_nco_set_freq(self._h, freq_hz))
+
+    def next_cs_block(self, n: int) -> np.ndarray:
+        """nco.rs:42-58 next_cs, n times: complex64 (cos, sin) of each step's phasor."""
+        out = np.empty(int(n), np.complex64)
+        _check(_L.orion_nco_next_cs_block(self._h, out.ctypes.data, out.size))
+        return out
+
+
+class Biquad(_Block):
+    """dsp/iir.rs:15-41 Biquad::new(b0, b1, b2, a1, a2) (TDF-II); reset() = Biquad::reset."""
+
+    def __init__(self, b0: float, b1: float, b2: float, a1: float, a2: float):
+        super().__init__(_L.orion_biquad_new(b0, b1, b2, a1, a2))
+
+
+class LpDcCascade(_Block):
+    """dsp/iir.rs:111 LpDcCascade::design(fs, lp_fc, dc_cut_hz); process (:151-165), or
+    with sqrt_map=True process_mapped(x, f32::sqrt) (:170-186)."""
+
+    def __init__(self, fs: float, lp_fc: float, dc_cut_hz: float, sqrt_map: bool = False):
+        super().__init__(_L.orion_lp_dc_cascade_new(fs, lp_fc, dc_cut_hz))
+        if sqrt_map:
+            _check(_L.orion_lp_dc_cascade_set_sqrt_map(self._h, 1))
 
 
 class FirDecimator(_Block):
@@ -418,6 +503,76 @@ class FmPhaseAccumMod(_Block):
 
     def set_gain(self, g: float):
         _check(_L.orion_fm_phase_accum_mod_set_gain(self._h, g))
+
+
+class PmDirectPhaseMod(_Block):
+    """modulate/pm.rs:17-47 (phase kp * x in radians; rf_hz 0 for baseband)."""
+
+    def __init__(self, sample_rate: float, kp_rad_per_unit: float, rf_hz: float = 0.0):
+        super().__init__(_L.orion_pm_direct_phase_mod_new(sample_rate, kp_rad_per_unit, rf_hz))
+
+    def set_gain(self, g: float):
+        _check(_L.orion_pm_direct_phase_mod_set_gain(self._h, g))
+
+    def set_sensitivity(self, kp_rad_per_unit: float):
+        _check(_L.orion_pm_direct_phase_mod_set_sensitivity(self._h, kp_rad_per_unit))
+
+
+class CwKeyedMod(_Block):
+    """modulate/cw.rs:21-87: keying envelope (0..1) -> keyed tone IQ."""
+
+    def __init__(self, sample_rate: float, tone_hz: float, rise_ms: float, fall_ms: float):
+        super().__init__(_L.orion_cw_keyed_mod_new(sample_rate, tone_hz, rise_ms, fall_ms))
+
+    def set_gain(self, g: float):
+        _check(_L.orion_cw_keyed_mod_set_gain(self._h, g))
+
+
+class TxLowpass:
+    """multicarrier/tx_lowpass.rs:88-195: the TX spectral-mask spec, its sizing helpers
+    (the reference's f32 arithmetic, in the library) and apply() = filter_aligned of
+    FirLowpassIq::design(num_taps, cutoff_norm, stopband_db) on the GPU."""
+
+    def __init__(self, cutoff_norm: float, num_taps: int, stopband_db: float):
+        self.cutoff_norm, self.num_taps, self.stopband_db = float(np.float32(cutoff_norm)), int(num_taps), \
+            float(np.float32(stopband_db))
+
+    def _spec(self):
+        return C.byref(TxLowpassSpec(self.cutoff_norm, self.num_taps, self.stopband_db))
+
+    @classmethod
+    def for_null_band(cls, n_fft: int, occupied_half: int, num_taps: int, stopband_db: float) -> "TxLowpass":
+        s = _L.orion_tx_lowpass_for_null_band(n_fft, occupied_half, num_taps, stopband_db)
+        return cls(s.cutoff_norm, s.num_taps, s.stopband_db)
+
+    @staticmethod
+    def taps_for_null_band(n_fft: int, occupied_half: int, stopband_db: float) -> int:
+        return int(_L.orion_tx_lowpass_taps_for_null_band(n_fft, occupied_half, stopband_db))
+
+    def group_delay(self) -> int:
+        return int(_L.orion_tx_lowpass_group_delay(self._spec()))
+
+    def transition_norm(self) -> float:
+        return float(_L.orion_tx_lowpass_transition_norm(self._spec()))
+
+    def transition_fits(self, n_fft: int, occupied_half: int) -> bool:
+        return bool(_L.orion_tx_lowpass_transition_fits(self._spec(), n_fft, occupied_half))
+
+    def stopband_edge_norm(self) -> float:
+        return float(_L.orion_tx_lowpass_stopband_edge_norm(self._spec()))
+
+    def fits_guard(self, cp_len: int, roll_off: int, backoff: int) -> bool:
+        return bool(_L.orion_tx_lowpass_fits_guard(self._spec(), cp_len, roll_off, backoff))
+
+    def filter(self) -> "FirLowpassIq":
+        return FirLowpassIq(_L.orion_tx_lowpass_filter(self._spec()))
+
+    def apply(self, stream):
+        """tx_lowpass.rs:192-195: filter_aligned across the whole stream. A numpy array
+        is returned filtered (a copy); a contiguous complex64 CUDA tensor is filtered
+        in place on the device."""
+        f = self.filter()
+        return f.filter_aligned_device(stream) if _is_torch(stream) else f.filter_aligned(stream)
 
 
 class SsbPhasingMod(_Block):

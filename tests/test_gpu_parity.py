@@ -80,6 +80,147 @@ def test_rotator_golden(gpu_lib):
     report("rotator golden max|err|/|x|", float(np.max(np.abs(got - GOLD["rotator_out"]) / (np.abs(GOLD["x_c"]) + 1e-3))), 1e-4)
 
 
+def _theta(f, fs):
+    """Exact angle of the reference's f32 step phasor (rotator.rs:17-18, nco.rs:21-22)."""
+    import np_ref as R
+
+    phi = np.float32(np.float32(R.TAU * np.float32(f)) / np.float32(fs))
+    return float(np.arctan2(np.float64(R.sinf(phi)), np.float64(R.cosf(phi))))
+
+
+def _exact_phasors(n, segments):
+    """Phasor after each of n steps of an oscillator retuned at the given sample
+    counts: segments = [(start, theta)], the phase continuing across each retune
+    (the reference keeps z and swaps w, rotator.rs:35-39 / nco.rs:33-38)."""
+    ph = np.zeros(n, np.float64)
+    acc = 0.0
+    for j, (s0, th) in enumerate(segments):
+        s1 = segments[j + 1][0] if j + 1 < len(segments) else n
+        k = np.arange(1, s1 - s0 + 1, dtype=np.float64)
+        ph[s0:s1] = acc + th * k
+        acc += th * (s1 - s0)
+    return np.exp(1j * np.mod(ph, 2 * np.pi))
+
+
+@pytest.mark.parametrize("f1,f2,fs", [(-1.5e6, 0.75e6, 10e6), (1500.0, -700.0, 48e3)])
+def test_rotator_set_freq_reset_phase_mix_usb(gpu_lib, oracle, f1, f2, fs):
+    """rotator.rs:35-39 set_freq mid-stream (w changes, the phase continues),
+    :28-31 reset_phase, :88-94 mix_usb_block on the same oscillator. The GPU phasor
+    is the exact one of the reference's f32 steps: <= 1e-6 from the exact rotation;
+    the oracle (the reference's f32 recurrence) within its own drift + 1e-6."""
+    n, ns = 1 << 18, 100_003
+    x = (complex_tone(fs, 0.0731 * fs, n) * np.complex64(0.8 - 0.3j)).astype(np.complex64)
+    ex = x.astype(np.complex128) * _exact_phasors(n, [(0, _theta(f1, fs)), (ns, _theta(f2, fs))])
+    R = gpu_lib.Rotator(f1, fs)
+    got = np.concatenate([R.process(x[:ns]), (R.set_freq(f2, fs), R.process(x[ns:]))[1]])
+    ref = oracle.rotator_retune(x, f1, fs, ns, f2)
+    report(f"rotator set_freq {f1}->{f2} GPU vs exact max|err|", float(np.max(np.abs(got - ex))), 1e-6)
+    drift = np.abs(ref - ex)
+    print(f"[parity] rotator set_freq reference drift max {float(drift.max()):.3e}")
+    assert np.all(np.abs(got - ref) <= drift + 1e-6)
+    # mix_usb_block: y = fma(I, cos, Q sin) with the same (retuned) phasors
+    U = gpu_lib.Rotator(f1, fs)
+    gu = np.concatenate([U.mix_usb_block(x[:ns]), (U.set_freq(f2, fs), U.mix_usb_block(x[ns:]))[1]])
+    pu = _exact_phasors(n, [(0, _theta(f1, fs)), (ns, _theta(f2, fs))])
+    eu = x.real.astype(np.float64) * pu.real + x.imag.astype(np.float64) * pu.imag
+    report("rotator mix_usb_block GPU vs exact max|err|", float(np.max(np.abs(gu - eu))), 1e-6)
+    ru = oracle.rotator_retune(x, f1, fs, ns, f2, usb=True)
+    assert np.all(np.abs(gu - ru) <= np.abs(ru - eu) + 1e-6)
+    # mix_usb_block and rotate_block advance one oscillator: interleaved calls equal one stream
+    M = gpu_lib.Rotator(f1, fs)
+    a = M.process(x[:5000])
+    b = M.mix_usb_block(x[5000:9000])
+    p = _exact_phasors(9000, [(0, _theta(f1, fs))])
+    report("rotate_block then mix_usb_block (shared phase) max|err|",
+           max(float(np.max(np.abs(a - x[:5000] * p[:5000]))),
+               float(np.max(np.abs(b - (x[5000:9000].real * p[5000:].real + x[5000:9000].imag * p[5000:].imag))))),
+           1e-6)
+    # reset_phase: back to 1 + j0 with the current step; the same as a fresh oscillator on f2
+    R.reset_phase()
+    got_r = R.process(x[:50_000])
+    ref_r = gpu_lib.Rotator(f2, fs).process(x[:50_000])
+    report("rotator reset_phase vs fresh", float(np.max(np.abs(got_r - ref_r))), 0.0)
+    orr = oracle.rotator_retune(x[:60_000], f1, fs, 10_000, 0.0, reset=True)[10_000:]
+    report("rotator reset_phase vs oracle (f1) max|err|",
+           float(np.max(np.abs(gpu_lib.Rotator(f1, fs).process(x[10_000:60_000]) - orr))), 1e-4)
+
+
+@pytest.mark.parametrize("f1,f2,fs", [(12e3, -3e3, 48e3), (1.5e6, 2.5e6, 10e6)])
+def test_nco_block(gpu_lib, oracle, f1, f2, fs):
+    """nco.rs:20-66: mix_with_nco per sample (the non-FMA product), set_freq mid-stream
+    (phase continuous), next_cs as a block; GPU vs the exact phasor <= 1e-6, vs the
+    oracle's f32 recurrence within its drift."""
+    n, ns = 1 << 17, 70_001
+    x = cnoise(n, 0.5)
+    p = _exact_phasors(n, [(0, _theta(f1, fs)), (ns, _theta(f2, fs))])
+    N = gpu_lib.Nco(f1, fs)
+    got = np.concatenate([N.process(x[:ns]), (N.set_freq(f2), N.process(x[ns:]))[1]])
+    ex = x.astype(np.complex128) * p
+    report(f"nco mix {f1}->{f2} GPU vs exact max|err|", float(np.max(np.abs(got - ex))), 1e-6)
+    ref = oracle.nco(x, f1, fs, ns, f2)
+    assert np.all(np.abs(got - ref) <= np.abs(ref - ex) + 1e-6)
+    G = gpu_lib.Nco(f1, fs)
+    g = np.concatenate([G.next_cs_block(ns), (G.set_freq(f2), G.next_cs_block(n - ns))[1]])
+    report("nco next_cs GPU vs exact max|err|", float(np.max(np.abs(g - p))), 1e-6)
+    rg = oracle.nco(x, f1, fs, ns, f2, gen=True)
+    assert np.all(np.abs(g - rg) <= np.abs(rg - p) + 1e-6)
+    assert gpu_lib._L.orion_nco_set_freq(gpu_lib.Rotator(f1, fs)._h, f2) == -4  # ORION_E_TYPE
+    assert gpu_lib._L.orion_rotator_set_freq(N._h, f2, fs) == -4
+
+
+def _biquad_resonator(r, f0, fs):
+    """A two-pole resonator (poles r e^{+-j w0}) with a zero pair at +-1: b = (1-r)(1, 0, -1)."""
+    w = 2 * np.pi * f0 / fs
+    g = 1.0 - r
+    return (np.float32(g), np.float32(0.0), np.float32(-g), np.float32(-2 * r * np.cos(w)), np.float32(r * r))
+
+
+@pytest.mark.parametrize("kind", ["lp_rbj", "resonator_r0.9999", "resonator_r0.99"])
+def test_biquad(gpu_lib, oracle, kind):
+    """iir.rs:15-41 Biquad::new(b0, b1, b2, a1, a2): the generic TDF-II block. A design
+    whose state decays within a chunk runs one pass (k_scan_sp); a pole at r = 0.9999
+    does not forget (r^8192 = 0.44) and takes the three-kernel scan with f64 carries.
+    Tolerance: the reference's own 1-ulp input sensitivity (floor_tol)."""
+    if kind == "lp_rbj":
+        c = tuple(gpu_lib.lp_cascade_design(48e3, 3000.0))
+    else:
+        c = _biquad_resonator(float(kind.split("r")[-1]), 1234.0, 48e3)
+    x = RNG.standard_normal(200_003).astype(np.float32)
+    fn = lambda v: oracle.biquad(v, *c)  # noqa: E731
+    ref = fn(x)
+    tol = floor_tol(1e-6, fn, x)
+    B = gpu_lib.Biquad(*c)
+    report(f"biquad {kind} one call nrmse", nrmse(B.process(x), ref), tol)
+    report(f"biquad {kind} streamed 10007 nrmse", nrmse(stream(gpu_lib.Biquad(*c), x, 10007), ref), tol)
+    B3 = gpu_lib.Biquad(*c).configure_option("scan_path", 1)
+    report(f"biquad {kind} three-kernel streamed nrmse", nrmse(stream(B3, x, 65_536), ref), tol)
+    B.reset()
+    report(f"biquad {kind} after reset nrmse", nrmse(B.process(x[:50_000]), ref[:50_000]), tol)
+
+
+@pytest.mark.parametrize("sqrt_map", [False, True])
+@pytest.mark.parametrize("fs,lp,dc", [(48e3, 2520.0, 2.0), (8e3, 3000.0, 2.0)])
+def test_lp_dc_cascade(gpu_lib, oracle, sqrt_map, fs, lp, dc):
+    """iir.rs:111-186 LpDcCascade as a standalone block: process (LP4 then the DC
+    blocker) and process_mapped(x, f32::sqrt); single pass (k_lpdc_sp) where the LP4
+    forgets within the warm-up, the scans otherwise, and streamed calls."""
+    n = 150_001
+    if sqrt_map:  # a power envelope (the AM-PowerSqrt use): positive
+        x = (np.abs(cnoise(n)) ** 2 + 0.5).astype(np.float32)
+    else:
+        x = (RNG.standard_normal(n) + 0.25).astype(np.float32)
+    fn = lambda v: oracle.lp_dc_cascade(v, fs, lp, dc, sqrt_map)  # noqa: E731
+    ref = fn(x)
+    tol = floor_tol(1e-6, fn, x)
+    got = gpu_lib.LpDcCascade(fs, lp, dc, sqrt_map=sqrt_map).process(x)
+    report(f"lp_dc_cascade fs={fs} sqrt={sqrt_map} nrmse", nrmse(got, ref), tol)
+    got = stream(gpu_lib.LpDcCascade(fs, lp, dc, sqrt_map=sqrt_map), x, 33_333)
+    report(f"lp_dc_cascade fs={fs} sqrt={sqrt_map} streamed nrmse", nrmse(got, ref), tol)
+    L3 = gpu_lib.LpDcCascade(fs, lp, dc, sqrt_map=sqrt_map).configure_option("scan_path", 1)
+    report(f"lp_dc_cascade fs={fs} sqrt={sqrt_map} scans nrmse", nrmse(stream(L3, x, 33_333), ref), tol)
+    assert np.array_equal(gpu_lib.LpDcCascade(fs, lp, dc).taps(), oracle.lpdc_coeffs(fs, lp, dc))
+
+
 # ---- FirDecimator (a4) ------------------------------------------------------------------
 def test_decimator_golden(gpu_lib):
     D = gpu_lib.FirDecimator(10e6, 8, 200e3, 79e3)
@@ -591,6 +732,66 @@ def test_ssb_phasing_mod(gpu_lib, oracle, usb, rf, fs):
     if rf == 0.0:
         d = gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0).process(got)
         report("ssb mod -> demod round trip vs oracle nrmse", nrmse(d, oracle.ssb_demod(ref, FS, 1500.0, 2800.0)), 1e-4)
+
+
+@pytest.mark.parametrize("rf,kp,gain", [(0.0, 0.9, 1.0), (12e3, 2.5, 0.7), (1.5e6, 1.2, 1.0)])
+def test_pm_direct_phase_mod(gpu_lib, oracle, rf, kp, gain):
+    """modulate/pm.rs:36-47 on the device: (cos kp x, sin kp x) * gain mixed with the
+    RF Nco (non-FMA). Baseband: the GPU's cosf/sinf vs glibc's (a few ulp); with RF,
+    the reference's phasor recurrence drift bounds the difference, as for the Rotator."""
+    fs = FS if rf < 1e6 else 10e6
+    n = 1 << 18
+    a = _speech(n, fs)
+    m = gpu_lib.PmDirectPhaseMod(fs, kp, rf)
+    m.set_gain(gain)
+    got = np.concatenate([m.process(a[:100_001]), m.process(a[100_001:])])
+    ref = oracle.pm_mod(a, fs, kp, rf) * np.float32(gain)
+    bb = (np.exp(1j * kp * a.astype(np.float64)) * gain) * _exact_phasors(n, [(0, _theta(rf, fs))])
+    report(f"pm_mod rf={rf} GPU vs exact max|err|", float(np.max(np.abs(got - bb))), 2e-6)
+    assert np.all(np.abs(got - ref) <= np.abs(ref - bb) + 2e-6)
+    m.set_sensitivity(kp / 2)
+    assert m.process(a[:10]).shape == (10,)
+
+
+@pytest.mark.parametrize("tone,rise,fall", [(0.0, 5.0, 5.0), (700.0, 2.0, 8.0), (12e3, 0.05, 1.0)])
+def test_cw_keyed_mod(gpu_lib, oracle, tone, rise, fall):
+    """modulate/cw.rs:45-87 on the device: the keying envelope (input clamped to [0, 1],
+    rise/fall one-pole) is the same switched recurrence as AgcRms (chunked warm-ups,
+    bitwise exactness check, in-order re-runs): bit-exact with the oracle's envelope,
+    so with tone 0 the whole output is bit-exact; with a tone, the reference's NCO
+    recurrence drift bounds the difference. Keying: on/off steps, ragged levels, and
+    values outside [0, 1]."""
+    n = 1 << 18
+    k = np.repeat(np.tile(np.array([1.0, 0.0, 0.6, 1.4, -0.2, 1.0, 0.0], np.float32), 1 + n // 7000), 1000)[:n]
+    k = (k + 0.01 * RNG.standard_normal(n).astype(np.float32) * (np.arange(n) % 3 == 0)).astype(np.float32)
+    m = gpu_lib.CwKeyedMod(FS, tone, rise, fall)
+    got = np.concatenate([m.process(k[:77_777]), m.process(k[77_777:])])
+    ref = oracle.cw_mod(k, FS, tone, rise, fall)
+    if tone == 0.0:
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), "bit-exact at baseband"
+    env = np.abs(ref.astype(np.complex128))
+    ex = env * _exact_phasors(n, [(0, _theta(tone, FS))])
+    report(f"cw_mod tone={tone} |GPU| vs |oracle| max", float(np.max(np.abs(np.abs(got) - env))), 1e-6)
+    assert np.all(np.abs(got - ref) <= np.abs(ref - ex) + 2e-6)
+    m2 = gpu_lib.CwKeyedMod(FS, tone, rise, fall)
+    m2.set_gain(0.5)
+    report("cw_mod set_gain", float(np.max(np.abs(m2.process(k[:5000]) - 0.5 * got[:5000]))), 1e-6)
+
+
+def test_tx_lowpass_apply(gpu_lib, oracle):
+    """multicarrier/tx_lowpass.rs:185-195: TxLowpass::for_null_band(...).apply(stream) =
+    filter_aligned of the designed FirLowpassIq, host copy and in place on the device."""
+    import torch
+
+    tx = gpu_lib.TxLowpass.for_null_band(2048, 852, 45, 60.0)
+    x = cnoise(300_001)
+    taps = oracle.kaiser_lowpass_taps(tx.num_taps, tx.cutoff_norm, tx.stopband_db)
+    assert np.array_equal(tx.filter().taps().view(np.uint32), taps.view(np.uint32))
+    ref = oracle.fir_lowpass_iq_aligned(x, taps)
+    report("tx_lowpass apply (host) nrmse", nrmse(tx.apply(x), ref), 1e-6)
+    xd = torch.from_numpy(x).cuda()
+    tx.apply(xd)
+    report("tx_lowpass apply (device, in place) nrmse", nrmse(xd.cpu().numpy(), ref), 1e-6)
 
 
 def test_modulator_setters_reject_other_blocks(gpu_lib):

@@ -45,6 +45,76 @@ def test_golden_blocks(oracle):
     _eq(oracle.fir_lowpass_iq_aligned(x, GOLD["kaiser_31"]), GOLD["firiq_aligned_out"])
     _eq(oracle.add_awgn(np.zeros(300, np.complex64), 0.01, SEED), GOLD["awgn_p001"])
     _eq(oracle.wbfm(GOLD["wbfm_iq"]), GOLD["wbfm_out"])
+    _eq(oracle.rotator_retune(x, 1500.0, 48e3, len(x), 0.0, usb=True), GOLD["mix_usb_out"])
+    _eq(oracle.nco(x, 12e3, 48e3), GOLD["nco_mix_out"])
+    _eq(oracle.biquad(xr, *GOLD["biquad_coeffs"]), GOLD["biquad_out"])
+    _eq(oracle.lp_dc_cascade(xr, 48e3, 2520.0, 2.0), GOLD["lpdc_out"])
+    _eq(oracle.lp_dc_cascade(GOLD["lpdc_sqrt_in"], 48e3, 2520.0, 2.0, True), GOLD["lpdc_sqrt_out"])
+    _eq(oracle.pm_mod(_golden_audio(), 48e3, 0.9, 12e3), GOLD["pm_mod_out"])
+    _eq(oracle.cw_mod(GOLD["cw_key"], 48e3, 700.0, 2.0, 8.0), GOLD["cw_mod_out"])
+
+
+def _golden_audio():
+    t = np.arange(3000, dtype=np.float32) / 48e3
+    return (0.5 * np.sin(2 * np.pi * 1000 * t)).astype(np.float32)
+
+
+def test_np_ref_reproduces_every_golden_output():
+    """The independent numpy restatement (tests/np_ref.py, correctly rounded FMA
+    emulation) recomputes every recorded output from the recorded inputs bit for
+    bit: each fixture is agreed by two restatements of the reference source."""
+    import np_ref as R
+
+    x, xr, aud = GOLD["x_c"], GOLD["x_r"], _golden_audio()
+    checks = {
+        "rotator_out": lambda: R.rotator(x, -1.5e6, 10e6),
+        "fir_lowpass_out": lambda: R.fir_lowpass(xr, R.fir_lowpass_taps(1.25e6, 15e3, 10e3)),
+        "decim_out": lambda: R.fir_decimator(x, 10e6, 8, 200e3, 79e3),
+        "lp_cascade_out": lambda: R.lp_cascade(xr, 1.25e6, 13.5e3),
+        "fm_iq": lambda: R.fm_mod(aud, 48e3, 2500.0),
+        "fm_demod_out": lambda: R.fm_demod(GOLD["fm_iq"], 48e3, 2500.0, 5000.0),
+        "pm_demod_out": lambda: R.pm_demod(GOLD["fm_iq"], 48e3, 0.9, 5000.0),
+        "ssb_demod_out": lambda: R.ssb_demod(GOLD["ssb_iq"], 48e3, 1500.0, 2800.0),
+        "am_iq": lambda: R.am_mod(aud, 48e3, 0.0, 0.8, 0.5),
+        "am_demod_out": lambda: R.am_demod(GOLD["am_iq"], 48e3, 5000.0),
+        "am_abs_demod_out": lambda: R.am_demod(GOLD["am_iq"], 48e3, 5000.0, (0.9482, 0.3920)),
+        "cw_demod_out": lambda: R.cw_demod(GOLD["am_iq"], 48e3, 700.0, 300.0),
+        "dc_out": lambda: R.dc_blocker(xr, 48e3, 2.0),
+        "firiq_out": lambda: R.fir_lowpass_iq(x, GOLD["kaiser_31"]),
+        "firiq_aligned_out": lambda: R.fir_lowpass_iq_aligned(x, GOLD["kaiser_31"]),
+        "kaiser_127": lambda: R.kaiser_lowpass_taps(127, 0.2, 60.0),
+        "mix_usb_out": lambda: R.rotator_mix_usb(x, 1500.0, 48e3),
+        "nco_mix_out": lambda: R.nco_mix(x, 12e3, 48e3),
+        "biquad_out": lambda: R.biquad(xr, *GOLD["biquad_coeffs"]),
+        "lpdc_out": lambda: R.lp_dc_cascade(xr, 48e3, 2520.0, 2.0),
+        "lpdc_sqrt_out": lambda: R.lp_dc_cascade(GOLD["lpdc_sqrt_in"], 48e3, 2520.0, 2.0, True),
+        "pm_mod_out": lambda: R.pm_mod(aud, 48e3, 0.9, 12e3),
+        "cw_mod_out": lambda: R.cw_mod(GOLD["cw_key"], 48e3, 700.0, 2.0, 8.0),
+        "wbfm_out": lambda: R.wbfm(GOLD["wbfm_iq"]),
+        "awgn_p001": lambda: R.add_awgn(np.zeros(300, np.complex64), 0.01, SEED),
+    }
+    for key, fn in checks.items():
+        got = np.asarray(fn())
+        _eq(got.astype(GOLD[key].dtype), GOLD[key])
+
+
+def test_np_ref_fma_is_correctly_rounded():
+    """np_ref._fma against exact rational arithmetic, including a double-rounding
+    tie that a plain f64 a*b + c rounded to f32 gets wrong."""
+    from fractions import Fraction
+
+    import np_ref as R
+
+    rng = np.random.default_rng(3)
+    for _ in range(3000):
+        a, b, c = (np.float32(v) for v in rng.standard_normal(3) * np.exp(rng.uniform(-20, 20, 3)))
+        ex = Fraction(float(a)) * Fraction(float(b)) + Fraction(float(c))
+        r = R._fma(a, b, c)
+        for q in (np.nextafter(r, np.float32(np.inf)), np.nextafter(r, np.float32(-np.inf))):
+            assert abs(Fraction(float(r)) - ex) <= abs(Fraction(float(q)) - ex)
+    a, b, c = np.float32(1 - 2 ** -23), np.float32(64 + 2 ** -17), np.float32(2 ** 30 + 128)
+    assert R._fma(a, b, c) == np.float32(2 ** 30 + 128)  # exact: 2^30 + 192 - 2^-40
+    assert np.float32(np.float64(a) * np.float64(b) + np.float64(c)) == np.float32(2 ** 30 + 256)
 
 
 def test_golden_atan2(oracle):
