@@ -141,8 +141,13 @@ def test_rotator_set_freq_reset_phase_mix_usb(gpu_lib, oracle, f1, f2, fs):
     ref_r = gpu_lib.Rotator(f2, fs).process(x[:50_000])
     report("rotator reset_phase vs fresh", float(np.max(np.abs(got_r - ref_r))), 0.0)
     orr = oracle.rotator_retune(x[:60_000], f1, fs, 10_000, 0.0, reset=True)[10_000:]
-    report("rotator reset_phase vs oracle (f1) max|err|",
-           float(np.max(np.abs(gpu_lib.Rotator(f1, fs).process(x[10_000:60_000]) - orr))), 1e-4)
+    g2 = gpu_lib.Rotator(f1, fs)
+    g2.process(x[:10_000])
+    g2.reset_phase()
+    got2 = g2.process(x[10_000:60_000])
+    ex2 = x[10_000:60_000].astype(np.complex128) * _exact_phasors(50_000, [(0, _theta(f1, fs))])
+    report("rotator reset_phase GPU vs exact max|err|", float(np.max(np.abs(got2 - ex2))), 1e-6)
+    assert np.all(np.abs(got2 - orr) <= np.abs(orr - ex2) + 1e-6)
 
 
 @pytest.mark.parametrize("f1,f2,fs", [(12e3, -3e3, 48e3), (1.5e6, 2.5e6, 10e6)])
@@ -205,8 +210,8 @@ def test_lp_dc_cascade(gpu_lib, oracle, sqrt_map, fs, lp, dc):
     blocker) and process_mapped(x, f32::sqrt); single pass (k_lpdc_sp) where the LP4
     forgets within the warm-up, the scans otherwise, and streamed calls."""
     n = 150_001
-    if sqrt_map:  # a power envelope (the AM-PowerSqrt use): positive
-        x = (np.abs(cnoise(n)) ** 2 + 0.5).astype(np.float32)
+    if sqrt_map:  # a power envelope (the AM-PowerSqrt use) whose LP4 output stays positive
+        x = (0.2 * np.abs(cnoise(n)) ** 2 + 2.0).astype(np.float32)
     else:
         x = (RNG.standard_normal(n) + 0.25).astype(np.float32)
     fn = lambda v: oracle.lp_dc_cascade(v, fs, lp, dc, sqrt_map)  # noqa: E731
@@ -216,8 +221,11 @@ def test_lp_dc_cascade(gpu_lib, oracle, sqrt_map, fs, lp, dc):
     report(f"lp_dc_cascade fs={fs} sqrt={sqrt_map} nrmse", nrmse(got, ref), tol)
     got = stream(gpu_lib.LpDcCascade(fs, lp, dc, sqrt_map=sqrt_map), x, 33_333)
     report(f"lp_dc_cascade fs={fs} sqrt={sqrt_map} streamed nrmse", nrmse(got, ref), tol)
+    # the scans (three-kernel; with the sqrt map an LP4 scan, then a DC scan through HBM):
+    # the DC pole (1 - 2.6e-4) carries the f64 block-carry rounding a long way, as for
+    # AmEnvelopeDemod PowerSqrt's two-scan form (1e-5)
     L3 = gpu_lib.LpDcCascade(fs, lp, dc, sqrt_map=sqrt_map).configure_option("scan_path", 1)
-    report(f"lp_dc_cascade fs={fs} sqrt={sqrt_map} scans nrmse", nrmse(stream(L3, x, 33_333), ref), tol)
+    report(f"lp_dc_cascade fs={fs} sqrt={sqrt_map} scans nrmse", nrmse(stream(L3, x, 33_333), ref), max(tol, 1e-5))
     assert np.array_equal(gpu_lib.LpDcCascade(fs, lp, dc).taps(), oracle.lpdc_coeffs(fs, lp, dc))
 
 
@@ -769,9 +777,10 @@ def test_cw_keyed_mod(gpu_lib, oracle, tone, rise, fall):
     ref = oracle.cw_mod(k, FS, tone, rise, fall)
     if tone == 0.0:
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), "bit-exact at baseband"
-    env = np.abs(ref.astype(np.complex128))
+    env = oracle.cw_mod(k, FS, 0.0, rise, fall).real.astype(np.float64)  # the reference's envelope, exactly
     ex = env * _exact_phasors(n, [(0, _theta(tone, FS))])
-    report(f"cw_mod tone={tone} |GPU| vs |oracle| max", float(np.max(np.abs(np.abs(got) - env))), 1e-6)
+    report(f"cw_mod tone={tone} GPU vs exact (reference envelope x exact phasor) max", float(np.max(np.abs(got - ex))),
+           1e-6)
     assert np.all(np.abs(got - ref) <= np.abs(ref - ex) + 2e-6)
     m2 = gpu_lib.CwKeyedMod(FS, tone, rise, fall)
     m2.set_gain(0.5)
