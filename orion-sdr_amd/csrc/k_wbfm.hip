@@ -35,8 +35,25 @@
 #include "kernels.hpp"
 #include "poly.hpp"
 
+// Experiment builds only (tools/wbfm_exp.py; the product build leaves it 0): bit 1
+// reads every tile from the channel's first 512 KB (L2-resident: no HBM stream),
+// bit 2 skips the audio FIR, bit 4 skips the backs' IIR, bit 8 the predecessor
+// wait. Outputs are wrong under any bit.
+#ifndef ORION_WBFM_EXP
+#define ORION_WBFM_EXP 0
+#endif
+
 namespace orion {
 namespace {
+
+// Ordering of a wave's own LDS hand-offs (a write, then reads of the same words by
+// any lane of the same wave): the DS instructions of one wave execute in issue
+// order, so no lgkmcnt wait is needed, only a compiler fence that keeps the
+// accesses in program order. (Experiment bit 16: the old s_waitcnt lgkmcnt(0).)
+__device__ __forceinline__ void lds_order() {
+  if constexpr ((ORION_WBFM_EXP & 16) != 0) wave_lds_fence();
+  else asm volatile("" ::: "memory");
+}
 
 constexpr int NT = 256;
 constexpr int T = kWbfmT;
@@ -98,6 +115,8 @@ __device__ __forceinline__ void front2_load(const f2* __restrict__ x, long long 
     lo = static_cast<int>(max(-B, -kSat));                                   // even
     hi = static_cast<int>(min(max((n - 2 - B) & ~1LL, -kSat), kSat));        // even, >= lo
     xb = x + B;
+  } else if constexpr ((ORION_WBFM_EXP & 1) != 0) {
+    xb = x + (B & ((1LL << 16) - 1));
   } else {
     xb = x + min(max(B, 0LL), (n - Fw<R>::NEW) & ~1LL);
   }
@@ -236,7 +255,7 @@ __global__ __launch_bounds__(64, R <= 2 ? 3 : 2) void k_wbfm_front2(const WbfmAr
           *reinterpret_cast<f4*>(U + c * G::LR + 2 * h) = f4{y0.x, y0.y, y1.x, y1.y};
         }
       }
-      wave_lds_fence();
+      lds_order();
     }
     // ---- stage the new samples: NCO mix, polyphase scatter ----
     const bool bnd = porg < 0 || porg + 8LL * (G::TW + Q) > a.n;
@@ -269,7 +288,7 @@ __global__ __launch_bounds__(64, R <= 2 ? 3 : 2) void k_wbfm_front2(const WbfmAr
     if (bnd) {
       // Tile reaching before x[0] or past x[n-1]: the clamped prefetch staged
       // wrong samples there; rewrite exactly those slots (history / zeros).
-      wave_lds_fence();
+      lds_order();
 #pragma unroll 1
       for (int p = 8 * Q + l; p < 8 * (G::TW + Q); p += 64) {
         const long long P = porg + p;
@@ -279,7 +298,7 @@ __global__ __launch_bounds__(64, R <= 2 ? 3 : 2) void k_wbfm_front2(const WbfmAr
         }
       }
     }
-    wave_lds_fence();
+    lds_order();
 
     // ---- polyphase FIR: outputs jd0 + R l + rho ----
     f2 d[R];
@@ -724,14 +743,34 @@ __device__ __forceinline__ void phase(const f2* __restrict__ U, int c, int lp, c
 }
 }  // namespace g8
 
+// Issue priority: hi = the wave's turn for priority (kernel comment); boost = a
+// latency-critical section (experiment bits 32: staging and the post-FIR chain,
+// 64: the FMA blocks).
+template <int L>
+__device__ __forceinline__ void prio() {
+  __builtin_amdgcn_s_setprio(L);
+}
+__device__ __forceinline__ void set_prio(bool hi, bool boost) {
+  constexpr bool kB = (ORION_WBFM_EXP & 96) != 0;
+  if (hi) {
+    if (boost) prio<3>();
+    else prio<kB ? 2 : 1>();
+  } else {
+    if (boost) prio<1>();
+    else prio<0>();
+  }
+}
+
 template <bool A16, bool CLAMP>
 __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg, long long jd0,
                                          const f2 (&ph)[8][2], f2 (&v)[8][2], const FuPrefetch& pf, f2 Sv,
-                                         f2& carry, float* __restrict__ phit, int svi) {
+                                         f2& carry, float* __restrict__ phit, int svi, bool hi, float& tch) {
   using G = fu::G;
   f2* __restrict__ U = T.U;
   const int l = T.l;
-  if (n > 0) {  // halo: entries TW .. TW+Q of every row -> 0 .. Q, times e^{-j theta NEW}
+  if constexpr ((ORION_WBFM_EXP & 32) != 0) set_prio(hi, true);
+  constexpr bool kOldHalo = (ORION_WBFM_EXP & 256) != 0;
+  if (kOldHalo && n > 0) {  // halo: entries TW .. TW+Q of every row -> 0 .. Q, times e^{-j theta NEW}
 #pragma unroll
     for (int r2 = 0; r2 < 2; ++r2) {
       const int e = l + 64 * r2;
@@ -743,7 +782,20 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
         *reinterpret_cast<f4*>(U + dst) = f4{y0.x, y0.y, y1.x, y1.y};
       }
     }
-    wave_lds_fence();
+    lds_order();
+  }
+  // Halo (n > 0): the previous tile's entries TW .. TW+Q of each row become entries
+  // 0 .. Q, times e^{-j theta NEW}. Entries 0..15 of every row (lane l: row l & 7,
+  // pair l >> 3: conflict-free b128 stores) and entry Q of rows 1..7 (lanes 0..6;
+  // row 0's entry Q is a staged sample). The sources are read BEFORE the staging
+  // stores overwrite them and written after (DS operations of a wave execute in
+  // order), so the read's latency hides behind the staging.
+  const int hc = l & 7, hh = l >> 3;
+  f4 hw = f4{0, 0, 0, 0};
+  f2 hq = f2{0, 0};
+  if (!kOldHalo && n > 0) {
+    hw = *reinterpret_cast<const f4*>(U + hc * g8::LRS + 2 * (80 + g8::pchunk(hh)));
+    if (l < 7) hq = U[(l + 1) * g8::LRS + g8::slot(G::TW + Q)];
   }
   const bool bnd = porg < 0 || porg + 8LL * (G::TW + Q) > T.a.n;
 #pragma unroll
@@ -753,11 +805,24 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
     if (k % 4 == 3) asm volatile("" ::: "memory");
   }
   asm volatile("" ::: "memory");
+  if (!kOldHalo && n > 0) {
+    const f2 y0 = cmul(f2{hw.x, hw.y}, T.corr), y1 = cmul(f2{hw.z, hw.w}, T.corr);
+    *reinterpret_cast<f4*>(U + hc * g8::LRS + 2 * g8::pchunk(hh)) = f4{y0.x, y0.y, y1.x, y1.y};
+    if (l < 7) U[(l + 1) * g8::LRS + g8::slot(Q)] = cmul(hq, T.corr);
+  }
   // unconditional: a conditional prefetch makes the compiler's wait counting assume
   // the loads may be absent and drain them (vmcnt(0))
   front2_load<2, A16, CLAMP>(pf.xl, pf.nl, pf.porg, l, v);
+  if constexpr ((ORION_WBFM_EXP & 1024) != 0) {
+    // L2 touch of the tile after the prefetched one: one dword per 128-B line (64
+    // lanes = the tile's 8 KB). The previous touch's value is consumed here (an
+    // empty asm use), so the compiler counts it in vmcnt behind this tile's loads.
+    asm volatile("" ::"v"(tch));
+    const long long tp = min(max(pf.porg + G::NEW + 8 * Q + 16LL * l, 0LL), pf.nl - 1);
+    tch = reinterpret_cast<const float*>(pf.xl + tp)[0];
+  }
   if (bnd) {
-    wave_lds_fence();
+    lds_order();
 #pragma unroll 1
     for (int p = (n == 0 ? 0 : 8 * Q) + l; p < 8 * (G::TW + Q); p += 64) {
       const long long Pp = porg + p;
@@ -767,9 +832,10 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
       }
     }
   }
-  wave_lds_fence();
+  lds_order();
   // group g: phases 2g, 2g+1; window entries 8l' .. 8l'+23 of the phase's row
   const int g = g8::group(l), lp = l & 15;
+  if constexpr ((ORION_WBFM_EXP & 96) != 0) set_prio(hi, (ORION_WBFM_EXP & 64) != 0);
   f2 d[8];
   // phase 2g opens the eight chains with a product (no zeroing), phase 2g+1 follows;
   // the compiler barrier keeps the second phase's reads behind the first's FMAs
@@ -777,6 +843,7 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
   g8::phase<true, true>(U, 2 * g, lp, T.Gt, d);
   asm volatile("" ::: "memory");
   g8::phase<false, true>(U, 2 * g + 1, lp, T.Gt, d);
+  if constexpr ((ORION_WBFM_EXP & 96) != 0) set_prio(hi, (ORION_WBFM_EXP & 32) != 0);
   // rows 0<->1, 2<->3: even rows keep outputs 0..3, odd rows 4..7 (x: d[i], y: d[i+4])
   f2 K[4];
 #pragma unroll
@@ -812,6 +879,8 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
       acc += f2{__shfl_xor(acc.x, off, 64), __shfl_xor(acc.y, off, 64)};
     carry = cmul(acc, S);
   }
+  // (an LDS permute: the lane-swap form, permlane32 + permlane16 + DPP, measured
+  // 4-5 us slower per launch)
   const int src = g8::prev_lane(l);
   f2 pv = f2{__shfl(F[1].x, src, 64), __shfl(F[1].y, src, 64)};
   if (l == 0) pv = carry;
@@ -819,6 +888,7 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
   *reinterpret_cast<f2*>(phit + j0) = f2{fm_disc_pk_rcp(F[0], pv, T.C.k), fm_disc_pk_rcp(F[1], F[0], T.C.k)};
   carry = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(F[1].x), 63)),
              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(F[1].y), 63))};
+  if constexpr ((ORION_WBFM_EXP & 32) != 0) set_prio(hi, false);
   const WbfmArgs& a = T.a;
   if (jd0 <= a.n_dec - 1 && a.n_dec - 1 < jd0 + G::TW) {  // carried state of the next call
     const int rl = static_cast<int>(a.n_dec - 1 - jd0);
@@ -915,7 +985,7 @@ __device__ __forceinline__ void iir16(const WbfmFusedConst& Bc, const float* __r
     xs[i + 2] = f2{u.z, w.z};
     xs[i + 3] = f2{u.w, w.w};
   }
-  wave_lds_fence();
+  lds_order();
   const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
   f2 z[4] = {f2{0, 0}, f2{0, 0}, f2{0, 0}, f2{0, 0}};
 #pragma unroll
@@ -979,10 +1049,10 @@ __device__ __forceinline__ void zs_only16(const WbfmFusedConst& Bc, const float*
       tl[8 + i] = f.y;
     }
   }
-  wave_lds_fence();
+  lds_order();
   hout[0] = tmp[l];
   hout[1] = tmp[l + 64];
-  wave_lds_fence();
+  lds_order();
 }
 
 // The back of one sub-range [A0, A0 + Lr) from its exact entering state sw and
@@ -1018,7 +1088,14 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
   f2 ef[4];
   {  // lane l: samples 16l .. 16l+15 (iir16), written to P one scalar at a time
     double send[4];
-    iir16(Bc, Phi, l, sw, xs, ef, send);
+    if constexpr ((ORION_WBFM_EXP & 4) == 0) {
+      iir16(Bc, Phi, l, sw, xs, ef, send);
+    } else {
+#pragma unroll
+      for (int i = 0; i < CH; ++i) xs[i] = f2{Phi[16 * l + i], Phi[16 * l + 8 + i]};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ef[k] = f2{static_cast<float>(sw[k]), 0.0f};
+    }
     if (trace_r >= 0) fu::trace(a, trace_r, 10);
     const int jl = Lr - 1;
     float cap[4] = {0, 0, 0, 0};
@@ -1058,13 +1135,13 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
     for (int k = 0; k < 4; ++k)
       sw[k] = static_cast<double>(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(ef[k].y), 63)));
   }
-  wave_lds_fence();
+  lds_order();
 #pragma unroll
   for (int r2 = 0; r2 < 2; ++r2) {  // pairs j in [-128, 0): (history, f[j + NH])
     const int t = l + 64 * r2;
     P[Y::pslot(t)] = f2{hist[r2], P[Y::pslot(t + NH)].x};
   }
-  wave_lds_fence();
+  lds_order();
 #pragma unroll
   for (int r2 = 0; r2 < 2; ++r2) hist[r2] = P[Y::pslot(NH + l + 64 * r2)].y;  // f[L - 128 + t]: the next history
   if (publish_r >= 0) publish_end(a, publish_r, sw, hist, l);
@@ -1076,7 +1153,7 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
 #pragma unroll
     for (int i = 0; i < CH; ++i) acc[i] = f2{0.0f, 0.0f};
 #pragma unroll 1
-    for (int kb = 0; kb < 128 / KB; ++kb) {
+    for (int kb = 0; kb < ((ORION_WBFM_EXP & 2) ? 0 : 128 / KB); ++kb) {
       // tap k = KB kb + kk of output i reads pair e = CH l + i - k + PB
       // = CH (l - kb) + O + m, m = i + KB - 1 - kk
       const f2* __restrict__ Pl = P + (CH + 1) * (l - KB * kb / CH) + O;
@@ -1117,7 +1194,7 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
       a.carry_out[ch * kWbfmCarry + 8 + t] = f;
     }
   }
-  wave_lds_fence();
+  lds_order();
   if (trace_r >= 0) fu::trace(a, trace_r, 12);  // debug: audio FIR done
 }
 
@@ -1192,6 +1269,7 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
     const float* ci = a.carry_in + g.ch * kWbfmCarry;
     carry = f2{ci[4], ci[5]};
   }
+  float tch = 0.0f;             // L2 touch (experiment bit 1024)
   double sw[4] = {0, 0, 0, 0};  // IIR state entering the next sub-range
   float hist[2] = {0, 0};       // its FIR history
   // past the segment: a dummy read of the channel's first tile, shared by every
@@ -1215,16 +1293,16 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
     }
 #pragma unroll 1
     for (int tin = 0; tin < sg::NS; ++tin, ++n, porg += G::NEW) {
-      if ((16 * n < kSegPrioQ16 * ntiles) == late) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
+      const bool hi = (16 * n < kSegPrioQ16 * ntiles) == late;
+      set_prio(hi, false);
       if ((n & 63) == 0)  // lane l: the common phasor of tile n + l
         Sv = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1 + static_cast<long long>(l) * G::NEW),
                         a.step[g.ch]);
       const long long jd0 = g.A + static_cast<long long>(n) * TW;
       const FuPrefetch p0 = n + 1 < ntiles ? FuPrefetch{org.xl, org.nl, porg + G::NEW, true} : dummy;
-      fu_tile8<A16, CLAMP>(T, n, porg, jd0, ph, va, p0, Sv, carry, Phi + TW * tin, n & 63);
+      fu_tile8<A16, CLAMP>(T, n, porg, jd0, ph, va, p0, Sv, carry, Phi + TW * tin, n & 63, hi, tch);
     }
-    wave_lds_fence();
+    lds_order();
     if (sub == 0) {
       // keep sub-range 0's phi for the deferred back in the segment's global slot
       f4* gs = reinterpret_cast<f4*>(myslot + kFuSlot);
@@ -1259,14 +1337,14 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
     hist[0] = ci[8 + l];
     hist[1] = ci[8 + 64 + l];
   } else {
-    fu::wait_for(a.flags + 3LL * (g.r - 1), a.epoch, a.err, a.spin);
+    if constexpr ((ORION_WBFM_EXP & 8) == 0) fu::wait_for(a.flags + 3LL * (g.r - 1), a.epoch, a.err, a.spin);
     const uint32_t* ps = a.hand + static_cast<long long>(g.r - 1) * sg::kSegSlot;
 #pragma unroll
     for (int k = 0; k < 4; ++k) sw[k] = sg::uni(fu::u2d(fu::ld_agent(ps + 2 + 2 * k), fu::ld_agent(ps + 3 + 2 * k)));
     hist[0] = __uint_as_float(fu::ld_agent(ps + 16 + l));
     hist[1] = __uint_as_float(fu::ld_agent(ps + 16 + 64 + l));
   }
-  wave_lds_fence();
+  lds_order();
   fu::trace(a, g.r, 2);
   sg::back(a, Bc, g.ch, g.A, min(sg::L, g.Lr), g.last && nsub == 1, Phi, P, l, sw, hist);
   fu::trace(a, g.r, 3);

@@ -64,6 +64,13 @@ def _load():
         raise ImportError(
             f"orion_sdr: native library {_LIB} is missing — build it with "
             "`make -C orion-sdr_amd` (hipcc, gfx950). There is no CPU fallback.")
+    # The library and torch both need libamdhip64.so.7 (one soname: the first one
+    # loaded serves the process). Load torch's first, as bench.py does, so torch's
+    # own device path keeps the runtime it was built against whatever the import order.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(_LIB)
     vp, sz, f, i = C.c_void_p, C.c_size_t, C.c_float, C.c_int
     fp = C.POINTER(C.c_float)
