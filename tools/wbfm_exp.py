@@ -35,7 +35,7 @@ def child(k, w, nch, n):
     print(json.dumps({"med": t[len(t) // 2], "min": t[0], "mean": sum(t) / len(t)}))
 
 
-def multi(names, k, w, nch, n):
+def multi(names, k, w, nch, n, maxseg=0):
     """All variants in ONE process (each library loaded as its own module), launches
     interleaved A B C, B C A, ... so that the chip's clock state hits every variant
     alike; HIP events around each launch."""
@@ -55,6 +55,9 @@ def multi(names, k, w, nch, n):
     x = torch.randn((nch, n) if nch > 1 else (n,), dtype=torch.complex64, device=dev, generator=g)
     out = torch.empty((nch, n // 8) if nch > 1 else (n // 8,), dtype=torch.float32, device=dev)
     blks = {nm: m.WbfmChain(f_off=[0.0] * nch if nch > 1 else 0.0) for nm, m in mods.items()}
+    if maxseg:
+        for b in blks.values():
+            b.configure("segmented", maxseg)
     s = torch.cuda.current_stream(dev)
     for _ in range(w):
         for b in blks.values():
@@ -85,13 +88,14 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 26)
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--multi", action="store_true", help="all variants in one process, launches interleaved")
+    ap.add_argument("--maxseg", type=int, default=0, help="cap on the segmented kernel's waves")
     a = ap.parse_args()
     if a.child:
         return child(a.k, a.w, a.nch, a.n)
     if a.multi:
         for r in range(a.rounds):
             print(f"-- round {r}", flush=True)
-            multi(a.names, a.k, a.w, a.nch, a.n)
+            multi(a.names, a.k, a.w, a.nch, a.n, a.maxseg)
         return None
     res = {nm: [] for nm in a.names}
     for r in range(a.rounds):
