@@ -451,55 +451,60 @@ __device__ __forceinline__ void dc_combine(double m1, double d1, double& m2, dou
   m2 = m2 * m1;
 }
 
-// Staging of k_lpdc_sp (Ssb / AmAbs front ends) at SC samples per lane: every load
-// of the thread first, then the premap into the padded image (posS). The SSB mixing
-// phasor of sample e = t + k NT is (S_h tab[t]) tab[(k mod 16) NT], S_h the exact
-// phasor of the chunk's sample 4096 h (the table holds kScanCH phasors).
+// Staging of k_lpdc_sp at SC samples per lane, wave-local: wave w stages the chunk's
+// elements [64 SC w, 64 SC (w + 1)) (lane l: e = 64 SC w + l + 64 k, coalesced), which
+// are exactly the lane runs its own lanes process, so no workgroup barrier separates
+// the staging, the LP4 re-run's rewrite and the output staging from their readers (a
+// wave's LDS operations execute in order). The SSB mixing phasor of element e is
+// (S_h tab[e mod kScanCH - 64 k]) tab[64 k], S_h the exact phasor of the chunk's
+// sample kScanCH h, h = e / kScanCH (uniform in the wave).
 template <int SC>
 __device__ __forceinline__ int posS(int e) { return e + e / SC; }
+__device__ __forceinline__ void wave_order() { asm volatile("" ::: "memory"); }
 template <Pre PR, int SC>
 __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long base, int cnt, float* sb) {
-  static_assert(SC * NT <= 2 * kScanCH, "two phasor table spans cover the chunk");
+  constexpr int WR = 64 * SC;  // elements per wave
+  static_assert(kScanCH % WR == 0 && SC * NT <= 2 * kScanCH, "wave ranges inside one phasor table span");
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e0 = w * WR + l;
   if constexpr (PR == Pre::Real || PR == Pre::RealLp || PR == Pre::RealLpSqrt) {  // f32 input
     const float* __restrict__ xr = static_cast<const float*>(a.x) + ch * a.x_stride + base;
     float v[SC];
 #pragma unroll
     for (int k = 0; k < SC; ++k) {
-      const int e = threadIdx.x + k * NT;
+      const int e = e0 + 64 * k;
       v[k] = e < cnt ? xr[e] : 0.0f;
     }
 #pragma unroll
-    for (int k = 0; k < SC; ++k) sb[posS<SC>(threadIdx.x + k * NT)] = v[k];
+    for (int k = 0; k < SC; ++k) sb[posS<SC>(e0 + 64 * k)] = v[k];
     return;
   }
   const f2* __restrict__ x = static_cast<const f2*>(a.x) + ch * a.x_stride + base;
-  f2 St[2] = {f2{1.0f, 0.0f}, f2{1.0f, 0.0f}};
+  f2 St = f2{1.0f, 0.0f};
   if constexpr (PR == Pre::Ssb) {
-#pragma unroll
-    for (int h = 0; h < (SC * NT + kScanCH - 1) / kScanCH; ++h)
-      St[h] = cmul(phasor_q64(static_cast<uint64_t>(a.k0 + base + 1 + h * kScanCH), a.step), a.tab[threadIdx.x]);
+    const int h = (w * WR) / kScanCH;
+    St = cmul(phasor_q64(static_cast<uint64_t>(a.k0 + base + 1 + static_cast<long long>(h) * kScanCH), a.step),
+              a.tab[(w * WR) % kScanCH + l]);
   }
   f2 v[SC];
 #pragma unroll
   for (int k = 0; k < SC; ++k) {
-    const int e = threadIdx.x + k * NT;
+    const int e = e0 + 64 * k;
     v[k] = e < cnt ? x[e] : f2{0.0f, 0.0f};
   }
 #pragma unroll
   for (int k = 0; k < SC; ++k) {
-    const int e = threadIdx.x + k * NT;
     const f2 z = v[k];
     float o;
     if constexpr (PR == Pre::Ssb) {
-      constexpr int KT = kScanCH / NT;
-      const f2 p = cmul(St[k / KT], a.tab[(k % KT) * NT]);
+      const f2 p = cmul(St, a.tab[64 * k]);
       o = __builtin_fmaf(z.x, p.x, z.y * p.y);  // ssb.rs:37
     } else if constexpr (PR == Pre::AmSqrt) {
       o = __builtin_fmaf(z.x, z.x, z.y * z.y);  // am.rs:204
     } else {
       o = __builtin_fmaf(a.c.k1, fabsf(z.x), a.c.k2 * fabsf(z.y));  // am.rs:238
     }
-    sb[posS<SC>(e)] = o;
+    sb[posS<SC>(e0 + 64 * k)] = o;
   }
 }
 
@@ -534,7 +539,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   const RecLP4 lp{{a.c.b0, a.c.b1, a.c.b2, a.c.a1, a.c.a2}};
   const float r = a.c.r;
   stage_sp<PR, SC>(a, ch, base, cnt, sb);
-  __syncthreads();
+  wave_order();  // wave-local staging
 
   // ---- LP4: zero-state lane aggregates, block scan, exact re-run ----
   float xs[C];
@@ -621,10 +626,10 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
       xs[i] = lp.step(ef, xs[i]);  // LP output x (f32, reference update)
       if constexpr (PR == Pre::AmSqrt || PR == Pre::RealLpSqrt) xs[i] = sqrtf(xs[i]);  // process_mapped(.., f32::sqrt)
     }
-  __syncthreads();  // every lane has read its sb inputs
+  wave_order();  // (the wave's own inputs: read before they are overwritten, in order)
 #pragma unroll
   for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
-  __syncthreads();
+  __syncthreads();  // lane 0 of wave w reads wave w - 1's last LP output (xprev0)
   }  // LP
 
   // ---- DC blocker: zero-state lane pairs (r^k, y_k), block scan ----
@@ -765,12 +770,19 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
     co[6] = ci[6];
     co[7] = ci[7];
   }
-  __syncthreads();
+  wave_order();  // output staging, wave-local (every cross-wave read of sb was before the last barrier)
 #pragma unroll
   for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
-  __syncthreads();
+  wave_order();
   float* yo = static_cast<float*>(a.y) + ch * a.y_stride + o0;
-  for (int e2 = warm + t; e2 < cnt; e2 += NT) yo[e2 - warm] = sb[posS<SC>(e2)];
+  {
+    const int e0 = wave * (64 * SC) + lane;
+#pragma unroll
+    for (int k = 0; k < SC; ++k) {
+      const int e2 = e0 + 64 * k;
+      if (e2 >= warm && e2 < cnt) yo[e2 - warm] = sb[posS<SC>(e2)];
+    }
+  }
 }
 
 // ---- single-pass scan for recurrences that forget (k_scan_sp) ---------------------

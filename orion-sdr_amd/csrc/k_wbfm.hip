@@ -743,47 +743,13 @@ __device__ __forceinline__ void phase(const f2* __restrict__ U, int c, int lp, c
 }
 }  // namespace g8
 
-// Issue priority: hi = the wave's turn for priority (kernel comment); boost = a
-// latency-critical section (experiment bits 32: staging and the post-FIR chain,
-// 64: the FMA blocks).
-template <int L>
-__device__ __forceinline__ void prio() {
-  __builtin_amdgcn_s_setprio(L);
-}
-__device__ __forceinline__ void set_prio(bool hi, bool boost) {
-  constexpr bool kB = (ORION_WBFM_EXP & 96) != 0;
-  if (hi) {
-    if (boost) prio<3>();
-    else prio<kB ? 2 : 1>();
-  } else {
-    if (boost) prio<1>();
-    else prio<0>();
-  }
-}
-
 template <bool A16, bool CLAMP>
 __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg, long long jd0,
                                          const f2 (&ph)[8][2], f2 (&v)[8][2], const FuPrefetch& pf, f2 Sv,
-                                         f2& carry, float* __restrict__ phit, int svi, bool hi, float& tch) {
+                                         f2& carry, float* __restrict__ phit, int svi) {
   using G = fu::G;
   f2* __restrict__ U = T.U;
   const int l = T.l;
-  if constexpr ((ORION_WBFM_EXP & 32) != 0) set_prio(hi, true);
-  constexpr bool kOldHalo = (ORION_WBFM_EXP & 256) != 0;
-  if (kOldHalo && n > 0) {  // halo: entries TW .. TW+Q of every row -> 0 .. Q, times e^{-j theta NEW}
-#pragma unroll
-    for (int r2 = 0; r2 < 2; ++r2) {
-      const int e = l + 64 * r2;
-      if (e < 72) {
-        const int c = e / 9, h = e - 9 * c;
-        const int dst = c * g8::LRS + 2 * g8::pchunk(h);
-        const f4 w = *reinterpret_cast<const f4*>(U + dst + 2 * 80);  // pchunk(TW/2 + h) = 80 + pchunk(h)
-        const f2 y0 = cmul(f2{w.x, w.y}, T.corr), y1 = cmul(f2{w.z, w.w}, T.corr);
-        *reinterpret_cast<f4*>(U + dst) = f4{y0.x, y0.y, y1.x, y1.y};
-      }
-    }
-    lds_order();
-  }
   // Halo (n > 0): the previous tile's entries TW .. TW+Q of each row become entries
   // 0 .. Q, times e^{-j theta NEW}. Entries 0..15 of every row (lane l: row l & 7,
   // pair l >> 3: conflict-free b128 stores) and entry Q of rows 1..7 (lanes 0..6;
@@ -793,7 +759,7 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
   const int hc = l & 7, hh = l >> 3;
   f4 hw = f4{0, 0, 0, 0};
   f2 hq = f2{0, 0};
-  if (!kOldHalo && n > 0) {
+  if (n > 0) {
     hw = *reinterpret_cast<const f4*>(U + hc * g8::LRS + 2 * (80 + g8::pchunk(hh)));
     if (l < 7) hq = U[(l + 1) * g8::LRS + g8::slot(G::TW + Q)];
   }
@@ -805,7 +771,7 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
     if (k % 4 == 3) asm volatile("" ::: "memory");
   }
   asm volatile("" ::: "memory");
-  if (!kOldHalo && n > 0) {
+  if (n > 0) {
     const f2 y0 = cmul(f2{hw.x, hw.y}, T.corr), y1 = cmul(f2{hw.z, hw.w}, T.corr);
     *reinterpret_cast<f4*>(U + hc * g8::LRS + 2 * g8::pchunk(hh)) = f4{y0.x, y0.y, y1.x, y1.y};
     if (l < 7) U[(l + 1) * g8::LRS + g8::slot(Q)] = cmul(hq, T.corr);
@@ -813,14 +779,6 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
   // unconditional: a conditional prefetch makes the compiler's wait counting assume
   // the loads may be absent and drain them (vmcnt(0))
   front2_load<2, A16, CLAMP>(pf.xl, pf.nl, pf.porg, l, v);
-  if constexpr ((ORION_WBFM_EXP & 1024) != 0) {
-    // L2 touch of the tile after the prefetched one: one dword per 128-B line (64
-    // lanes = the tile's 8 KB). The previous touch's value is consumed here (an
-    // empty asm use), so the compiler counts it in vmcnt behind this tile's loads.
-    asm volatile("" ::"v"(tch));
-    const long long tp = min(max(pf.porg + G::NEW + 8 * Q + 16LL * l, 0LL), pf.nl - 1);
-    tch = reinterpret_cast<const float*>(pf.xl + tp)[0];
-  }
   if (bnd) {
     lds_order();
 #pragma unroll 1
@@ -835,7 +793,6 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
   lds_order();
   // group g: phases 2g, 2g+1; window entries 8l' .. 8l'+23 of the phase's row
   const int g = g8::group(l), lp = l & 15;
-  if constexpr ((ORION_WBFM_EXP & 96) != 0) set_prio(hi, (ORION_WBFM_EXP & 64) != 0);
   f2 d[8];
   // phase 2g opens the eight chains with a product (no zeroing), phase 2g+1 follows;
   // the compiler barrier keeps the second phase's reads behind the first's FMAs
@@ -843,7 +800,6 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
   g8::phase<true, true>(U, 2 * g, lp, T.Gt, d);
   asm volatile("" ::: "memory");
   g8::phase<false, true>(U, 2 * g + 1, lp, T.Gt, d);
-  if constexpr ((ORION_WBFM_EXP & 96) != 0) set_prio(hi, (ORION_WBFM_EXP & 32) != 0);
   // rows 0<->1, 2<->3: even rows keep outputs 0..3, odd rows 4..7 (x: d[i], y: d[i+4])
   f2 K[4];
 #pragma unroll
@@ -888,7 +844,6 @@ __device__ __forceinline__ void fu_tile8(const FuTile& T, int n, long long porg,
   *reinterpret_cast<f2*>(phit + j0) = f2{fm_disc_pk_rcp(F[0], pv, T.C.k), fm_disc_pk_rcp(F[1], F[0], T.C.k)};
   carry = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(F[1].x), 63)),
              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(F[1].y), 63))};
-  if constexpr ((ORION_WBFM_EXP & 32) != 0) set_prio(hi, false);
   const WbfmArgs& a = T.a;
   if (jd0 <= a.n_dec - 1 && a.n_dec - 1 < jd0 + G::TW) {  // carried state of the next call
     const int rl = static_cast<int>(a.n_dec - 1 - jd0);
@@ -1269,7 +1224,6 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
     const float* ci = a.carry_in + g.ch * kWbfmCarry;
     carry = f2{ci[4], ci[5]};
   }
-  float tch = 0.0f;             // L2 touch (experiment bit 1024)
   double sw[4] = {0, 0, 0, 0};  // IIR state entering the next sub-range
   float hist[2] = {0, 0};       // its FIR history
   // past the segment: a dummy read of the channel's first tile, shared by every
@@ -1293,14 +1247,14 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
     }
 #pragma unroll 1
     for (int tin = 0; tin < sg::NS; ++tin, ++n, porg += G::NEW) {
-      const bool hi = (16 * n < kSegPrioQ16 * ntiles) == late;
-      set_prio(hi, false);
+      if ((16 * n < kSegPrioQ16 * ntiles) == late) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
       if ((n & 63) == 0)  // lane l: the common phasor of tile n + l
         Sv = phasor_q64(static_cast<uint64_t>(a.k0 + porg + 1 + static_cast<long long>(l) * G::NEW),
                         a.step[g.ch]);
       const long long jd0 = g.A + static_cast<long long>(n) * TW;
       const FuPrefetch p0 = n + 1 < ntiles ? FuPrefetch{org.xl, org.nl, porg + G::NEW, true} : dummy;
-      fu_tile8<A16, CLAMP>(T, n, porg, jd0, ph, va, p0, Sv, carry, Phi + TW * tin, n & 63, hi, tch);
+      fu_tile8<A16, CLAMP>(T, n, porg, jd0, ph, va, p0, Sv, carry, Phi + TW * tin, n & 63);
     }
     lds_order();
     if (sub == 0) {
@@ -1348,574 +1302,6 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
   fu::trace(a, g.r, 2);
   sg::back(a, Bc, g.ch, g.A, min(sg::L, g.Lr), g.last && nsub == 1, Phi, P, l, sw, hist);
   fu::trace(a, g.r, 3);
-}
-
-// ---- paired chain: k_wbfm_pair --------------------------------------------------------
-// One 512-thread workgroup per CU = four A/B wave pairs. A workgroup's waves reach the
-// SIMDs in a fixed cyclic order, so waves w and w + 4 share a SIMD: each SIMD runs one
-// pair. A pair walks a segment of sub-ranges exactly as a k_wbfm_seg wave does, with
-// the work split by kind:
-//   wave A (w < 4): the input loads, the NCO mix and polyphase staging, the halo, the
-//     post-FIR chain (tile phasor, previous output, discriminator), the IIR (iir16 and
-//     the reference's f32 pass into the audio FIR's pair image) and every hand-off;
-//   wave B (w >= 4): the decimator's FMAs (both phases' windows read at once, its 32
-//     taps held in registers) and the audio FIR.
-// B's FMA blocks are VALU-bound while A's work is mostly latency (LDS and memory round
-// trips, dependent chains), so on one SIMD they overlap. Hand-offs go through LDS
-// counters, each with one writer: u_ready (A: tile n staged), u_free (B: tile n's
-// windows read), f_ready (B: tile n's two outputs per lane in F[n & 1]), f_free (A:
-// F[n & 1] read), p_ready (A: a sub-range's pair image written), p_free (B: its FIR
-// done). Tile images and F are double-buffered. A wave's LDS operations execute in
-// order, so a counter stored after the data orders the data for a reader that polls
-// the counter first, and a counter stored right after issuing reads (no wait for their
-// data) frees the buffer: the writer's later stores execute after those reads.
-namespace pr {
-constexpr int kPairs = 4;
-struct PairLds {
-  f2 U[2][g8::LDS_F2];    // tile images (tile n in U[n & 1])
-  f4 F[2][64];            // B -> A: F[0], F[1] of one tile per lane, double-buffered
-  f2 P[sg::Y::PSlots];    // the audio FIR's pair image (A writes, B reads)
-  float Phi[sg::L];       // a sub-range's discriminator outputs (A only)
-  f2 cacc;                // B -> A: the segment's carried output before the tile phasor
-  uint32_t flag[6];
-};
-enum { kUReady = 0, kUFree, kFReady, kFFree, kPReady, kPFree };
-
-__device__ __forceinline__ uint32_t ld_flag(const uint32_t* f) {  // wave-uniform (a scalar loop)
-  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-__device__ __forceinline__ void set_flag(uint32_t* f, uint32_t v) {
-  asm volatile("" ::: "memory");
-  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  asm volatile("" ::: "memory");
-}
-// Bounded wait for a counter >= v: a timeout sets the handle's error word and the
-// wave goes on (its outputs are then invalid, and the host reports the error).
-// Debug timing (a.trace): per-wave sums of the time spent in each kind of wait.
-struct Tr {
-  long long* p;  // this wave's 8 trace words, or null
-  __device__ __forceinline__ static long long now() { return static_cast<long long>(__builtin_amdgcn_s_memrealtime()); }
-  __device__ __forceinline__ void put(int i, long long v) const {
-    if (p && (threadIdx.x & 63) == 0) p[i] = v;
-  }
-};
-__device__ __forceinline__ void wait_flag(const uint32_t* f, uint32_t v, int* err, uint32_t spin,
-                                          const Tr* tr = nullptr, long long* acc = nullptr) {
-  const long long t0 = (tr && tr->p) ? Tr::now() : 0;
-  for (uint32_t it = 0; it < spin; ++it) {
-    if (ld_flag(f) >= v) {
-      asm volatile("" ::: "memory");
-      if (tr && tr->p) *acc += Tr::now() - t0;
-      return;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ long long hw_id() {
-  return static_cast<long long>(__builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11)));
-}
-
-// Segment of pair r (k_wbfm_seg's geometry).
-__device__ __forceinline__ FuRange range_of(const WbfmArgs& a, int r, int spc, int S) {
-  FuRange g;
-  g.r = r;
-  g.ch = r / spc;
-  g.wl = r - g.ch * spc;
-  g.A = static_cast<long long>(g.wl) * S;
-  g.B = min(g.A + S, a.n_dec);
-  g.Lr = static_cast<int>(g.B - g.A);
-  g.first = g.wl == 0;
-  g.last = g.B == a.n_dec;
-  return g;
-}
-
-// B: one phase's FMAs from registers (taps walked from q = Q-1 down).
-template <bool FIRST>
-__device__ __forceinline__ void b_phase(const f4 (&w)[12], const float (&t)[Q], f2 (&d)[8]) {
-#pragma unroll
-  for (int qi = 0; qi < Q; ++qi) {
-    const int q = Q - 1 - qi;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int m = r + Q - q;
-      const f4& wc = w[m >> 1];
-      const f2 xv = (m & 1) ? f2{wc.z, wc.w} : f2{wc.x, wc.y};
-      if (FIRST && qi == 0) d[r] = splat2(t[q]) * xv;
-      else d[r] = fma2(splat2(t[q]), xv, d[r]);
-    }
-  }
-}
-
-// A: the back of one sub-range up to the audio FIR (sg::back's IIR half): iir16 from
-// the exact entering state sw, the reference's f32 pass into the pair image P, the
-// history pairs; returns the end state in sw and the last 128 IIR outputs in hist.
-__device__ __forceinline__ void a_back(const WbfmArgs& a, const WbfmFusedConst& Bc, int ch, int Lr, bool chan_last,
-                                       const float* Phi, f2* P, int l, double (&sw)[4], float (&hist)[2],
-                                       int publish_r) {
-  using Y = sg::Y;
-  constexpr int CH = sg::CH, NH = Y::NH;
-  const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
-  f2 xs[CH];
-  f2 ef[4];
-  {
-    double send[4];
-    sg::iir16(Bc, Phi, l, sw, xs, ef, send);
-    const int jl = Lr - 1;
-    float cap[4] = {0, 0, 0, 0};
-    bool have = false;
-    int po = 2 * Y::pslot(16 * (l & 31) + fu::PB) + (l >> 5);
-    asm volatile("" : "+v"(po));
-    float* __restrict__ pe = reinterpret_cast<float*>(P) + po;
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int j = 16 * l + i;
-      const f2 f = bq.lp4(ef, xs[i]);
-      pe[2 * i] = f.x;
-      pe[2 * (i + CH + 1)] = f.y;
-      if (chan_last) {
-        if (j == jl) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) cap[k] = ef[k].x;
-          have = true;
-        }
-        if (j + 8 == jl) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) cap[k] = ef[k].y;
-          have = true;
-        }
-      }
-    }
-    if (have) {
-      float* co = a.carry_out + ch * kWbfmCarry;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) co[k] = cap[k];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      sw[k] = static_cast<double>(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(ef[k].y), 63)));
-  }
-  lds_order();
-#pragma unroll
-  for (int r2 = 0; r2 < 2; ++r2) {  // pairs j in [-128, 0): (history, f[j + NH])
-    const int t = l + 64 * r2;
-    P[Y::pslot(t)] = f2{hist[r2], P[Y::pslot(t + NH)].x};
-  }
-  lds_order();
-#pragma unroll
-  for (int r2 = 0; r2 < 2; ++r2) hist[r2] = P[Y::pslot(NH + l + 64 * r2)].y;
-  if (publish_r >= 0) sg::publish_end(a, publish_r, sw, hist, l);
-  if (chan_last) {  // the next call's FIR history: f[n_dec - 128 .. n_dec)
-#pragma unroll
-    for (int r2 = 0; r2 < 2; ++r2) {
-      const int t = l + 64 * r2;
-      const int j = Lr - 128 + t;
-      const float f = j < NH ? P[Y::pslot(j + fu::PB)].x : P[Y::pslot(j - NH + fu::PB)].y;
-      a.carry_out[ch * kWbfmCarry + 8 + t] = f;
-    }
-  }
-  lds_order();
-}
-
-// B: the audio FIR of one sub-range [A0, A0 + Lr) from the pair image (sg::back's FIR half).
-__device__ __forceinline__ void b_fir(const WbfmArgs& a, const WbfmFusedConst& Bc, int ch, long long A0, int Lr,
-                                      const f2* P, int l) {
-  constexpr int CH = sg::CH, NH = sg::Y::NH, KB = 16;
-  constexpr int O = fu::PB - (KB - 1);
-  f2 acc[CH];
-#pragma unroll
-  for (int i = 0; i < CH; ++i) acc[i] = f2{0.0f, 0.0f};
-  // windows ping-pong: block kb + 1's reads are in flight during block kb's FMAs
-  auto load = [&](f2 (&w)[CH + KB - 1], int kb) {
-    const f2* __restrict__ Pl = P + (CH + 1) * (l - KB * kb / CH) + O;
-#pragma unroll
-    for (int m = 0; m < CH + KB - 1; ++m) w[m] = Pl[m + (O + m) / CH];
-  };
-  auto fmas = [&](const f2 (&w)[CH + KB - 1], int kb) {
-#pragma unroll
-    for (int kk = 0; kk < KB; ++kk) {
-      const f2 tap = splat2(Bc.a[KB * kb + kk]);
-#pragma unroll
-      for (int i = 0; i < CH; ++i) acc[i] = fma2(tap, w[i + KB - 1 - kk], acc[i]);
-    }
-  };
-  f2 wa[CH + KB - 1], wb[CH + KB - 1];
-  load(wa, 0);
-#pragma unroll 1
-  for (int kb = 0; kb < 128 / KB; kb += 2) {
-    load(wb, kb + 1);
-    fmas(wa, kb);
-    if (kb + 2 < 128 / KB) load(wa, kb + 2);
-    fmas(wb, kb + 1);
-  }
-  float* __restrict__ y = a.y + ch * a.y_stride + A0;
-  if (Lr == sg::L && (reinterpret_cast<uintptr_t>(y) & 15) == 0) {
-    float4* ya = reinterpret_cast<float4*>(y + CH * l);
-    float4* yb = reinterpret_cast<float4*>(y + NH + CH * l);
-#pragma unroll
-    for (int i = 0; i < CH; i += 4) {
-      ya[i / 4] = float4{acc[i].x, acc[i + 1].x, acc[i + 2].x, acc[i + 3].x};
-      yb[i / 4] = float4{acc[i].y, acc[i + 1].y, acc[i + 2].y, acc[i + 3].y};
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int j = CH * l + i;
-      if (j < Lr) y[j] = acc[i].x;
-      if (j + NH < Lr) y[j + NH] = acc[i].y;
-    }
-  }
-}
-
-// ---- wave B ----
-__device__ __forceinline__ void pair_b(const WbfmArgs& a, const WbfmFrontConst& C, const WbfmFusedConst& Bc,
-                                       PairLds& L, const float* Gt, const FuRange& g, int l) {
-  const int nsub = (g.Lr + sg::L - 1) / sg::L;
-  const int ntiles = nsub * sg::NS;
-  const int grp = g8::group(l), lp = l & 15;
-  float t0[Q], t1[Q];
-#pragma unroll
-  for (int q4 = 0; q4 < Q / 4; ++q4) {
-    const f4 u0 = reinterpret_cast<const f4*>(Gt + 2 * grp * Q)[q4];
-    const f4 u1 = reinterpret_cast<const f4*>(Gt + (2 * grp + 1) * Q)[q4];
-    t0[4 * q4] = u0.x; t0[4 * q4 + 1] = u0.y; t0[4 * q4 + 2] = u0.z; t0[4 * q4 + 3] = u0.w;
-    t1[4 * q4] = u1.x; t1[4 * q4 + 1] = u1.y; t1[4 * q4 + 2] = u1.z; t1[4 * q4 + 3] = u1.w;
-  }
-  const int ro0 = 2 * grp * g8::LRS / 2 + 5 * lp, ro1 = (2 * grp + 1) * g8::LRS / 2 + 5 * lp;  // f4 offsets
-  int jobs = 0;  // audio FIR jobs done: sub-ranges 1 .. nsub-1 in order, then sub-range 0
-  const Tr tr{a.trace ? a.trace + static_cast<long long>(g.r) * kFuTracePoints + 8 : nullptr};
-  long long wu = 0, wf = 0, wp = 0, tfir = 0;
-  tr.put(0, Tr::now());
-  tr.put(7, hw_id());
-#pragma unroll 1
-  for (int n = 0; n < ntiles; ++n) {
-    wait_flag(&L.flag[kUReady], n + 1, a.err, a.spin, &tr, &wu);
-    const f2* __restrict__ Un = L.U[n & 1];
-    const f4* __restrict__ row0 = reinterpret_cast<const f4*>(Un) + ro0;
-    const f4* __restrict__ row1 = reinterpret_cast<const f4*>(Un) + ro1;
-    f4 w0[12], w1[12];
-#pragma unroll
-    for (int h = 0; h < 12; ++h) w0[h] = row0[5 * (h >> 2) + (h & 3)];
-#pragma unroll
-    for (int h = 0; h < 12; ++h) w1[h] = row1[5 * (h >> 2) + (h & 3)];
-    if (n == 0 && !g.first) {
-      // d[A-1], the previous segment's last output, from this tile's image (rows
-      // i = 0..15; A staged U[c][0], c >= 1): taps 2l, 2l+1 per lane, summed over the
-      // wave; A multiplies it by the tile phasor
-      f2 acc = f2{0.0f, 0.0f};
-#pragma unroll
-      for (int t2 = 0; t2 < 2; ++t2) {
-        const int k = 2 * l + t2, c = k & 7, q = k >> 3;
-        acc = fma2(splat2(Gt[c * Q + q]), Un[c * g8::LRS + g8::slot(15 - q)], acc);
-      }
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1)
-        acc += f2{__shfl_xor(acc.x, off, 64), __shfl_xor(acc.y, off, 64)};
-      L.cacc = acc;
-    }
-    set_flag(&L.flag[kUFree], n + 1);  // issued after the reads: the image is free
-    f2 d[8];
-    b_phase<true>(w0, t0, d);
-    b_phase<false>(w1, t1, d);
-    f2 K[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const auto sx = __builtin_amdgcn_permlane16_swap(__float_as_uint(d[i].x), __float_as_uint(d[i + 4].x), false, false);
-      const auto sy = __builtin_amdgcn_permlane16_swap(__float_as_uint(d[i].y), __float_as_uint(d[i + 4].y), false, false);
-      K[i] = f2{__uint_as_float(sx[0]), __uint_as_float(sy[0])} + f2{__uint_as_float(sx[1]), __uint_as_float(sy[1])};
-    }
-    f2 F[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const auto sx = __builtin_amdgcn_permlane32_swap(__float_as_uint(K[i].x), __float_as_uint(K[i + 2].x), false, false);
-      const auto sy = __builtin_amdgcn_permlane32_swap(__float_as_uint(K[i].y), __float_as_uint(K[i + 2].y), false, false);
-      F[i] = f2{__uint_as_float(sx[0]), __uint_as_float(sy[0])} + f2{__uint_as_float(sx[1]), __uint_as_float(sy[1])};
-    }
-    if (n >= 2) wait_flag(&L.flag[kFFree], n - 1, a.err, a.spin, &tr, &wf);  // A has read F[n & 1] of tile n - 2
-    L.F[n & 1][l] = f4{F[0].x, F[0].y, F[1].x, F[1].y};
-    set_flag(&L.flag[kFReady], n + 1);
-    // sub-range s's pair image is written by A once it has posted tile 8s + 7 (during
-    // its tile 8s + 8): take the FIR after tile 8s + 9
-    if (jobs < nsub - 2 && n == sg::NS * (jobs + 2) + 1) {
-      wait_flag(&L.flag[kPReady], jobs + 1, a.err, a.spin, &tr, &wp);
-      const long long A0 = g.A + static_cast<long long>(jobs + 1) * sg::L;
-      const long long t0 = tr.p ? Tr::now() : 0;
-      if constexpr ((ORION_WBFM_EXP & 131072) == 0)
-        b_fir(a, Bc, g.ch, A0, static_cast<int>(min(static_cast<long long>(sg::L), g.B - A0)), L.P, l);
-      lds_order();
-      if (tr.p) tfir += Tr::now() - t0;
-      ++jobs;
-      set_flag(&L.flag[kPFree], jobs);
-    }
-  }
-  tr.put(1, Tr::now());
-  // the remaining FIRs: the segment's later sub-ranges, then sub-range 0
-#pragma unroll 1
-  for (; jobs < nsub; ++jobs) {
-    wait_flag(&L.flag[kPReady], jobs + 1, a.err, a.spin, &tr, &wp);
-    const int s = jobs + 1 < nsub ? jobs + 1 : 0;
-    const long long A0 = g.A + static_cast<long long>(s) * sg::L;
-    b_fir(a, Bc, g.ch, A0, static_cast<int>(min(static_cast<long long>(sg::L), g.B - A0)), L.P, l);
-    lds_order();
-    set_flag(&L.flag[kPFree], jobs + 1);
-  }
-  tr.put(2, Tr::now());
-  tr.put(3, wu);
-  tr.put(4, wf);
-  tr.put(5, wp);
-  tr.put(6, tfir);
-}
-
-// ---- wave A ----
-template <bool A16, bool CLAMP>
-__device__ __forceinline__ void pair_a(const WbfmArgs& a, const WbfmFrontConst& C, const WbfmFusedConst& Bc,
-                                       PairLds& L, const FuRange& g, int l) {
-  using G = fu::G;
-  constexpr int TW = G::TW;
-  f2* __restrict__ U = L.U[0];
-  float* __restrict__ Phi = L.Phi;
-  const int nsub = (g.Lr + sg::L - 1) / sg::L;
-  const int ntiles = nsub * sg::NS;
-  uint32_t* const myslot = a.hand + static_cast<long long>(g.r) * sg::kSegSlot;
-  const FuPrefetch org = fu_origin(a, g);
-  f2 va[G::KL][2];
-  front2_load<2, A16, CLAMP>(org.xl, org.nl, org.porg, l, va);
-  const f2* __restrict__ tabc = a.tab + static_cast<long long>(g.ch) * kWbfmNS;
-  const f2* __restrict__ xc = a.x + g.ch * a.x_stride;
-  const f2* __restrict__ hc = a.hist_in + g.ch * kWbfmHist;
-  const f2 cn = tabc[G::NEW];
-  const f2 corr = f2{cn.x, -cn.y};
-  const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
-  const int s0 = c0 * g8::LRS + g8::slot((8 * Q + 2 * l + c0) / 8);
-  const int s1 = c1 * g8::LRS + g8::slot((8 * Q + 2 * l + 1 + c1) / 8);
-  long long porg = org.porg;
-  {  // halo rows of the first tile (clamped here, exact via the boundary fixup)
-    const long long P0 = porg + 2 * l;
-    const long long hi = (org.nl & ~1LL) - 2;
-    const long long Pc = P0 < 0 ? 0 : (P0 > hi ? hi : P0);
-    const f2 x0 = org.xl[Pc], x1 = org.xl[Pc + 1];
-    const f4 th = *reinterpret_cast<const f4*>(tabc + 2 * l);
-    U[c0 * g8::LRS + g8::slot((2 * l + c0) / 8)] = cmul_rot(x0, f2{th.x, th.y});
-    U[c1 * g8::LRS + g8::slot((2 * l + 1 + c1) / 8)] = cmul_rot(x1, f2{th.z, th.w});
-  }
-  {  // p = -l (row c = l, entry 0), l = 1..7: used only by d[A-1]
-    const long long Pm = max(porg - (l & 7), 0LL);
-    const f2 xm = xc[Pm];
-    const f2 tc = tabc[l & 7];
-    if (!g.first && l >= 1 && l < 8) U[l * g8::LRS] = cmul_rot(xm, f2{tc.x, -tc.y});
-  }
-  f2 ph[G::KL][2];  // per-lane staging phasors e^{j theta p}, p = 8Q + 2l + r + 128k
-  {
-    const f4 tv = *reinterpret_cast<const f4*>(tabc + 8 * Q + 2 * l);
-    const f2 tb0 = f2{tv.x, tv.y}, tb1 = f2{tv.z, tv.w};
-#pragma unroll
-    for (int k = 0; k < G::KL; ++k) {
-      const f2 ek = tabc[128 * k];
-      ph[k][0] = cmul(tb0, ek);
-      ph[k][1] = cmul(tb1, ek);
-    }
-  }
-  f2 Sv = f2{0, 0};
-  f2 carry = f2{0.0f, 0.0f};
-  if (g.first) {
-    const float* ci = a.carry_in + g.ch * kWbfmCarry;
-    carry = f2{ci[4], ci[5]};
-  }
-  double sw[4] = {0, 0, 0, 0};
-  float hist[2] = {0, 0};
-  int pjobs = 0;  // pair images written
-  const FuPrefetch dummy{org.xl, org.nl, -8LL * Q, true};
-  const int hc_ = l & 7, hh = l >> 3;
-  const Tr tr{a.trace ? a.trace + static_cast<long long>(g.r) * kFuTracePoints : nullptr};
-  long long wu = 0, wf = 0, wp = 0, tst = 0, tpo = 0, tii = 0;
-  tr.put(0, Tr::now());
-  tr.put(7, hw_id());
-
-  // post of tile m: tile phasor, previous output, discriminator -> Phi; at a
-  // sub-range's last tile, the sub-range's IIR
-  auto post = [&](int m) {
-    const long long porg_m = org.porg + static_cast<long long>(m) * G::NEW;
-    if ((m & 63) == 0)  // lane l: the common phasor of tile m + l
-      Sv = phasor_q64(static_cast<uint64_t>(a.k0 + porg_m + 1 + static_cast<long long>(l) * G::NEW), a.step[g.ch]);
-    wait_flag(&L.flag[kFReady], m + 1, a.err, a.spin, &tr, &wf);
-    if constexpr ((ORION_WBFM_EXP & 131072) != 0) {  // experiment: no post, no IIR
-      set_flag(&L.flag[kFFree], m + 1);
-      if (m % sg::NS == sg::NS - 1 && m / sg::NS > 0) {
-        wait_flag(&L.flag[kPFree], pjobs, a.err, a.spin, &tr, &wp);
-        set_flag(&L.flag[kPReady], ++pjobs);
-      }
-      return;
-    }
-    const long long tp0 = tr.p ? Tr::now() : 0;
-    const f4 fv = L.F[m & 1][l];
-    f2 cacc = f2{0, 0};
-    if (m == 0 && !g.first) cacc = L.cacc;
-    set_flag(&L.flag[kFFree], m + 1);
-    const int svi = m & 63;
-    const f2 S = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.x), svi)),
-                    __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Sv.y), svi))};
-    f2 F[2] = {cmul(f2{fv.x, fv.y}, S), cmul(f2{fv.z, fv.w}, S)};
-    if (m == 0 && !g.first) carry = cmul(cacc, S);
-    const int src = g8::prev_lane(l);
-    f2 pv = f2{__shfl(F[1].x, src, 64), __shfl(F[1].y, src, 64)};
-    if (l == 0) pv = carry;
-    const int j0 = g8::first_out(l);
-    float* phit = Phi + TW * (m % sg::NS);
-    *reinterpret_cast<f2*>(phit + j0) = f2{fm_disc_pk_rcp(F[0], pv, C.k), fm_disc_pk_rcp(F[1], F[0], C.k)};
-    carry = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(F[1].x), 63)),
-               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(F[1].y), 63))};
-    const long long jd0 = g.A + static_cast<long long>(m) * TW;
-    if (jd0 <= a.n_dec - 1 && a.n_dec - 1 < jd0 + TW) {  // carried state of the next call
-      const int rl = static_cast<int>(a.n_dec - 1 - jd0);
-      float* co = a.carry_out + g.ch * kWbfmCarry;
-#pragma unroll
-      for (int r = 0; r < 2; ++r)
-        if (j0 + r == rl) {
-          co[4] = F[r].x;
-          co[5] = F[r].y;
-          co[6] = 0.0f;
-          co[7] = 0.0f;
-        }
-#pragma unroll
-      for (int t2 = 0; t2 < kWbfmHist / 64; ++t2) {
-        const int t = l + 64 * t2;
-        a.hist_out[g.ch * kWbfmHist + t] = load_hist(xc, a.n, hc, kWbfmHist, a.n - kWbfmHist + t);
-      }
-    }
-    if (tr.p) tpo += Tr::now() - tp0;
-    if (m % sg::NS == sg::NS - 1) {  // sub-range s = m / 8 complete
-      lds_order();
-      const long long ti0 = tr.p ? Tr::now() : 0;
-      const int s = m / sg::NS;
-      if (s == 0) {
-        // keep sub-range 0's phi for the deferred back in the segment's global slot
-        f4* gs = reinterpret_cast<f4*>(myslot + kFuSlot);
-#pragma unroll
-        for (int i = 0; i < sg::L / 256; ++i) gs[l + 64 * i] = *reinterpret_cast<const f4*>(Phi + 4 * (l + 64 * i));
-        sg::zs_only16(Bc, Phi, Phi, l, sw, hist);
-        if (nsub == 1 && !g.last) sg::publish_end(a, g.r, sw, hist, l);
-      } else {
-        const long long A0 = g.A + static_cast<long long>(s) * sg::L;
-        const int Lr = static_cast<int>(min(static_cast<long long>(sg::L), g.B - A0));
-        const bool lastsub = s == nsub - 1;
-        wait_flag(&L.flag[kPFree], pjobs, a.err, a.spin, &tr, &wp);  // B is done with the previous image
-        a_back(a, Bc, g.ch, Lr, g.last && lastsub, Phi, L.P, l, sw, hist, lastsub && !g.last ? g.r : -1);
-        set_flag(&L.flag[kPReady], ++pjobs);
-      }
-      lds_order();
-      if (tr.p) tii += Tr::now() - ti0;
-    }
-  };
-
-#pragma unroll 1
-  for (int n = 0; n < ntiles; ++n, porg += G::NEW) {
-    U = L.U[n & 1];
-    f4 hw = f4{0, 0, 0, 0};
-    f2 hq = f2{0, 0};
-    if (n > 0) {
-      // the previous tile's entries TW .. TW+Q, from the other image (read-only: B may
-      // still be reading its windows); then wait until B has read tile n - 2 from this one
-      const f2* __restrict__ Uo = L.U[(n - 1) & 1];
-      hw = *reinterpret_cast<const f4*>(Uo + hc_ * g8::LRS + 2 * (80 + g8::pchunk(hh)));
-      if (l < 7) hq = Uo[(l + 1) * g8::LRS + g8::slot(G::TW + Q)];
-      if (n >= 2) wait_flag(&L.flag[kUFree], n - 1, a.err, a.spin, &tr, &wu);
-    }
-    const long long ts0 = tr.p ? Tr::now() : 0;
-    const bool bnd = porg < 0 || porg + 8LL * (G::TW + Q) > a.n;
-#pragma unroll
-    for (int k = 0; k < G::KL; ++k) {
-      if constexpr ((ORION_WBFM_EXP & 262144) != 0) {  // experiment: no staging stores
-        const f2 a0 = cmul_rot_pk(va[k][0], ph[k][0]), a1 = cmul_rot_pk(va[k][1], ph[k][1]);
-        asm volatile("" ::"v"(a0.x), "v"(a0.y), "v"(a1.x), "v"(a1.y));
-      } else {
-        U[s0 + 20 * k] = cmul_rot_pk(va[k][0], ph[k][0]);
-        U[s1 + 20 * k] = cmul_rot_pk(va[k][1], ph[k][1]);
-      }
-      if (k % 4 == 3) asm volatile("" ::: "memory");
-    }
-    asm volatile("" ::: "memory");
-    if (n > 0) {
-      const f2 y0 = cmul(f2{hw.x, hw.y}, corr), y1 = cmul(f2{hw.z, hw.w}, corr);
-      *reinterpret_cast<f4*>(U + hc_ * g8::LRS + 2 * g8::pchunk(hh)) = f4{y0.x, y0.y, y1.x, y1.y};
-      if (l < 7) U[(l + 1) * g8::LRS + g8::slot(Q)] = cmul(hq, corr);
-    }
-    const FuPrefetch p0 = n + 1 < ntiles ? FuPrefetch{org.xl, org.nl, porg + G::NEW, true} : dummy;
-    front2_load<2, A16, CLAMP>(p0.xl, p0.nl, p0.porg, l, va);
-    if (bnd) {
-      lds_order();
-#pragma unroll 1
-      for (int p = (n == 0 ? 0 : 8 * Q) + l; p < 8 * (G::TW + Q); p += 64) {
-        const long long Pp = porg + p;
-        if (!CLAMP || Pp < 0 || Pp >= a.n || p < 8 * Q) {
-          const int c = (-p) & 7;
-          U[c * g8::LRS + g8::slot((p + c) / 8)] = cmul_rot(load_hist(xc, a.n, hc, kWbfmHist, Pp), tabc[p]);
-        }
-      }
-    }
-    set_flag(&L.flag[kUReady], n + 1);
-    if (tr.p) tst += Tr::now() - ts0;
-    if (n > 0) post(n - 1);
-  }
-  post(ntiles - 1);
-  // ---- deferred: sub-range 0 from the predecessor's end state ----
-  {
-    const f4* gs = reinterpret_cast<const f4*>(myslot + kFuSlot);
-    f4 u[sg::L / 256];
-#pragma unroll
-    for (int i = 0; i < sg::L / 256; ++i) u[i] = __builtin_nontemporal_load(gs + l + 64 * i);
-#pragma unroll
-    for (int i = 0; i < sg::L / 256; ++i) *reinterpret_cast<f4*>(Phi + 4 * (l + 64 * i)) = u[i];
-  }
-  if (g.first || (ORION_WBFM_EXP & 131072) != 0) {
-    const float* __restrict__ ci = a.carry_in + g.ch * kWbfmCarry;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) sw[k] = ci[k];
-    hist[0] = ci[8 + l];
-    hist[1] = ci[8 + 64 + l];
-  } else {
-    fu::wait_for(a.flags + 3LL * (g.r - 1), a.epoch, a.err, a.spin);
-    const uint32_t* ps = a.hand + static_cast<long long>(g.r - 1) * sg::kSegSlot;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) sw[k] = sg::uni(fu::u2d(fu::ld_agent(ps + 2 + 2 * k), fu::ld_agent(ps + 3 + 2 * k)));
-    hist[0] = __uint_as_float(fu::ld_agent(ps + 16 + l));
-    hist[1] = __uint_as_float(fu::ld_agent(ps + 16 + 64 + l));
-  }
-  lds_order();
-  wait_flag(&L.flag[kPFree], pjobs, a.err, a.spin);
-  a_back(a, Bc, g.ch, min(sg::L, g.Lr), g.last && nsub == 1, Phi, L.P, l, sw, hist, -1);
-  set_flag(&L.flag[kPReady], ++pjobs);
-  tr.put(1, tst);
-  tr.put(2, tpo);
-  tr.put(3, wu);
-  tr.put(4, wf);
-  tr.put(5, wp);
-  tr.put(6, tii);
-}
-}  // namespace pr
-
-template <bool A16, bool CLAMP>
-__global__ __launch_bounds__(512, 1) void k_wbfm_pair(const WbfmArgs a, const WbfmFrontConst C,
-                                                      const WbfmFusedConst Bc, int spc, int S, int nseg) {
-  __shared__ pr::PairLds L[pr::kPairs];
-  __shared__ __attribute__((aligned(16))) float Gt[128];
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, p = w & 3;
-  if (threadIdx.x < 128) Gt[threadIdx.x] = C.g[threadIdx.x];
-  if (w < 4 && l < 6) L[p].flag[l] = 0;
-  __syncthreads();
-  int blk = blockIdx.x;
-  {  // XCD-contiguous runs of segments (k_wbfm_seg)
-    const int nb = static_cast<int>(gridDim.x);
-    if ((nb & 7) == 0) blk = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
-  }
-  const int r = blk * pr::kPairs + p;
-  if (r >= nseg) return;
-  const FuRange g = pr::range_of(a, r, spc, S);
-  if (w < 4) {
-    __builtin_amdgcn_s_setprio(1);
-    pr::pair_a<A16, CLAMP>(a, C, Bc, L[p], g, l);
-  } else {
-    pr::pair_b(a, C, Bc, L[p], Gt, g, l);
-  }
 }
 
 }  // namespace
@@ -1980,17 +1366,7 @@ void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFused
     ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     cap = std::max(1, per_cu) * std::max(1, ncu);
   }
-  constexpr bool kPair = (ORION_WBFM_EXP & 65536) != 0;
-  static int capp = 0;
-  if (kPair && capp == 0) {
-    int per_cu = 0, dev = 0, ncu = 0;
-    ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wbfm_pair<true, false>, 512, 0));
-    ORION_HIP(hipGetDevice(&dev));
-    ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    if (per_cu < 1) throw HipError("k_wbfm_pair does not fit a CU");
-    capp = per_cu * ncu * pr::kPairs;
-  }
-  const long long capx = max_segments > 0 ? std::min<long long>(max_segments, kPair ? capp : cap) : (kPair ? capp : cap);
+  const long long capx = max_segments > 0 ? std::min<long long>(max_segments, cap) : cap;
   const long long nsub_ch = (a.n_dec + kSgL - 1) / kSgL;
   long long spc = std::max<long long>(1, std::min<long long>(capx / nch, nsub_ch));
   const long long S = (nsub_ch + spc - 1) / spc * kSgL;
@@ -2000,18 +1376,6 @@ void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFused
   const bool a16 = (reinterpret_cast<uintptr_t>(a.x) % 16 == 0) && (a.x_stride % 2 == 0);
   const bool clamp = a.n < 2LL * Fw<2>::NEW;
   const int gi = static_cast<int>(grid), sp = static_cast<int>(spc), Si = static_cast<int>(S);
-  if constexpr (kPair) {
-    const int nbk = (gi + pr::kPairs - 1) / pr::kPairs;
-    if (clamp) {
-      if (a16) k_wbfm_pair<true, true><<<nbk, 512, 0, s>>>(a, f, b, sp, Si, gi);
-      else k_wbfm_pair<false, true><<<nbk, 512, 0, s>>>(a, f, b, sp, Si, gi);
-    } else {
-      if (a16) k_wbfm_pair<true, false><<<nbk, 512, 0, s>>>(a, f, b, sp, Si, gi);
-      else k_wbfm_pair<false, false><<<nbk, 512, 0, s>>>(a, f, b, sp, Si, gi);
-    }
-    ORION_LAUNCH_CHECK();
-    return;
-  }
   if (clamp) {
     if (a16) k_wbfm_seg<true, true><<<gi, 64, 0, s>>>(a, f, b, sp, Si);
     else k_wbfm_seg<false, true><<<gi, 64, 0, s>>>(a, f, b, sp, Si);
