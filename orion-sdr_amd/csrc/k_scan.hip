@@ -631,6 +631,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
   __syncthreads();  // lane 0 of wave w reads wave w - 1's last LP output (xprev0)
   }  // LP
+  if constexpr (!LP) __syncthreads();  // lane 0 of wave w reads wave w - 1's last staged sample (xprev0)
 
   // ---- DC blocker: zero-state lane pairs (r^k, y_k), block scan ----
   // x before the lane's first sample: lane 0 of chunk 0 takes the carried x1; lane 0 of a
