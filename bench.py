@@ -271,6 +271,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-max-samples", type=int, default=1 << 24)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--rest", type=float, default=0.0, help="idle seconds between input synthesis and the warm-up")
     ap.add_argument("--shard", default="stream", choices=["stream", "channels"],
                     help="C2 on several GPUs: one stream cut in time (with a halo), or a channel per GPU")
     args = ap.parse_args()
@@ -295,6 +296,8 @@ def main():
     out_dtype = torch.complex64 if args.config in ("c1", "c3") else torch.float32
     out = torch.empty(out_shape, dtype=out_dtype, device=dev)
     torch.cuda.synchronize(dev)
+    if args.rest > 0:
+        time.sleep(args.rest)
 
     def step():
         blk.process_device(x, out, stream.cuda_stream)
