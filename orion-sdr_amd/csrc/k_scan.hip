@@ -521,6 +521,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   __shared__ float sb[PADN];
   __shared__ double tot[4][S];
   __shared__ double dtot[4][2];
+  __shared__ float xlast[4];  // each wave's last element (the DC pass's x before the next wave)
   __shared__ double excl_sh;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int ch = static_cast<int>(blockIdx.x % nch);
@@ -629,15 +630,18 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   wave_order();  // (the wave's own inputs: read before they are overwritten, in order)
 #pragma unroll
   for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
-  __syncthreads();  // lane 0 of wave w reads wave w - 1's last LP output (xprev0)
+  wave_order();
   }  // LP
-  if constexpr (!LP) __syncthreads();  // lane 0 of wave w reads wave w - 1's last staged sample (xprev0)
 
   // ---- DC blocker: zero-state lane pairs (r^k, y_k), block scan ----
   // x before the lane's first sample: lane 0 of chunk 0 takes the carried x1; lane 0 of a
   // later chunk the sample before the chunk (with the LP4 that sample's position is a
-  // warm-up sample, which the DC pass skips)
-  float xprev0 = t * C == 0 ? ci[DX] : sb[posS<SC>(t * C - 1)];
+  // warm-up sample, which the DC pass skips). Lane 0 of wave w > 0 needs wave w - 1's last
+  // element: it runs its zero-state pass with x_prev = 0 and, after the totals barrier,
+  // corrects its pair (y_k shifts by x_prev r^k, so d by x_prev m / r, and every later
+  // lane's inclusive pair by x_prev mi / r; the wave's total likewise) — no barrier for it.
+  const bool xcross = wave > 0 && lane == 0;
+  float xprev0 = t * C == 0 ? ci[DX] : (xcross ? 0.0f : sb[posS<SC>(t * C - 1)]);
   if constexpr (!LP)
     if (t == 0 && c > 0) xprev0 = static_cast<const float*>(a.x)[ch * a.x_stride + base - 1];
   double m = 1.0, d = 0.0;
@@ -665,11 +669,22 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   if (lane == 63) {
     dtot[wave][0] = mi;
     dtot[wave][1] = di;
+    xlast[wave] = xs[C - 1];
   }
   __syncthreads();
+  constexpr int WR = 64 * SC;  // elements per wave
+  const double rd = static_cast<double>(r);
+  // the x_prev correction of wave w's pairs (lane 0 of a wave holds a valid sample iff
+  // the wave does: its first element is past the warm-up)
+  auto xcorr = [&](int w) -> double { return (w > 0 && w * WR < cnt) ? static_cast<double>(xlast[w - 1]) : 0.0; };
+  {
+    const double xw = xcorr(wave);
+    di -= xw * mi / rd;
+    if (xcross) xprev0 = static_cast<float>(xw);
+  }
   double wm = 1.0, wd = 0.0;  // pairs of the waves before this one
   for (int w = 0; w < wave; ++w) {
-    double m2 = dtot[w][0], d2 = dtot[w][1];
+    double m2 = dtot[w][0], d2 = dtot[w][1] - xcorr(w) * dtot[w][0] / rd;
     dc_combine(wm, wd, m2, d2);
     wm = m2;
     wd = d2;
@@ -677,7 +692,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   if (wave == 0) {  // chunk aggregate, look-back (one wave, 64 predecessors per step), prefix
     double bm = 1.0, bd = 0.0;
     for (int w = 0; w < 4; ++w) {
-      double m2 = dtot[w][0], d2 = dtot[w][1];
+      double m2 = dtot[w][0], d2 = dtot[w][1] - xcorr(w) * dtot[w][0] / rd;
       dc_combine(bm, bd, m2, d2);
       bm = m2;
       bd = d2;
