@@ -122,13 +122,14 @@ __device__ __forceinline__ float agc_walk(const typename Pol::In* __restrict__ x
   return env;
 }
 
-// One wave walks samples [s, e) in order from env (the re-runs of k_agc_fix and the
-// sequential path). The 64 lanes load 64 samples and form d and both candidate
-// (1 - a) * d products; the envelope chain itself is uniform across the wave
-// (d and the products read lane by lane into SGPRs: compare, two selects, one
-// multiply, one add per sample), then every lane forms its sample's output. Same
-// f32 ops and roundings as the reference's per-sample update.
-template <class Pol>
+// One wave walks samples [s, e) in order from env (the re-runs of k_agc_fix, the
+// sequential path and the long-warm-up chunks of k_agc_wave). The 64 lanes load 64
+// samples and form d and both candidate (1 - a) * d products; the envelope chain
+// itself is uniform across the wave (d and the products read lane by lane: compare,
+// two selects, one multiply, one add per sample), then every lane forms its
+// sample's output. Same f32 ops and roundings as the reference's per-sample
+// update. OUT = false: envelope only (a warm-up).
+template <class Pol, bool OUT = true>
 __device__ __forceinline__ float agc_wave_walk(const typename Pol::In* __restrict__ x,
                                                typename Pol::Out* __restrict__ y, long long s, long long e, float env,
                                                const Pol& P) {
@@ -150,7 +151,7 @@ __device__ __forceinline__ float agc_wave_walk(const typename Pol::In* __restric
         const float rj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pr), j));
         const bool up = P.up(xj, env);
         env = (up ? P.att : P.rel) * env + (up ? aj : rj);
-        mine = lane == j ? env : mine;
+        if constexpr (OUT) mine = lane == j ? env : mine;
       }
     } else {
       for (int j = 0; j < cnt; ++j) {
@@ -159,10 +160,12 @@ __device__ __forceinline__ float agc_wave_walk(const typename Pol::In* __restric
         const float rj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pr), j));
         const bool up = P.up(xj, env);
         env = (up ? P.att : P.rel) * env + (up ? aj : rj);
-        mine = lane == j ? env : mine;
+        if constexpr (OUT) mine = lane == j ? env : mine;
       }
     }
-    if (i < e) y[i] = P.out(cur, mine, i);
+    if constexpr (OUT) {
+      if (i < e) y[i] = P.out(cur, mine, i);
+    }
     cur = nxt;
   }
   return env;
@@ -200,6 +203,33 @@ __global__ __launch_bounds__(256) void k_agc(const void* __restrict__ in, void* 
   env = agc_walk<Pol, true>(x, y, b, e, env, P);
   ext[c] = env;
   if (e == n) env_out[0] = env;
+}
+
+// Pass 1 for long warm-ups (few chunks: a lane per chunk would leave the chip
+// idle and walk W samples with its own strided loads, ~110 ns per sample): one
+// wave per chunk, warm-up and chunk by the wave walk (coalesced, ~27 ns per
+// sample). Same ent / ext records as k_agc.
+template <class Pol>
+__global__ __launch_bounds__(64) void k_agc_wave(const void* __restrict__ in, void* __restrict__ out, long long n,
+                                                 long long L, long long W, Pol P, const float* __restrict__ env_in,
+                                                 float* __restrict__ env_out, float* __restrict__ ent,
+                                                 float* __restrict__ ext, long long* __restrict__ first_bad) {
+  const auto* x = static_cast<const typename Pol::In*>(in);
+  auto* y = static_cast<typename Pol::Out*>(out);
+  const long long c = blockIdx.x;
+  const long long b = c * L;
+  const bool lead = threadIdx.x == 0;
+  if (c == 0 && lead) first_bad[0] = (n + L - 1) / L;
+  const long long e = b + L < n ? b + L : n;
+  const long long s0 = b - W > 0 ? b - W : 0;
+  float env = s0 == 0 ? P.seed(env_in[0], P.drive(x[0])) : P.warm_seed(P.drive(x[s0]));
+  env = agc_wave_walk<Pol, false>(x, y, s0, b, env, P);
+  if (lead) ent[c] = env;
+  env = agc_wave_walk<Pol, true>(x, y, b, e, env, P);
+  if (lead) {
+    ext[c] = env;
+    if (e == n) env_out[0] = env;
+  }
 }
 
 // Pass 2: the first chunk whose entering envelope is not (bitwise) its
@@ -294,7 +324,12 @@ class EnvelopeRunner {
     float* ext = ent + chunks;
     const unsigned grid = static_cast<unsigned>((chunks + 255) / 256);
     const long long W = warm_ < 0 ? 0 : warm_;
-    hipLaunchKernelGGL(k_agc<Pol>, dim3(grid), dim3(256), 0, s, in, out, n, L, W, P, ein, eout, ent, ext, first_bad);
+    if (chunks <= kWaveChunks) {
+      hipLaunchKernelGGL(k_agc_wave<Pol>, dim3(static_cast<unsigned>(chunks)), dim3(64), 0, s, in, out, n, L, W, P, ein,
+                         eout, ent, ext, first_bad);
+    } else {
+      hipLaunchKernelGGL(k_agc<Pol>, dim3(grid), dim3(256), 0, s, in, out, n, L, W, P, ein, eout, ent, ext, first_bad);
+    }
     ORION_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_agc_check, dim3(static_cast<unsigned>((chunks - 1 + 255) / 256)), dim3(256), 0, s, ent, ext,
                        chunks, first_bad);
@@ -308,6 +343,8 @@ class EnvelopeRunner {
   }
 
  private:
+  // Up to this many chunks (four waves per SIMD), a wave per chunk (k_agc_wave).
+  static constexpr long long kWaveChunks = 4096;
   long long warm_ = 0;
   DevBuf env_;          // two floats: the carried envelope, ping-ponged per call
   DevBuf chunk_state_;  // first disagreeing chunk, then ent[chunks], ext[chunks]
