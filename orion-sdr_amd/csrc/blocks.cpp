@@ -229,11 +229,12 @@ class PmModBlock final : public Block {
 };
 
 // modulate/fm.rs:11-74. F32 audio -> C32 IQ; the running phase is carried on the
-// device (f64, reduced mod 2 pi) so consecutive calls chain without a host sync.
+// device (a Q0.64 turn count, exact mod 2 pi) so consecutive calls chain without a
+// host sync.
 class FmModBlock final : public Block {
  public:
   FmModBlock(float fs, float dev_hz, float rf_hz) : fs_(fs), dev_(dev_hz), osc_(oscillator(rf_hz, fs)) {
-    for (auto& c : carry_) c.resize(sizeof(double));
+    for (auto& c : carry_) c.resize(sizeof(uint64_t));
     const auto t = phasor_table(osc_.theta, static_cast<size_t>(fm_mod_rtab_len()));
     rtab_.upload(t.data(), t.size() * sizeof(float));
     reset();
@@ -258,16 +259,16 @@ class FmModBlock final : public Block {
         epoch_ = 1;
       }
       launch_fm_mod_sp(static_cast<const float*>(in), static_cast<f2*>(out), nn, kf, g_, rec_.as<uint32_t>(), epoch_,
-                       carry_[cur_].as<double>(), carry_[cur_ ^ 1].as<double>(), k_, osc_.step_q64, rtab_.as<f2>(),
-                       dev_err(), s);
+                       carry_[cur_].as<uint64_t>(), carry_[cur_ ^ 1].as<uint64_t>(), k_, osc_.step_q64,
+                       rtab_.as<f2>(), dev_err(), s);
       cur_ ^= 1;
       k_ += n;
       return {n, n};
     }
-    sums_.resize(static_cast<size_t>(fm_mod_chunks(static_cast<long long>(n))) * sizeof(double));
+    sums_.resize(static_cast<size_t>(fm_mod_chunks(static_cast<long long>(n))) * sizeof(uint64_t));
     launch_fm_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), kf, g_,
-                  sums_.as<double>(), carry_[cur_].as<double>(), carry_[cur_ ^ 1].as<double>(), k_, osc_.step_q64,
-                  rtab_.as<f2>(), s);
+                  sums_.as<uint64_t>(), carry_[cur_].as<uint64_t>(), carry_[cur_ ^ 1].as<uint64_t>(), k_,
+                  osc_.step_q64, rtab_.as<f2>(), s);
     cur_ ^= 1;
     k_ += n;
     return {n, n};

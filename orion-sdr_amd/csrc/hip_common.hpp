@@ -85,6 +85,46 @@ __device__ __forceinline__ f2 phasor_at(uint64_t ph) {
   return f2{__builtin_fmaf(-s, d, c), __builtin_fmaf(c, d, s)};
 }
 
+// f32 sin and cos, correctly rounded but for rare near-ties: the argument reduced by
+// pi/2 in f64 (two-part pi/2: exact enough for |x| < 2^20), then Taylor polynomials on
+// |r| <= pi/4 through r^15 / r^16 (truncation < 2^-45 relative), one rounding to f32.
+// The reference's f32 sin / cos / sin_cos (glibc's sinf / cosf, < 0.56 ulp) give the same
+// values but for rare near-ties, with no systematic difference (a phase that sums the
+// pairs' angles, FmPhaseAccumMod, must not drift). No Payne-Hanek path: the library
+// sincosf's is if-converted into every call (~180 VALU); this is ~30. |x| >= 2^20: the
+// library.
+__device__ __forceinline__ void sincos_cr(float x, float* s, float* c) {
+  if (!(fabsf(x) < 1048576.0f)) {
+    sincosf(x, s, c);
+    return;
+  }
+  const double d = x;
+  const double nq = rint(d * 0.63661977236758134);
+  const double r = __builtin_fma(-nq, 6.123233995736766e-17, __builtin_fma(-nq, 1.5707963267948966, d));
+  const double r2 = r * r;
+  double ps = -1.0 / 1307674368000.0;
+  ps = __builtin_fma(ps, r2, 1.0 / 6227020800.0);
+  ps = __builtin_fma(ps, r2, -1.0 / 39916800.0);
+  ps = __builtin_fma(ps, r2, 1.0 / 362880.0);
+  ps = __builtin_fma(ps, r2, -1.0 / 5040.0);
+  ps = __builtin_fma(ps, r2, 1.0 / 120.0);
+  ps = __builtin_fma(ps, r2, -1.0 / 6.0);
+  double pc = 1.0 / 20922789888000.0;
+  pc = __builtin_fma(pc, r2, -1.0 / 87178291200.0);
+  pc = __builtin_fma(pc, r2, 1.0 / 479001600.0);
+  pc = __builtin_fma(pc, r2, -1.0 / 3628800.0);
+  pc = __builtin_fma(pc, r2, 1.0 / 40320.0);
+  pc = __builtin_fma(pc, r2, -1.0 / 720.0);
+  pc = __builtin_fma(pc, r2, 1.0 / 24.0);
+  pc = __builtin_fma(pc, r2, -0.5);
+  const float sr = static_cast<float>(__builtin_fma(ps * r2, r, r));
+  const float cr = static_cast<float>(__builtin_fma(pc, r2, 1.0));
+  const int q = static_cast<int>(static_cast<long long>(nq) & 3);
+  const float s0 = (q & 1) ? cr : sr, c0 = (q & 1) ? sr : cr;
+  *s = (q & 2) ? -s0 : s0;
+  *c = ((q + 1) & 2) ? -c0 : c0;
+}
+
 // util.rs:305-322 atan2_approx, restated op for op (no contraction: this TU is
 // built with -ffp-contract=off, and the division is IEEE).
 __device__ __forceinline__ float atan2_approx(float y, float x) {

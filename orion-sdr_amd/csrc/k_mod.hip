@@ -44,7 +44,9 @@ __global__ __launch_bounds__(NT) void k_pm_mod(const float* __restrict__ x, f2* 
   for (long long i = blockIdx.x * static_cast<long long>(NT) + threadIdx.x; i < n;
        i += static_cast<long long>(gridDim.x) * NT) {
     const float phi = kp * x[i];
-    const float br = cosf(phi) * g, bi = sinf(phi) * g;
+    float sn, cs;
+    sincos_cr(phi, &sn, &cs);  // pm.rs:44 (phi.cos(), phi.sin())
+    const float br = cs * g, bi = sn * g;
     const f2 r = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
     y[i] = f2{br * r.x - bi * r.y, br * r.y + bi * r.x};
   }
@@ -73,212 +75,235 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_back(const float* __restrict__ v
   }
 }
 
-// ---- FmPhaseAccumMod: phi_i = phi_carry + sum_{j <= i} inc_j (f64), z = e^{j phi} ----
-// fm.rs:48-56 multiplies the running phasor by (cos dphi, sin dphi) rounded to
-// f32, dphi = kf x_i, renormalising every 1024 samples. The angle of that f32
-// pair, not dphi itself, is what the recurrence adds per sample, and its bias
-// is systematic (it drifted 1.2e-2 rad from the exact sum over 2^20 samples of
-// the C2 input): so the increment is atan2 of the same f32 pair, summed in f64.
-// What remains is the recurrence's own multiply rounding (a random walk) and
-// sincosf/sin_cos last-bit differences.
-// For |dphi| < 1/8 (every WBFM-rate deviation): dphi plus the angle between the
-// f32 pair and the exact (C, S) = (cos, sin) dphi, the latter from f64 Taylor
-// series (truncation < 1e-21), the former to first order (it is < 1e-7 rad).
-__device__ __forceinline__ double fm_inc(float kf, float x) {
-  const float dphi = kf * x;  // fm.rs:50
-  float s, c;
-  sincosf(dphi, &s, &c);  // fm.rs:51
-  const double d = dphi;
-  if (fabs(d) < 0.125) {
-    const double q = d * d;
-    const double S = d * (1.0 - q * (1.0 / 6) * (1.0 - q * (1.0 / 20) * (1.0 - q * (1.0 / 42) *
-                     (1.0 - q * (1.0 / 72) * (1.0 - q * (1.0 / 110))))));
-    const double C = 1.0 - q * 0.5 * (1.0 - q * (1.0 / 12) * (1.0 - q * (1.0 / 30) * (1.0 - q * (1.0 / 56) *
-                     (1.0 - q * (1.0 / 90) * (1.0 - q * (1.0 / 132))))));
-    // sin of the angle between them; |(c, s)| = 1 +- 1e-7, so dividing by their
-    // cosine (1 +- 1e-7) would change the ~1e-8 result by ~1e-15
-    return d + (static_cast<double>(s) * C - static_cast<double>(c) * S);
-  }
-  return atan2(static_cast<double>(s), static_cast<double>(c));
-}
+// ---- FmPhaseAccumMod (fm.rs:45-74) ----------------------------------------------------
+// The reference multiplies a running phasor z by the f32 pair (dc, ds) = sin_cos(kf x)
+// per sample (renormalising |z| every 1024 samples). The angle of that f32 pair, not
+// kf x itself, is what it adds, and the difference is systematic (1.2e-2 rad over 2^20
+// samples of the C2 input), so the phase must sum the pairs' own angles. Here:
+//   * thread t owns 16 consecutive samples; it forms their pairs, their product in f64
+//     and one f64 atan2 of that product: the sum of the 16 angles mod 2 pi, exact to
+//     ~1e-16 rad, as a Q0.64 turn count (wrapping uint64);
+//   * phases are sums of those counts — exact integer arithmetic, associative, so the
+//     prefix over threads, waves and chunks (decoupled look-back) is bit-reproducible
+//     in any order and never drifts, and the carried phase is exact mod 2 pi;
+//   * the thread's outputs: the phasor of its entering phase (phasor_at), then the
+//     reference's own recurrence z = z (dc, ds) (fm.rs:53-54, its op order) over its
+//     16 pairs; base = z gain (fm.rs:66); mix_with_nco's non-FMA product with the
+//     closed-form RF phasor (nco.rs:62-66).
+// Against an f64 phase and a per-sample sincosf of it this is ~3x less VALU per sample.
+constexpr double kTurnsPerRad = 2.9358905032820014e18;  // 2^64 / (2 pi)
 
-// Pass 1: the f64 sum of each chunk's phase increments.
-__global__ __launch_bounds__(NT) void k_fm_mod_sum(const float* __restrict__ x, long long n, float kf,
-                                                   double* __restrict__ sums) {
-  __shared__ double part[NT / 64];
-  const long long base = static_cast<long long>(blockIdx.x) * kFmCH;
-  double s = 0.0;
+struct FmPairs {
+  float c[kFmC], s[kFmC];
+};
+// The thread's pairs (fm.rs:50-51) and the Q0.64 sum of their angles; samples past n
+// (valid < kFmC) are pairs (1, 0).
+__device__ __forceinline__ uint64_t fm_pairs(float kf, const float* __restrict__ xs, int valid, FmPairs& p) {
+  double pr = 1.0, pi = 0.0;
 #pragma unroll
   for (int k = 0; k < kFmC; ++k) {
-    const long long i = base + threadIdx.x + static_cast<long long>(k) * NT;
-    if (i < n) s += fm_inc(kf, x[i]);
+    float sn = 0.0f, cs = 1.0f;
+    if (k < valid) sincos_cr(kf * xs[k], &sn, &cs);  // fm.rs:50-51
+    p.c[k] = cs;
+    p.s[k] = sn;
+    const double c = cs, s = sn;
+    const double nr = __builtin_fma(pr, c, -pi * s);
+    pi = __builtin_fma(pr, s, pi * c);
+    pr = nr;
   }
+  const double th = atan2(pi, pr);  // in [-pi, pi]: the 16 angles' sum mod 2 pi
+  // (half turns' count doubled: th = +-pi would overflow an int64 of 2^-64 turns)
+  return static_cast<uint64_t>(static_cast<long long>(rint(th * kTurnsPerRad * 0.5))) * 2u;
+}
+
+// Outputs of the chunk: thread t's samples i0 .. i0 + 15 (i0 = base + 16 t) from its
+// entering phase ph, stored coalesced through LDS in two passes of 8 per thread (each
+// thread owning 16 consecutive samples would store 64 lanes x 8 B at a 128-B stride per
+// instruction). ys: kFmYs f2 slots (pass h: thread t's 8 at 8 t + pad, one pad per 16:
+// conflict-free b64 stores), aliasing the input staging: every thread is past its
+// reads of it (the caller's barrier). Pass h covers the chunk's samples 16 t' + 8 h + j.
+constexpr int kFmYs = (kFmCH + kFmCH / 16) / 2;  // f2 slots (= the input staging's floats / 2)
+__device__ __forceinline__ void fm_out(const FmPairs& p, uint64_t ph, float gain, f2 R0, const f2* __restrict__ rtab,
+                                       f2* ys, f2* __restrict__ y, long long base, long long n) {
+  f2 z = phasor_at(ph);
+  const int t = threadIdx.x;
+  const bool full = base + kFmCH <= n;
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int w = 0; w < NT / 64; ++w) t += part[w];
-    sums[blockIdx.x] = t;
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * h + j;
+      // fm.rs:53-54: zr = z.re.mul_add(dc, -z.im*ds); zi = z.im.mul_add(dc, z.re*ds)
+      z = f2{__builtin_fmaf(z.x, p.c[k], -(z.y * p.s[k])), __builtin_fmaf(z.y, p.c[k], z.x * p.s[k])};
+      const f2 bz = f2{z.x * gain, z.y * gain};  // fm.rs:66 base = z * gain
+      const f2 r = cmul(R0, rtab[k]);
+      const int e = 8 * t + j;
+      ys[e + (e >> 4)] = f2{bz.x * r.x - bz.y * r.y, bz.x * r.y + bz.y * r.x};  // nco.rs:65 (no FMA)
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int e = t + NT * m;
+      const long long i = base + 16 * (e >> 3) + 8 * h + (e & 7);
+      if (full || i < n) y[i] = ys[e + (e >> 4)];
+    }
+    __syncthreads();
   }
 }
 
-// Pass 2 (one workgroup): exclusive prefix of the chunk sums from the carried
-// phase (each thread a run of consecutive chunks, one workgroup scan of the run
-// totals); the carried phase of the next call (reduced mod 2 pi).
-__global__ __launch_bounds__(NT) void k_fm_mod_carry(double* __restrict__ sums, int nchunk,
-                                                     const double* __restrict__ carry_in,
-                                                     double* __restrict__ carry_out) {
-  __shared__ double tot[NT / 64];
+// Exclusive / inclusive prefix of a uint64 over the workgroup (4 waves); tot: 4 slots.
+__device__ __forceinline__ uint64_t u64_up(uint64_t v, int d) {
+  const uint32_t lo = __shfl_up(static_cast<uint32_t>(v), d, 64), hi = __shfl_up(static_cast<uint32_t>(v >> 32), d, 64);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wg_scan_u64(uint64_t v, uint64_t* tot, uint64_t& total) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int per = (nchunk + NT - 1) / NT;
-  const int c0 = min(nchunk, t * per), c1 = min(nchunk, c0 + per);
-  double run = 0.0;
-  for (int c = c0; c < c1; ++c) run += sums[c];
-  double inc = run;
+  uint64_t inc = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const double o = __shfl_up(inc, d, 64);
+    const uint64_t o = u64_up(inc, d);
     if (lane >= d) inc += o;
   }
   if (lane == 63) tot[w] = inc;
   __syncthreads();
-  double before = carry_in[0] + inc - run;
-  for (int k = 0; k < w; ++k) before += tot[k];
+  uint64_t before = inc - v;
+  total = 0;
+#pragma unroll
+  for (int k = 0; k < NT / 64; ++k) {
+    if (k < w) before += tot[k];
+    total += tot[k];
+  }
+  return before;
+}
+
+// Coalesced load of the chunk into LDS; thread t then reads its 16 consecutive samples.
+// The loads are unconditional (index clamped to n - 1, n >= 1): all 16 in flight at
+// once. A guarded load per sample compiles to a branch around each, and each then
+// waits for its own load before the LDS store (16 serial memory latencies per chunk).
+__device__ __forceinline__ int fm_stage(const float* __restrict__ x, long long n, long long base, float* xs) {
+  float v[kFmC];
+#pragma unroll
+  for (int k = 0; k < kFmC; ++k) v[k] = x[min(base + threadIdx.x + k * NT, n - 1)];
+#pragma unroll
+  for (int k = 0; k < kFmC; ++k) {
+    const int e = threadIdx.x + k * NT;
+    xs[e + (e >> 4)] = base + e < n ? v[k] : 0.0f;
+  }
+  __syncthreads();
+  const long long i0 = base + static_cast<long long>(threadIdx.x) * kFmC;
+  return static_cast<int>(max(0LL, min(static_cast<long long>(kFmC), n - i0)));
+}
+
+// Three-pass form (orion_block_configure MOD_PASSES 3). Pass 1: each chunk's Q0.64 sum.
+__global__ __launch_bounds__(NT) void k_fm_mod_sum(const float* __restrict__ x, long long n, float kf,
+                                                   uint64_t* __restrict__ sums) {
+  __shared__ uint64_t tot[NT / 64];
+  __shared__ float xs[kFmCH + kFmCH / 16];
+  const long long base = static_cast<long long>(blockIdx.x) * kFmCH;
+  const int valid = fm_stage(x, n, base, xs);
+  FmPairs p;
+  const int e = threadIdx.x * kFmC;
+  const uint64_t q = fm_pairs(kf, xs + e + (e >> 4), valid, p);
+  uint64_t total;
+  (void)wg_scan_u64(q, tot, total);
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+// Pass 2 (one workgroup): exclusive prefix of the chunk sums from the carried phase;
+// the carried phase of the next call.
+__global__ __launch_bounds__(NT) void k_fm_mod_carry(uint64_t* __restrict__ sums, int nchunk,
+                                                     const uint64_t* __restrict__ carry_in,
+                                                     uint64_t* __restrict__ carry_out) {
+  __shared__ uint64_t tot[NT / 64];
+  const int t = threadIdx.x;
+  const int per = (nchunk + NT - 1) / NT;
+  const int c0 = min(nchunk, t * per), c1 = min(nchunk, c0 + per);
+  uint64_t run = 0;
+  for (int c = c0; c < c1; ++c) run += sums[c];
+  uint64_t total;
+  uint64_t before = carry_in[0] + wg_scan_u64(run, tot, total);
   for (int c = c0; c < c1; ++c) {
-    const double v = sums[c];
+    const uint64_t v = sums[c];
     sums[c] = before;
     before += v;
   }
-  if (t == NT - 1) carry_out[0] = before - 6.283185307179586 * rint(before * 0.15915494309189535);
+  if (t == 0) carry_out[0] = carry_in[0] + total;
 }
 
-// Pass 3: per chunk, the inclusive prefix of the increments (thread-local runs,
-// then a workgroup scan of the run totals), z = e^{j phi} * gain, and
-// mix_with_nco's non-FMA complex product with the RF phasor (nco.rs:62-66).
+// Pass 3: the block scan of the thread sums from the chunk's entering phase, outputs.
 __global__ __launch_bounds__(NT) void k_fm_mod_apply(const float* __restrict__ x, f2* __restrict__ y, long long n,
-                                                     float kf, float gain, const double* __restrict__ offs,
+                                                     float kf, float gain, const uint64_t* __restrict__ offs,
                                                      uint64_t k0, uint64_t step, const f2* __restrict__ rtab) {
-  __shared__ double tot[NT / 64];
-  __shared__ float xs[kFmCH + kFmCH / 16];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  __shared__ uint64_t tot[NT / 64];
+  __shared__ __attribute__((aligned(16))) f2 ys[kFmYs];  // the input staging, then the outputs
+  float* xs = reinterpret_cast<float*>(ys);
+  static_assert(2 * kFmYs >= kFmCH + kFmCH / 16, "staging fits");
   const long long base = static_cast<long long>(blockIdx.x) * kFmCH;
-  // coalesced load, then each thread owns kFmC consecutive samples
-  for (int k = 0; k < kFmC; ++k) {
-    const int e = t + k * NT;
-    const long long i = base + e;
-    xs[e + (e >> 4)] = i < n ? x[i] : 0.0f;
-  }
-  __syncthreads();
-  double d[kFmC];
-  double run = 0.0;
-#pragma unroll
-  for (int k = 0; k < kFmC; ++k) {
-    const int e = t * kFmC + k;
-    d[k] = fm_inc(kf, xs[e + (e >> 4)]);
-    run += d[k];
-  }
-  double inc = run;
-#pragma unroll
-  for (int dd = 1; dd < 64; dd <<= 1) {
-    const double o = __shfl_up(inc, dd, 64);
-    if (lane >= dd) inc += o;
-  }
-  if (lane == 63) tot[w] = inc;
-  __syncthreads();
-  double phi = offs[blockIdx.x] + inc - run;
-  for (int k = 0; k < w; ++k) phi += tot[k];
-  // RF phasor of sample i0 + k = (phasor of i0) x e^{j theta k} (rtab: k < kFmC)
-  const long long i0 = base + t * kFmC;
-  const f2 R0 = phasor_q64(k0 + static_cast<uint64_t>(i0) + 1, step);
-#pragma unroll
-  for (int k = 0; k < kFmC; ++k) {
-    const long long i = i0 + k;
-    phi += d[k];
-    if (i < n) {
-      const double red = phi - 6.283185307179586 * rint(phi * 0.15915494309189535);
-      float s, c;
-      sincosf(static_cast<float>(red), &s, &c);
-      const f2 b = f2{c * gain, s * gain};  // fm.rs:66 base = z * gain
-      const f2 r = cmul(R0, rtab[k]);
-      y[i] = f2{b.x * r.x - b.y * r.y, b.x * r.y + b.y * r.x};  // nco.rs:65 (no FMA)
-    }
-  }
+  const int valid = fm_stage(x, n, base, xs);
+  FmPairs p;
+  const int e = threadIdx.x * kFmC;
+  const uint64_t q = fm_pairs(kf, xs + e + (e >> 4), valid, p);
+  uint64_t total;
+  const uint64_t ph = offs[blockIdx.x] + wg_scan_u64(q, tot, total);  // (its barrier: xs is dead)
+  const long long i0 = base + e;
+  const f2 R0 = phasor_q64(k0 + static_cast<uint64_t>(i0) + 1, step);  // RF phasor of i0 + k = R0 rtab[k]
+  fm_out(p, ph, gain, R0, rtab, ys, y, base, n);
 }
 
-// Single pass (default; the three passes above stay behind ORION_FM_MOD_3P=1): each
-// chunk computes its increments once, publishes its f64 aggregate, and takes the
-// phase entering it by decoupled look-back over its predecessors (wave 0: lane i
-// looks at chunk c-1-i; the nearest chunk with a published inclusive prefix, or the
-// carried phase before chunk 0, closes the sum), then publishes its own inclusive
-// prefix. Chunk-major grid: every predecessor was dispatched earlier and publishes
-// its aggregate before it waits, so the walk always ends. Records: 8 u32 per chunk,
-// [0, 2) aggregate, [2, 4) inclusive prefix (f64), 6 / 7 their flags (launch epoch).
+// Single pass (default): each chunk publishes its Q0.64 sum, takes the phase entering
+// it by decoupled look-back over its predecessors (wave 0: lane i looks at chunk
+// c-1-i; the nearest chunk with a published inclusive prefix, or the carried phase
+// before chunk 0, closes the sum), then publishes its inclusive prefix. Integer sums:
+// the result does not depend on which records the walk found. Chunk-major grid: every
+// predecessor was dispatched earlier and publishes its sum before it waits, so the
+// walk always ends. Records: 8 u32 per chunk, [0, 2) sum, [2, 4) inclusive prefix,
+// 6 / 7 their flags (launch epoch).
 __device__ __forceinline__ void fm_st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint32_t fm_ld(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void fm_st64(uint32_t* p, double v) {
-  const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
-  fm_st(p, static_cast<uint32_t>(b));
-  fm_st(p + 1, static_cast<uint32_t>(b >> 32));
+__device__ __forceinline__ void fm_st64(uint32_t* p, uint64_t v) {
+  fm_st(p, static_cast<uint32_t>(v));
+  fm_st(p + 1, static_cast<uint32_t>(v >> 32));
 }
-__device__ __forceinline__ double fm_ld64(const uint32_t* p) {
-  const unsigned long long lo = fm_ld(p), hi = fm_ld(p + 1);
-  return __longlong_as_double(static_cast<long long>((hi << 32) | lo));
+__device__ __forceinline__ uint64_t fm_ld64(const uint32_t* p) {
+  return (static_cast<uint64_t>(fm_ld(p + 1)) << 32) | fm_ld(p);
 }
 
 __global__ __launch_bounds__(NT) void k_fm_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
                                                   float kf, float gain, uint32_t* __restrict__ rec, uint32_t epoch,
-                                                  const double* __restrict__ carry_in, double* __restrict__ carry_out,
+                                                  const uint64_t* __restrict__ carry_in, uint64_t* __restrict__ carry_out,
                                                   uint64_t k0, uint64_t step, const f2* __restrict__ rtab,
                                                   int* __restrict__ err, uint32_t spin) {
-  __shared__ double tot[NT / 64];
-  __shared__ double excl_sh;
-  __shared__ float xs[kFmCH + kFmCH / 16];
+  __shared__ uint64_t tot[NT / 64];
+  __shared__ uint64_t excl_sh;
+  __shared__ __attribute__((aligned(16))) f2 ys[kFmYs];  // the input staging, then the outputs
+  float* xs = reinterpret_cast<float*>(ys);
+  static_assert(2 * kFmYs >= kFmCH + kFmCH / 16, "staging fits");
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int c = static_cast<int>(blockIdx.x);
   const int nchunk = static_cast<int>((n + kFmCH - 1) / kFmCH);
   const bool last = c == nchunk - 1;
   const long long base = static_cast<long long>(c) * kFmCH;
-  for (int k = 0; k < kFmC; ++k) {
-    const int e = t + k * NT;
-    const long long i = base + e;
-    xs[e + (e >> 4)] = i < n ? x[i] : 0.0f;
-  }
-  __syncthreads();
-  double d[kFmC];
-  double run = 0.0;
-#pragma unroll
-  for (int k = 0; k < kFmC; ++k) {
-    const int e = t * kFmC + k;
-    d[k] = base + e < n ? fm_inc(kf, xs[e + (e >> 4)]) : 0.0;
-    run += d[k];
-  }
-  double inc = run;
-#pragma unroll
-  for (int dd = 1; dd < 64; dd <<= 1) {
-    const double o = __shfl_up(inc, dd, 64);
-    if (lane >= dd) inc += o;
-  }
-  if (lane == 63) tot[w] = inc;
-  __syncthreads();
+  const int valid = fm_stage(x, n, base, xs);
+  FmPairs p;
+  const int e = t * kFmC;
+  const uint64_t q = fm_pairs(kf, xs + e + (e >> 4), valid, p);
+  uint64_t agg;
+  const uint64_t before = wg_scan_u64(q, tot, agg);
   if (w == 0) {
-    double agg = 0.0;
-    for (int v = 0; v < NT / 64; ++v) agg += tot[v];
     uint32_t* my = rec + static_cast<long long>(c) * 8;
     if (!last) {
       if (lane == 0) fm_st64(my, agg);
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the aggregate is visible before its flag
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the sum is visible before its flag
       if (lane == 0) fm_st(my + 6, epoch);
     }
-    double excl = 0.0;
+    uint64_t excl = 0;
     for (int b = c - 1;; b -= 64) {
       const int k = b - lane;
-      double v = 0.0;
+      uint64_t v = 0;
       bool closes = true;
       if (k >= 0) {
         const uint32_t* pr = rec + static_cast<long long>(k) * 8;
@@ -291,13 +316,17 @@ __global__ __launch_bounds__(NT) void k_fm_mod_sp(const float* __restrict__ x, f
         closes = fm_ld(pr + 7) == epoch;
         v = closes ? fm_ld64(pr + 2) : fm_ld64(pr);
       } else {
-        v = k == -1 ? carry_in[0] : 0.0;  // the carried phase before chunk 0
+        v = k == -1 ? carry_in[0] : 0;  // the carried phase before chunk 0
       }
       const unsigned long long bal = __ballot(closes);
       const int first = bal ? __builtin_ctzll(bal) : 64;
-      double term = lane <= first ? v : 0.0;
+      uint64_t term = lane <= first ? v : 0;
 #pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) term += __shfl_xor(term, off, 64);
+      for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t lo = __shfl_xor(static_cast<uint32_t>(term), off, 64);
+        const uint32_t hi = __shfl_xor(static_cast<uint32_t>(term >> 32), off, 64);
+        term += (static_cast<uint64_t>(hi) << 32) | lo;
+      }
       excl += term;
       if (first < 64) break;
     }
@@ -307,30 +336,15 @@ __global__ __launch_bounds__(NT) void k_fm_mod_sp(const float* __restrict__ x, f
         __builtin_amdgcn_s_waitcnt(0x0F70);
         fm_st(my + 7, epoch);
       } else {
-        const double end = excl + agg;  // the carried phase of the next call (reduced mod 2 pi)
-        carry_out[0] = end - 6.283185307179586 * rint(end * 0.15915494309189535);
+        carry_out[0] = excl + agg;  // the carried phase of the next call (exact mod 2 pi)
       }
       excl_sh = excl;
     }
   }
   __syncthreads();
-  double phi = excl_sh + inc - run;
-  for (int k = 0; k < w; ++k) phi += tot[k];
-  const long long i0 = base + t * kFmC;
+  const long long i0 = base + e;
   const f2 R0 = phasor_q64(k0 + static_cast<uint64_t>(i0) + 1, step);
-#pragma unroll
-  for (int k = 0; k < kFmC; ++k) {
-    const long long i = i0 + k;
-    phi += d[k];
-    if (i < n) {
-      const double red = phi - 6.283185307179586 * rint(phi * 0.15915494309189535);
-      float sn, cs;
-      sincosf(static_cast<float>(red), &sn, &cs);
-      const f2 bz = f2{cs * gain, sn * gain};  // fm.rs:66 base = z * gain
-      const f2 r = cmul(R0, rtab[k]);
-      y[i] = f2{bz.x * r.x - bz.y * r.y, bz.x * r.y + bz.y * r.x};  // nco.rs:65 (no FMA)
-    }
-  }
+  fm_out(p, excl_sh + before, gain, R0, rtab, ys, y, base, n);
 }
 
 }  // namespace
@@ -363,7 +377,7 @@ void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, uint64
 long long fm_mod_chunks(long long n) { return (n + kFmCH - 1) / kFmCH; }
 
 void launch_fm_mod_sp(const float* x, f2* y, long long n, float kf, float gain, uint32_t* rec, uint32_t epoch,
-                      const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
+                      const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
                       int* err, hipStream_t s) {
   if (n <= 0) return;
   const long long nchunk = fm_mod_chunks(n);
@@ -374,8 +388,8 @@ void launch_fm_mod_sp(const float* x, f2* y, long long n, float kf, float gain, 
 }
 int fm_mod_rtab_len() { return kFmC; }
 
-void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, double* sums,
-                   const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
+void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, uint64_t* sums,
+                   const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
                    hipStream_t s) {
   if (n <= 0) return;
   const long long nchunk = fm_mod_chunks(n);

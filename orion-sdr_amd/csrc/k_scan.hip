@@ -983,7 +983,7 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
 // (warm-up of kSpWarm samples from a zero state after the first chunk, as in
 // k_lpdc_sp: the host checks ||A^kSpWarm||), and (I, side Q) x RF NCO stored.
 // carry: [I state 4][Q state 4] floats.
-__global__ __launch_bounds__(NT) void k_ssb_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
+__global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
                                                    uint64_t k0, uint64_t step_aud, uint64_t step_rf, float side,
                                                    ScanCoef cf, const double* __restrict__ mlp,
                                                    const float* __restrict__ carry_in, float* __restrict__ carry_out) {
@@ -998,19 +998,26 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_sp(const float* __restrict__ x, 
   const int cnt = static_cast<int>(min(static_cast<long long>(CH), n - base));
   const bool last = o0 + (cnt - warm) >= n;
   const RecLP4 lp{{cf.b0, cf.b1, cf.b2, cf.a1, cf.a2}};
-  {  // stage: x p.re, x p.im (ssb.rs:53-54), coalesced loads first
+  // Oscillator phasors of element e = t + k NT (the coalesced order of the staging and
+  // of the stores): P_t tab[k], P_t the exact phasor of element t, tab[k] = e^{j theta k NT}
+  // (audio NCO: tab[0..16), RF NCO: tab[16..32)) — two phasor evaluations per thread
+  // instead of two per sample.
+  __shared__ f2 tab[2 * C];
+  if (t < 2 * C) tab[t] = phasor_q64(static_cast<uint64_t>(t & (C - 1)) * NT, t < C ? step_aud : step_rf);
+  const f2 Pa = phasor_q64(k0 + static_cast<uint64_t>(base + t) + 1, step_aud);
+  const f2 Pr = phasor_q64(k0 + static_cast<uint64_t>(base + t) + 1, step_rf);
+  {  // stage: x p.re, x p.im (ssb.rs:53-54), coalesced loads first (unconditional, clamped)
     float v[C];
 #pragma unroll
-    for (int k = 0; k < C; ++k) {
-      const int e = t + k * NT;
-      v[k] = e < cnt ? x[base + e] : 0.0f;
-    }
+    for (int k = 0; k < C; ++k) v[k] = x[min(base + t + k * NT, n - 1)];
+    __syncthreads();  // tab
 #pragma unroll
     for (int k = 0; k < C; ++k) {
       const int e = t + k * NT;
-      const f2 p = phasor_q64(k0 + static_cast<uint64_t>(base + e) + 1, step_aud);
-      sb[0][pos(e)] = v[k] * p.x;
-      sb[1][pos(e)] = v[k] * p.y;
+      const float xv = e < cnt ? v[k] : 0.0f;
+      const f2 p = cmul(Pa, tab[k]);
+      sb[0][pos(e)] = xv * p.x;
+      sb[1][pos(e)] = xv * p.y;
     }
   }
   __syncthreads();
@@ -1101,13 +1108,19 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_sp(const float* __restrict__ x, 
 #pragma unroll
       for (int k = 0; k < S; ++k) carry_out[4 * b + k] = ef[k];
   }
+  // (I, side Q) staged in LDS (sb is free: every thread read its runs before the totals
+  // barrier; 17 f2 per thread: conflict-free b64 stores), then stored coalesced
+  // (each thread owning 16 consecutive samples would store 64 lanes x 8 B at a 128-B
+  // stride per instruction)
+  f2* zs = reinterpret_cast<f2*>(&sb[0][0]);
+  static_assert(2 * PADN >= 2 * (CH + CH / 16), "output staging fits");
 #pragma unroll
-  for (int i = 0; i < C; ++i) {  // ssb.rs:55-60
-    const int e = t * C + i;
-    if (e >= warm && e < cnt) {
-      const f2 r = phasor_q64(k0 + static_cast<uint64_t>(base + e) + 1, step_rf);
-      y[base + e] = cmul_rot(f2{xs[0][i], side * xs[1][i]}, r);
-    }
+  for (int i = 0; i < C; ++i) zs[17 * t + i] = f2{xs[0][i], side * xs[1][i]};
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < C; ++k) {  // ssb.rs:55-60
+    const int e = t + k * NT;
+    if (e >= warm && e < cnt) y[base + e] = cmul_rot(zs[e + (e >> 4)], cmul(Pr, tab[C + k]));
   }
 }
 

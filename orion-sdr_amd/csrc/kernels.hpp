@@ -24,19 +24,20 @@ void launch_pm_mod(const float* x, f2* y, long long n, uint64_t k0, uint64_t ste
 void launch_ssb_mod_front(const float* x, float* u, long long n, uint64_t k0, uint64_t step, hipStream_t s);
 // y = (v[i], side v[n + i]) * rf phasor k0 + i + 1
 void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, uint64_t step, float side, hipStream_t s);
-// FM phase accumulator: sums = fm_mod_chunks(n) doubles of workspace; carry_in /
-// carry_out: the running phase (one double each, ping-pong between calls)
+// FM phase accumulator: sums = fm_mod_chunks(n) uint64 of workspace; carry_in /
+// carry_out: the running phase as a Q0.64 turn count (one uint64 each, ping-pong
+// between calls; zero = phase 0)
 // rtab: e^{j theta k}, k < fm_mod_rtab_len(), of the RF oscillator
 long long fm_mod_chunks(long long n);
 // Single-pass form: rec = fm_mod_chunks(n) * 8 u32 look-back records (zeroed when
 // allocated), epoch = this launch's tag (never reused while a record may hold it).
 // err: the handle's host-visible error word (a look-back wait that timed out).
 void launch_fm_mod_sp(const float* x, f2* y, long long n, float kf, float gain, uint32_t* rec, uint32_t epoch,
-                      const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
+                      const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
                       int* err, hipStream_t s);
 int fm_mod_rtab_len();
-void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, double* sums,
-                   const double* carry_in, double* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
+void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, uint64_t* sums,
+                   const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
                    hipStream_t s);
 void launch_rotator(const f2* x_dev, f2* y_dev, long long n, uint64_t k0, uint64_t step_q64,
                     const f2* tab_dev, hipStream_t s);

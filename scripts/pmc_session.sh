@@ -11,4 +11,4 @@ for set in "${SS[@]}"; do
   i=$((i+1))
   timeout -k 10 90 rocprofv3 --pmc $set -d "$OUT/p$i" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ${BARGS:-} > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
 done
-python3 scripts/prof_summary.py "$OUT" | tee "$OUT/summary.txt"
+python3 scripts/prof_summary.py "$OUT" | tee "$OUT/summary.txt"; rm -rf "$OUT"/p[0-9]*/

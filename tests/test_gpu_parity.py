@@ -716,6 +716,11 @@ def test_fm_phase_accum_mod(gpu_lib, oracle):
     m = gpu_lib.FmPhaseAccumMod(fs, 75e3, 1.5e6)
     streamed = np.concatenate([m.process(aud[i:i + 300_007]) for i in range(0, n, 300_007)])
     report("fm_mod streamed vs one call max abs", float(np.max(np.abs(streamed - one))), 2e-6)
+    # phases are Q0.64 integer sums: the look-back's order cannot change a bit, so a
+    # repeat run and the three-pass form give the single pass's exact output
+    assert np.array_equal(gpu_lib.FmPhaseAccumMod(fs, 75e3, 1.5e6).process(aud), one)
+    m3 = gpu_lib.FmPhaseAccumMod(fs, 75e3, 1.5e6).configure_option("mod_passes", 3)
+    assert np.array_equal(m3.process(aud), one)
     report("fm_mod -> wbfm audio nrmse", nrmse(oracle.wbfm(one), oracle.wbfm(ref)), 1e-5)
     g = gpu_lib.FmPhaseAccumMod(fs, 75e3, 0.0)
     g.set_deviation(50e3)
