@@ -103,6 +103,43 @@ __device__ __forceinline__ float premap(const ScanArgs& a, int ch, long long i, 
   }
 }
 
+// premap with the samples already loaded: z = x[i], zp = x[i - 1] (any value when
+// i == 0: the carried previous sample is used), raw (untranslated) complex samples.
+template <Pre PR>
+__device__ __forceinline__ f2 cin_v(const ScanArgs& a, f2 z, long long i, long long base, f2 Swg) {
+  if constexpr (PR == Pre::Fm) {
+    if (a.translate) {
+      const f2 p = (i >= base) ? cmul(Swg, a.tab[i - base])
+                               : phasor_q64(static_cast<uint64_t>(a.k0 + i + 1), a.step);
+      const float c = p.x, d = -p.y;  // num-complex z * conj(p)
+      return f2{z.x * c - z.y * d, z.x * d + z.y * c};
+    }
+  }
+  return z;
+}
+template <Pre PR>
+__device__ __forceinline__ float premap_v(const ScanArgs& a, int ch, long long i, long long base, f2 Swg, f2 z,
+                                          f2 zp) {
+  if constexpr (PR == Pre::Fm || PR == Pre::Pm) {
+    const f2 zc = cin_v<PR>(a, z, i, base, Swg);
+    f2 p;
+    if (i > 0) {
+      p = cin_v<PR>(a, zp, i - 1, base, Swg);
+    } else {
+      const float* cr = a.carry_in + ch * kScanCarry;
+      p = f2{cr[6], cr[7]};
+    }
+    if constexpr (PR == Pre::Fm) return fm_disc(zc, p, a.c.k);
+    else return pm_disc(zc, p, a.c.k);
+  } else if constexpr (PR == Pre::AmSqrt) {
+    return __builtin_fmaf(z.x, z.x, z.y * z.y);  // am.rs:204
+  } else if constexpr (PR == Pre::Cw) {
+    return sqrtf(z.x * z.x + z.y * z.y);  // cw.rs:38
+  } else {
+    return z.x;  // Pre::Real: the f32 sample in z.x
+  }
+}
+
 template <Pre PR>
 __device__ __forceinline__ void stage(const ScanArgs& a, int ch, long long base, int cnt, float* sb) {
   f2 Swg = f2{1.0f, 0.0f};
@@ -843,11 +880,34 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
       for (int h = 0; h < 2; ++h) Sw[h] = phasor_q64(static_cast<uint64_t>(a.k0 + base + 1 + h * kScanCH), a.step);
     }
   }
-#pragma unroll 8
-  for (int k = 0; k < SC; ++k) {  // 8 loads in flight per batch: unrolled 32, the loads spill
-    const int e = t + k * NT;
-    const int h = k >= KT ? 1 : 0;
-    if (e < cnt) sb[posS<SC>(e)] = premap<PR>(a, ch, base + e, base + h * kScanCH, h ? Sw[1] : Sw[0]);
+  // Batches of 8 samples per thread: every load of a batch issued before any is used
+  // (unconditional, index clamped into [0, n)), then the pre-map. (A guarded load per
+  // sample compiles to a branch around each, which waits for its load before the LDS
+  // store: one memory latency per sample.) FM / PM also load x[i - 1] (an L1/L2 hit).
+  static_assert(SC % 8 == 0 && KT % 8 == 0, "staging batches");
+  constexpr bool kPair = PR == Pre::Fm || PR == Pre::Pm;
+  const long long nl = a.n - 1;
+#pragma unroll 1
+  for (int k0 = 0; k0 < SC; k0 += 8) {
+    f2 z[8], zp[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long long i = base + t + (k0 + j) * NT;
+      if constexpr (PR == Pre::Real) {
+        z[j] = f2{static_cast<const float*>(a.x)[ch * a.x_stride + min(i, nl)], 0.0f};
+      } else {
+        const f2* __restrict__ xc = static_cast<const f2*>(a.x) + ch * a.x_stride;
+        z[j] = xc[min(i, nl)];
+        if constexpr (kPair) zp[j] = xc[max(min(i - 1, nl), 0LL)];
+      }
+    }
+    const int h = k0 >= KT ? 1 : 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = t + (k0 + j) * NT;
+      if (e < cnt) sb[posS<SC>(e)] = premap_v<PR>(a, ch, base + e, base + h * kScanCH, h ? Sw[1] : Sw[0], z[j],
+                                                  kPair ? zp[j] : z[j]);
+    }
   }
   __syncthreads();
 
