@@ -7,4 +7,4 @@ timeout -k 10 300 python tools/block_bench.py > "$OUT/blocks.jsonl" 2> "$OUT/blo
 cat "$OUT/blocks.jsonl"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run -- python3 tools/block_bench.py --cpu-n 65536 > "$OUT/prof.log" 2>&1 || { tail -5 "$OUT/prof.log"; exit 1; }
 f=$(find "$OUT/prof" -name "*kernel_stats.csv" | head -1); cp "$f" "$OUT/kernel_stats_blocks.csv"
-echo "=== done"
+rm -rf "$OUT"/prof_*/ "$OUT"/prof/ 2>/dev/null; echo "=== done"

@@ -13,4 +13,4 @@ for c in ${CFGS:-c3 c4 c5}; do
   run prof_$c 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$c" -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu --config $c
 done
 for d in "$OUT"/prof_*; do f=$(find "$d" -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cp "$f" "$OUT/kernel_stats_$(basename $d | sed s/prof_//).csv"; done
-echo "=== done"
+rm -rf "$OUT"/prof_*/ "$OUT"/prof/ 2>/dev/null; echo "=== done"
