@@ -11,7 +11,7 @@ constexpr int NT = kScanNT;
 constexpr int CH = kScanCH;
 constexpr int PADN = CH + CH / 16 + 16;
 #ifndef ORION_SP_ABL
-#define ORION_SP_ABL 0  // timing experiments only: 1 no phasor table, 2 no look-back, 4 no LP scan
+#define ORION_SP_ABL 0  // timing experiments only: 1 no phasor table, 2 no look-back, 4 no LP scan, 8 staging + stores only
 #endif
 #ifndef ORION_SP_WAVES
 #define ORION_SP_WAVES 1  // occupancy hint for k_lpdc_sp (experiments: 6)
@@ -578,6 +578,16 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   const float r = a.c.r;
   stage_sp<PR, SC>(a, ch, base, cnt, sb);
   wave_order();  // wave-local staging
+  if constexpr ((ORION_SP_ABL & 8) != 0) {  // timing floor: staging and stores only
+    float* yo = static_cast<float*>(a.y) + ch * a.y_stride + o0;
+    const int e0 = wave * (64 * SC) + lane;
+#pragma unroll
+    for (int k = 0; k < SC; ++k) {
+      const int e2 = e0 + 64 * k;
+      if (e2 >= warm && e2 < cnt) yo[e2 - warm] = sb[posS<SC>(e2)];
+    }
+    return;
+  }
 
   // ---- LP4: zero-state lane aggregates, block scan, exact re-run ----
   float xs[C];
