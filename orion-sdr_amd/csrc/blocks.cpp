@@ -383,9 +383,7 @@ class FirRealBlock final : public Block {
     if (n == 0) return {0, 0};
     const float* x = static_cast<const float*>(in);
     launch_fir_real(x, static_cast<long long>(n), hist_[cur_].as<float>(), hist_len_, static_cast<float*>(out),
-                    K_, fast_, g_dev_.as<float>(), s);
-    launch_hist_update_r(x, static_cast<long long>(n), hist_[cur_].as<float>(), hist_[cur_ ^ 1].as<float>(),
-                         hist_len_, s);
+                    K_, fast_, g_dev_.as<float>(), s, hist_[cur_ ^ 1].as<float>());
     cur_ ^= 1;
     return {n, n};
   }
@@ -430,9 +428,7 @@ class FirIqBlock final : public Block {
     if (n == 0) return {0, 0};
     const f2* x = static_cast<const f2*>(in);
     launch_fir_iq(x, static_cast<long long>(n), hist_[cur_].as<f2>(), hist_len_, static_cast<f2*>(out),
-                  static_cast<long long>(n), 0, K_, fast_, g_dev_.as<float>(), s);
-    launch_hist_update_c(x, static_cast<long long>(n), hist_[cur_].as<f2>(), hist_[cur_ ^ 1].as<f2>(),
-                         hist_len_, s);
+                  static_cast<long long>(n), 0, K_, fast_, g_dev_.as<float>(), s, hist_[cur_ ^ 1].as<f2>());
     cur_ ^= 1;
     return {n, n};
   }

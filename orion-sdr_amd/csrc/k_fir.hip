@@ -365,12 +365,27 @@ __global__ __launch_bounds__(NT) void k_decim_generic(const f2* __restrict__ x, 
   }
 }
 
+// The next call's history, fused into the first workgroup of a FIR launch (saves the
+// separate k_hist_update launch, ~4 us of a 2^20-sample call): the last hist_len
+// samples of [old_h | x[0..n)] into new_h (a different buffer: the histories ping-pong).
+template <class V>
+__device__ __forceinline__ void hist_next(const V* __restrict__ x, long long n, const V* __restrict__ old_h,
+                                          V* __restrict__ new_h, int hist_len) {
+  if (new_h == nullptr || blockIdx.x != 0) return;
+  for (int i = threadIdx.x; i < hist_len; i += blockDim.x) {
+    const long long P = n - hist_len + i;
+    new_h[i] = P >= 0 ? x[P] : old_h[hist_len + P];
+  }
+}
+
 // --------------------------------------------------------- real FIR -------
 // y[i] = sum_{k<KP} g[k] x[i-k], 512 outputs per sub-tile, 2 per lane.
 template <int KP>
 __global__ __launch_bounds__(NT) void k_fir_real8(const float* __restrict__ x, long long n,
                                                   const float* __restrict__ hist, int hist_len,
-                                                  float* __restrict__ y, const Taps256 g) {
+                                                  float* __restrict__ y, const Taps256 g,
+                                                  float* __restrict__ hist_out = nullptr) {
+  hist_next(x, n, hist, hist_out, hist_len);
   constexpr int TH = 8 * NT, TT = 2 * TH;  // 2048 outputs per half, 4096 per tile
   constexpr int W = TH + KP + 2, PER = (W + NT - 1) / NT;
   constexpr int WP = W + 2 * (W / 8) + 2;
@@ -468,7 +483,9 @@ template <int KP, bool INPLACE = false>
 __global__ __launch_bounds__(NT) void k_fir_iq8(const f2* x, long long n,
                                                 const f2* __restrict__ hist, int hist_len,
                                                 f2* y, long long n_out, long long off,
-                                                const Taps256 g, const f2* __restrict__ E = nullptr) {
+                                                const Taps256 g, const f2* __restrict__ E = nullptr,
+                                                f2* __restrict__ hist_out = nullptr) {
+  if constexpr (!INPLACE) hist_next(x, n, hist, hist_out, hist_len);
   constexpr int TT = 8 * NT;
   constexpr int W = TT + KP + 2, PER = (W + NT - 1) / NT;
   constexpr int WP = W + 2 * (W / 8) + 2;
@@ -708,25 +725,31 @@ void launch_decim(const f2* x, long long n, const f2* hist, int hist_len, f2* ou
 }
 
 void launch_fir_real(const float* x, long long n, const float* hist, int hist_len, float* y, int K,
-                     const Taps256& g, const float* g_dev, hipStream_t s) {
+                     const Taps256& g, const float* g_dev, hipStream_t s, float* hist_out) {
   if (n <= 0) return;
   const int g16 = static_cast<int>(std::min<long long>(kMaxGrid, (n + 16 * NT - 1) / (16 * NT)));
-  if (K <= 64 && hist_len >= 64) k_fir_real8<64><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g);
-  else if (K <= 128 && hist_len >= 128) k_fir_real8<128><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g);
-  else if (K <= 256 && hist_len >= 256) k_fir_real8<256><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g);
-  else k_fir_real_generic<<<grid_for(n, NT), NT, 0, s>>>(x, n, hist, hist_len, y, K, g_dev);
+  if (K <= 64 && hist_len >= 64) k_fir_real8<64><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g, hist_out);
+  else if (K <= 128 && hist_len >= 128) k_fir_real8<128><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g, hist_out);
+  else if (K <= 256 && hist_len >= 256) k_fir_real8<256><<<g16, NT, 0, s>>>(x, n, hist, hist_len, y, g, hist_out);
+  else {
+    k_fir_real_generic<<<grid_for(n, NT), NT, 0, s>>>(x, n, hist, hist_len, y, K, g_dev);
+    if (hist_out) launch_hist_update_r(x, n, hist, hist_out, hist_len, s);
+  }
   ORION_LAUNCH_CHECK();
 }
 
 void launch_fir_iq(const f2* x, long long n, const f2* hist, int hist_len, f2* y, long long n_out,
-                   long long off, int K, const Taps256& g, const float* g_dev, hipStream_t s) {
+                   long long off, int K, const Taps256& g, const float* g_dev, hipStream_t s, f2* hist_out) {
   if (n_out <= 0) return;
   if (K <= 256 && hist_len >= (K <= 64 ? 64 : K <= 128 ? 128 : 256)) {
     const int g8 = grid_for(n_out, 8 * NT);
-    if (K <= 64) k_fir_iq8<64><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
-    else if (K <= 128) k_fir_iq8<128><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
-    else k_fir_iq8<256><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g);
-  } else k_fir_iq_generic<<<grid_for(n_out, NT), NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, K, g_dev);
+    if (K <= 64) k_fir_iq8<64><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
+    else if (K <= 128) k_fir_iq8<128><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
+    else k_fir_iq8<256><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
+  } else {
+    k_fir_iq_generic<<<grid_for(n_out, NT), NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, K, g_dev);
+    if (hist_out) launch_hist_update_c(x, n, hist, hist_out, hist_len, s);
+  }
   ORION_LAUNCH_CHECK();
 }
 

@@ -61,14 +61,17 @@ void launch_decim_batch(const f2* x_dev, long long x_stride, long long n, const 
                         int hist_len, f2* out_dev, long long out_stride, long long n_out, int nch,
                         int M, int K, const Taps256& g, const float* g_dev, hipStream_t s);
 // Real FIR y[i] = sum_k g[k] x[i-k] (x[P<0] from hist).
+// hist_out (optional): the next call's history (last hist_len of [hist | x]), written by
+// the FIR launch itself (no separate k_hist_update launch).
 void launch_fir_real(const float* x_dev, long long n, const float* hist_dev, int hist_len,
-                     float* y_dev, int K, const Taps256& g, const float* g_dev, hipStream_t s);
+                     float* y_dev, int K, const Taps256& g, const float* g_dev, hipStream_t s,
+                     float* hist_out = nullptr);
 // Complex-sample real-tap FIR y[i] = sum_k g[k] x[i + off - k], i < n_out
 // (x[P<0] from hist, x[P>=n] = 0). off = 0: streaming; off = (K-1)/2 with an
 // all-zero history: FirLowpassIq::filter_aligned.
 void launch_fir_iq(const f2* x_dev, long long n, const f2* hist_dev, int hist_len, f2* y_dev,
                    long long n_out, long long off, int K, const Taps256& g, const float* g_dev,
-                   hipStream_t s);
+                   hipStream_t s, f2* hist_out = nullptr);
 // Copy the last hist_len samples of [old_hist | x[0..n)] into new_hist.
 // FirLowpassIq::filter_aligned in place (k_fir_iq8 INPLACE + boundary copies);
 // writes the history the reference leaves (last hist_len of [x | 0^d]) to
