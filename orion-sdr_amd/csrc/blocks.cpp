@@ -335,9 +335,7 @@ class DecimBlock final : public Block {
     launch_decim_batch(x, static_cast<long long>(n), static_cast<long long>(n), hist_[cur_].as<f2>(),
                        hist_len_, static_cast<f2*>(out), static_cast<long long>(out_cap),
                        static_cast<long long>(n_write), nch_, static_cast<int>(m_), K_, fast_,
-                       g_dev_.as<float>(), s);
-    launch_hist_update_c(x, static_cast<long long>(n), hist_[cur_].as<f2>(), hist_[cur_ ^ 1].as<f2>(),
-                         hist_len_, s, nch_, static_cast<long long>(n));
+                       g_dev_.as<float>(), s, hist_[cur_ ^ 1].as<f2>());
     cur_ ^= 1;
     return {n, n_write};  // all input consumed, decim.rs:72-75
   }

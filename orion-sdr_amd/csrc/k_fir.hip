@@ -137,6 +137,19 @@ __device__ __forceinline__ void dw_load(const f2* __restrict__ x, long long n, l
   }
 }
 
+// The next call's history of channel ch (last hist_len of [hc | xc[0..n)]), written by
+// the wave that owns the channel's first output range (one wave, 64 lanes): no separate
+// k_hist_update launch. hist_out is the other buffer of the ping-pong pair.
+__device__ __forceinline__ void dw_hist_next(const f2* __restrict__ xc, long long n, const f2* __restrict__ hc,
+                                             f2* __restrict__ hist_out, int ch, int hist_len, int l) {
+  if (hist_out == nullptr) return;
+  f2* __restrict__ hn = hist_out + static_cast<long long>(ch) * hist_len;
+  for (int i = l; i < hist_len; i += 64) {
+    const long long P = n - hist_len + i;
+    hn[i] = P >= 0 ? xc[P] : hc[hist_len + P];
+  }
+}
+
 // ------------------------------------ four-group wave-independent decimator ---
 // k_decim_w4<Q>: k_decim_w with the decimator split over the four ds_read_b128
 // lane groups of gfx950 (as k_wbfm.hip's fu_tile8): lane group g (A = lanes 0-3,
@@ -273,7 +286,7 @@ template <int Q, bool A16, bool CLAMP>
 __global__ __launch_bounds__(64, 2) void k_decim_w4(const f2* __restrict__ x, long long x_stride, long long n,
                                                    const f2* __restrict__ hist, int hist_len, f2* __restrict__ out,
                                                    long long out_stride, long long n_out, const Taps256 g, int wpc,
-                                                   long long L) {
+                                                   long long L, f2* __restrict__ hist_out = nullptr) {
   using D = Dw4<Q>;
   __shared__ __attribute__((aligned(16))) f2 U[D::LDS_F2];
   __shared__ __attribute__((aligned(16))) float Gt[8 * Q];
@@ -287,6 +300,7 @@ __global__ __launch_bounds__(64, 2) void k_decim_w4(const f2* __restrict__ x, lo
   const int ntiles = (static_cast<int>((B - A + D::TW - 1) / D::TW) + 1) & ~1;
   const f2* __restrict__ xc = x + ch * x_stride;
   const f2* __restrict__ hc = hist + static_cast<long long>(ch) * hist_len;
+  if (A == 0) dw_hist_next(xc, n, hc, hist_out, ch, hist_len, l);
   f2* __restrict__ outc = out + ch * out_stride;
   const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
   const int s0 = c0 * D::LRS + D::slot((8 * Q + 2 * l + c0) / 8);
@@ -314,7 +328,7 @@ template <int Q, bool A16, bool CLAMP>
 __global__ __launch_bounds__(256, 3) void k_decim_w4q(const f2* __restrict__ x, long long x_stride, long long n,
                                                      const f2* __restrict__ hist, int hist_len, f2* __restrict__ out,
                                                      long long out_stride, long long n_out, const Taps256 g, int wpc,
-                                                     long long L, int nranges) {
+                                                     long long L, int nranges, f2* __restrict__ hist_out = nullptr) {
   using D = Dw4<Q>;
   __shared__ __attribute__((aligned(16))) f2 U4[4][D::LDS_F2];
   __shared__ __attribute__((aligned(16))) float Gt[8 * Q];
@@ -331,6 +345,7 @@ __global__ __launch_bounds__(256, 3) void k_decim_w4q(const f2* __restrict__ x, 
   const int ntiles = static_cast<int>((B - A + D::TW - 1) / D::TW);
   const f2* __restrict__ xc = x + ch * x_stride;
   const f2* __restrict__ hc = hist + static_cast<long long>(ch) * hist_len;
+  if (A == 0) dw_hist_next(xc, n, hc, hist_out, ch, hist_len, l);
   f2* __restrict__ outc = out + ch * out_stride;
   const int c0 = (-2 * l) & 7, c1 = (-2 * l - 1) & 7;
   const int s0 = c0 * D::LRS + D::slot((8 * Q + 2 * l + c0) / 8);
@@ -652,7 +667,7 @@ void launch_rotator(const f2* x, f2* y, long long n, uint64_t k0, uint64_t step,
 
 void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* hist, int hist_len,
                         f2* out, long long out_stride, long long n_out, int nch, int M, int K,
-                        const Taps256& g, const float* g_dev, hipStream_t s) {
+                        const Taps256& g, const float* g_dev, hipStream_t s, f2* hist_out) {
   if (n_out <= 0 || nch <= 0) return;
   const bool a16 = reinterpret_cast<uintptr_t>(x) % 16 == 0 && x_stride % 2 == 0;
   // M = 8 with 129..256 taps (C3): k_decim_w4q, four waves per workgroup sharing one
@@ -675,11 +690,11 @@ void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* 
     const bool clamp = n < 2 * 1024;
     const int gi = static_cast<int>((nr + 3) / 4), wi = static_cast<int>(wpc), ni = static_cast<int>(nr);
     if (clamp) {
-      if (a16) k_decim_w4q<32, true, true><<<gi, 256, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, ni);
-      else k_decim_w4q<32, false, true><<<gi, 256, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, ni);
+      if (a16) k_decim_w4q<32, true, true><<<gi, 256, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, ni, hist_out);
+      else k_decim_w4q<32, false, true><<<gi, 256, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, ni, hist_out);
     } else {
-      if (a16) k_decim_w4q<32, true, false><<<gi, 256, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, ni);
-      else k_decim_w4q<32, false, false><<<gi, 256, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, ni);
+      if (a16) k_decim_w4q<32, true, false><<<gi, 256, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, ni, hist_out);
+      else k_decim_w4q<32, false, false><<<gi, 256, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, ni, hist_out);
     }
     ORION_LAUNCH_CHECK();
     return;
@@ -704,17 +719,18 @@ void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* 
     const int gi = static_cast<int>(grid), wi = static_cast<int>(wpc);
 #define ORION_DW(KK, QQ)                                                                                    \
   if (clamp) {                                                                                              \
-    if (a16) KK<QQ, true, true><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
-    else KK<QQ, false, true><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
+    if (a16) KK<QQ, true, true><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, hist_out); \
+    else KK<QQ, false, true><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, hist_out); \
   } else {                                                                                                  \
-    if (a16) KK<QQ, true, false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
-    else KK<QQ, false, false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L); \
+    if (a16) KK<QQ, true, false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, hist_out); \
+    else KK<QQ, false, false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, g, wi, L, hist_out); \
   }
     if (K <= 128) { ORION_DW(k_decim_w4, 16) } else { ORION_DW(k_decim_w4, 32) }
 #undef ORION_DW
   } else {
     const dim3 grid(grid_for(n_out, NT), nch);
     k_decim_generic<<<grid, NT, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, M, K, g_dev);
+    if (hist_out) launch_hist_update_c(x, n, hist, hist_out, hist_len, s, nch, x_stride);
   }
   ORION_LAUNCH_CHECK();
 }

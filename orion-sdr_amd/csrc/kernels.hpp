@@ -57,9 +57,11 @@ void launch_decim(const f2* x_dev, long long n, const f2* hist_dev, int hist_len
                   long long n_out, int M, int K, const Taps256& g, const float* g_dev,
                   hipStream_t s);
 // Batched over channels: x[ch*x_stride + i], out[ch*out_stride + j], shared taps.
+// hist_out (optional): each channel's next history, written by the launch itself.
 void launch_decim_batch(const f2* x_dev, long long x_stride, long long n, const f2* hist_dev,
                         int hist_len, f2* out_dev, long long out_stride, long long n_out, int nch,
-                        int M, int K, const Taps256& g, const float* g_dev, hipStream_t s);
+                        int M, int K, const Taps256& g, const float* g_dev, hipStream_t s,
+                        f2* hist_out = nullptr);
 // Real FIR y[i] = sum_k g[k] x[i-k] (x[P<0] from hist).
 // hist_out (optional): the next call's history (last hist_len of [hist | x]), written by
 // the FIR launch itself (no separate k_hist_update launch).
