@@ -393,6 +393,50 @@ __device__ __forceinline__ void hist_next(const V* __restrict__ x, long long n, 
   }
 }
 
+// The FIR's 8-outputs-per-lane block loop over a padded LDS image L (pidx: two slots
+// per eight) and LDS taps Gt (k_fir_iq8: complex samples; k_fir_real8: two real halves
+// packed). Window base: staged p = pb + 2h, pb = 8 t + KP - 16 kb - 16 (a multiple of 8),
+// so pidx(pb + 2h) = 10 (pb / 8) + 2h + 2 (h >> 2): one base per lane, minus 20 per block,
+// compile-time offsets (ds_read_b128 with immediates). Output 8 t + r, tap 16 kb + kk
+// reads staged p = pb + 16 + r - kk. Per block the taps (wave-uniform LDS reads) come
+// first, then the window in the order the FMA chains first need it (tap kk = 0 uses
+// entries 16..23, kk = 1 entry 15, ...): LDS reads return in order, so the first FMAs
+// wait for 8 reads, not for all 16 and a scalar tap load (lgkmcnt(0)). The summation
+// order (kk ascending: the reference's) is unchanged.
+template <int KP>
+__device__ __forceinline__ void fir8_blocks(const f2* __restrict__ L, const float* __restrict__ Gt, int t,
+                                            f2 (&acc)[8]) {
+  const f2* __restrict__ Lt = L + 10 * t + 10 * (KP - 16) / 8;
+#pragma unroll 1
+  for (int kb = 0; kb < KP / 16; ++kb) {
+    const f2* __restrict__ Lb = Lt - 20 * kb;
+    const f4* __restrict__ tq = reinterpret_cast<const f4*>(Gt + 16 * kb);
+    float tp[16];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const f4 u = tq[q4];
+      tp[4 * q4] = u.x;
+      tp[4 * q4 + 1] = u.y;
+      tp[4 * q4 + 2] = u.z;
+      tp[4 * q4 + 3] = u.w;
+    }
+    f2 w[24];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const int h = i < 4 ? 8 + i : 11 - i;  // 8, 9, 10, 11, 7, 6, ..., 0
+      const f4 v = *reinterpret_cast<const f4*>(Lb + 2 * h + 2 * (h >> 2));
+      w[2 * h] = f2{v.x, v.y};
+      w[2 * h + 1] = f2{v.z, v.w};
+    }
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      const f2 tap = splat2(tp[kk]);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc[r] = fma2(tap, w[16 + r - kk], acc[r]);
+    }
+  }
+}
+
 // --------------------------------------------------------- real FIR -------
 // y[i] = sum_{k<KP} g[k] x[i-k], 512 outputs per sub-tile, 2 per lane.
 template <int KP>
@@ -406,7 +450,9 @@ __global__ __launch_bounds__(NT) void k_fir_real8(const float* __restrict__ x, l
   constexpr int WP = W + 2 * (W / 8) + 2;
   static_assert(KP % 16 == 0, "taps padded to 16");
   __shared__ __attribute__((aligned(16))) f2 L[WP];
+  __shared__ __attribute__((aligned(16))) float Gt[KP];  // the taps (read by the first barrier)
   auto pidx = [](int p) { return p + 2 * (p >> 3); };
+  for (int k = threadIdx.x; k < KP; k += NT) Gt[k] = g.g[k];
   auto ld = [&](long long P) {
     float v = 0.0f;
     if (P >= 0) v = P < n ? x[P] : 0.0f;
@@ -436,23 +482,7 @@ __global__ __launch_bounds__(NT) void k_fir_real8(const float* __restrict__ x, l
     f2 acc[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) acc[r] = f2{0.0f, 0.0f};
-#pragma unroll 1
-    for (int kb = 0; kb < KP / 16; ++kb) {
-      const int pb = 8 * t + KP - 16 * kb - 16;  // as k_fir_iq8 (off = 0)
-      f2 w[24];
-#pragma unroll
-      for (int h = 0; h < 12; ++h) {
-        const f4 v = *reinterpret_cast<const f4*>(L + pidx(pb + 2 * h));
-        w[2 * h] = f2{v.x, v.y};
-        w[2 * h + 1] = f2{v.z, v.w};
-      }
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const f2 tap = splat2(g.g[16 * kb + kk]);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) acc[r] = fma2(tap, w[16 + r - kk], acc[r]);
-      }
-    }
+    fir8_blocks<KP>(L, Gt, t, acc);  // as k_fir_iq8 (off = 0), both halves packed
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const long long j0 = J + half * TH + 8 * t;
@@ -506,8 +536,10 @@ __global__ __launch_bounds__(NT) void k_fir_iq8(const f2* x, long long n,
   constexpr int WP = W + 2 * (W / 8) + 2;
   static_assert(KP % 16 == 0, "taps padded to 16");
   __shared__ __attribute__((aligned(16))) f2 L[WP];
+  __shared__ __attribute__((aligned(16))) float Gt[KP];  // the taps (read by the first barrier)
   auto pidx = [](int p) { return p + 2 * (p >> 3); };
   const int t = threadIdx.x;
+  for (int k = t; k < KP; k += NT) Gt[k] = g.g[k];
   for (long long J = static_cast<long long>(blockIdx.x) * TT; J < n_out;
        J += static_cast<long long>(gridDim.x) * TT) {
     const long long org = J + off - KP;  // staged sample p <-> element org + p
@@ -550,25 +582,7 @@ __global__ __launch_bounds__(NT) void k_fir_iq8(const f2* x, long long n,
     f2 acc[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) acc[r] = f2{0.0f, 0.0f};
-#pragma unroll 1
-    for (int kb = 0; kb < KP / 16; ++kb) {
-      // output j0 + r, tap 16 kb + kk reads element j0 + off + r - 16 kb - kk =
-      // staged p = pb + 16 + r - kk, pb = 8 t + KP - 16 kb - 16 (even, >= 0)
-      const int pb = 8 * t + KP - 16 * kb - 16;
-      f2 w[24];
-#pragma unroll
-      for (int h = 0; h < 12; ++h) {
-        const f4 v = *reinterpret_cast<const f4*>(L + pidx(pb + 2 * h));
-        w[2 * h] = f2{v.x, v.y};
-        w[2 * h + 1] = f2{v.z, v.w};
-      }
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const f2 tap = splat2(g.g[16 * kb + kk]);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) acc[r] = fma2(tap, w[16 + r - kk], acc[r]);
-      }
-    }
+    fir8_blocks<KP>(L, Gt, t, acc);
     const long long j0 = J + 8 * t;
     if (j0 + 8 <= n_out && (reinterpret_cast<uintptr_t>(y + j0) & 15) == 0) {
       f4* yo = reinterpret_cast<f4*>(y + j0);
