@@ -10,6 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CFG = {  # samples per launch, input bytes, algorithmic bytes per sample, kernel name fragment
+    "c1": (1 << 20, 8 * (1 << 20), 16.0, "k_fir_iq8"),
     "c2": (1 << 26, 8 * (1 << 26), 8.5, "k_wbfm_seg"),
     "c3": (256 << 20, 8 * (256 << 20), 9.0, "k_decim_w4"),
     "c4": (8 << 24, 8 * (8 << 24), 8.5, "k_wbfm_seg"),
