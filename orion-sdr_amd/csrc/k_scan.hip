@@ -895,11 +895,16 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   // sample compiles to a branch around each, which waits for its load before the LDS
   // store: one memory latency per sample.) FM / PM also load x[i - 1] (an L1/L2 hit).
   static_assert(SC % 8 == 0 && KT % 8 == 0, "staging batches");
-  constexpr bool kPair = PR == Pre::Fm || PR == Pre::Pm;
+  // FM: the previous sample from the neighbour lane (below); PM: its own load of x[i - 1]
+  // (an L1/L2 hit; the neighbour form measured 6 % slower there: more spills)
+  constexpr bool kPair = PR == Pre::Fm, kPrev = PR == Pre::Pm;
   const long long nl = a.n - 1;
 #pragma unroll 1
   for (int k0 = 0; k0 < SC; k0 += 8) {
-    f2 z[8], zp[8];
+    const int h = k0 >= KT ? 1 : 0;
+    const long long bh = base + h * kScanCH;
+    const f2 Sh = h ? Sw[1] : Sw[0];
+    f2 z[8], zp[8], zq = f2{0.0f, 0.0f};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const long long i = base + t + (k0 + j) * NT;
@@ -908,15 +913,33 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
       } else {
         const f2* __restrict__ xc = static_cast<const f2*>(a.x) + ch * a.x_stride;
         z[j] = xc[min(i, nl)];
-        if constexpr (kPair) zp[j] = xc[max(min(i - 1, nl), 0LL)];
+        zp[j] = kPrev ? xc[max(min(i - 1, nl), 0LL)] : z[j];
       }
     }
-    const int h = k0 >= KT ? 1 : 0;
+    if constexpr (kPair) {
+      // FM: the previous sample of lane L is lane L - 1's (a DPP shift of the mapped
+      // sample: no second load, no second translation); lane 0 of the wave needs the sample before the wave's run of
+      // row k0 + j: lane j of the wave loads and maps it for all eight j in one load.
+      const long long iq = base + (t & ~63) + (k0 + (lane & 7)) * NT - 1;
+      zq = cin_v<PR>(a, (static_cast<const f2*>(a.x) + ch * a.x_stride)[max(min(iq, nl), 0LL)], iq, bh, Sh);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int e = t + (k0 + j) * NT;
-      if (e < cnt) sb[posS<SC>(e)] = premap_v<PR>(a, ch, base + e, base + h * kScanCH, h ? Sw[1] : Sw[0], z[j],
-                                                  kPair ? zp[j] : z[j]);
+      float o;
+      if constexpr (kPair) {
+        const f2 zc = cin_v<PR>(a, z[j], base + e, bh, Sh);
+        f2 p = f2{wave_up<1>(zc.x), wave_up<1>(zc.y)};
+        if (lane == 0) {
+          p = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(zq.x), j)),
+                 __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zq.y), j))};
+          if (base + e == 0) p = f2{ci[6], ci[7]};  // the carried previous sample
+        }
+        o = fm_disc(zc, p, a.c.k);
+      } else {
+        o = premap_v<PR>(a, ch, base + e, bh, Sh, z[j], zp[j]);
+      }
+      if (e < cnt) sb[posS<SC>(e)] = o;
     }
   }
   __syncthreads();
