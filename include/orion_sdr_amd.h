@@ -54,22 +54,42 @@ const char* orion_last_error(void);          /* thread-local message of the last
 int orion_device_count(void);
 int orion_set_device(int device);
 int orion_synchronize(void* stream);
+int orion_device_cus(void);                 /* compute units of the current device (< 0: error) */
 /* On-box bandwidth probe (no reference counterpart; bench.py's measured read
  * peak): one streaming read of the first orion_diag_stream_read_bytes(bytes)
  * bytes of the 16-B aligned device buffer `dev`, asynchronous on `stream`. */
 size_t orion_diag_stream_read_bytes(size_t bytes);
 int orion_diag_stream_read(const void* dev, size_t bytes, void* stream);
+/* Residency tests (no reference counterpart): `workgroups` one-wave workgroups that
+ * each hold lds_bytes of LDS (256 .. 160 KiB) for `seconds` (<= 10) of wall clock on
+ * `stream`, asynchronous; and a stream restricted to the first n_cus CUs (0: an
+ * ordinary non-blocking stream), destroyed with orion_diag_stream_destroy. */
+int orion_diag_spin(void* stream, uint32_t workgroups, uint32_t lds_bytes, double seconds);
+void* orion_diag_stream_create(uint32_t n_cus);
+int orion_diag_stream_destroy(void* stream);
 
 /* ---- constructors (one per reference constructor) ---------------------- */
 /* dsp/rotator.rs:16-26 Rotator::new(freq_hz, fs); Block-like rotate_block (:74-85). cf32->cf32
- * The oscillator is closed-form and phase-exact: the phasor after k steps is
- * e^{j theta k} with theta the exact angle of the reference's f32 step phasor w
- * (the reference's f32 recurrence drifts from it by its own rounding). */
+ * The oscillator tracks the reference's own f32 recurrence (z <- z w, renormalised
+ * every 1024 steps, :44-62), not the ideal phasor it drifts from: at construction and
+ * every set_freq / reset_phase the host runs that recurrence from the current state
+ * for up to ORION_OPT_NCO_TABLE outputs (default 2^20, a few ms) and the device reads
+ * its phasors. The finite-state recurrence falls into a cycle; when the cycle closes
+ * within the budget (-1.5 MHz / 10 MHz: after 21504 steps) every output is the
+ * reference's, bit for bit, forever. Otherwise outputs past the budget follow a drift
+ * model (the fitted mean step and renorm-period magnitude profile).
+ * Construction fails (NULL, orion_last_error) if TAU * freq_hz / fs is not finite. */
 orion_block* orion_rotator_new(float freq_hz, float fs);
-/* dsp/rotator.rs:35-39 Rotator::set_freq(freq_hz, fs): a new step phasor; the phase
- * continues from where it is (the reference keeps z). Synchronizes the device
- * (kernels in flight read the oscillator table). */
+/* dsp/rotator.rs:35-39 Rotator::set_freq(freq_hz, fs): a new step phasor; z and the
+ * renorm counter carry on (the reference keeps them). Synchronizes the device
+ * (kernels in flight read the oscillator table). ORION_E_ARG if TAU * freq_hz / fs is
+ * not finite (e.g. fs = 0: the reference would produce NaN forever). */
 int orion_rotator_set_freq(orion_block* b, float freq_hz, float fs);
+/* dsp/rotator.rs:44-68 Rotator::next / next_cs, n times: out[i] = the phasor after each
+ * step (cf32 pairs), advancing the same oscillator as rotate_block. Host buffer
+ * (synchronous) / device buffer. */
+int orion_rotator_next_cs_block(orion_block* b, void* out, size_t n);
+int orion_rotator_next_cs_block_device(orion_block* b, void* out_dev, size_t n, void* stream);
 /* dsp/rotator.rs:28-31 Rotator::reset_phase: phasor back to 1 + j0 (the step stays);
  * the same as orion_block_reset on a Rotator. */
 int orion_rotator_reset_phase(orion_block* b);
@@ -80,8 +100,15 @@ int orion_rotator_mix_usb_block(orion_block* b, const void* in, size_t n_in, flo
                                 orion_work_report* wr);
 int orion_rotator_mix_usb_block_device(orion_block* b, const void* in_dev, size_t n_in, float* out_dev, size_t out_cap,
                                        void* stream, orion_work_report* wr);
+/* Host only (no device; tests and diagnostics, no reference counterpart): the first n
+ * phasors of Rotator::new(freq_hz, fs) as the engine tabulates them with a budget of
+ * max_out outputs (the reference recurrence, its cycle, or the drift model past the
+ * budget) into out (cf32); cyc_len = 0 when no cycle closed within the budget. */
+int orion_osc_table_phasors(float freq_hz, float fs, uint64_t max_out, void* out, size_t n, uint64_t* cyc_start,
+                            uint64_t* cyc_len, uint64_t* n_tab);
 /* dsp/nco.rs:20-31 Nco::new(freq_hz, fs) as a block: process = mix_with_nco per sample
- * (nco.rs:63-66, the non-FMA product (x.re c - x.im s, x.re s + x.im c)). cf32->cf32 */
+ * (nco.rs:63-66, the non-FMA product (x.re c - x.im s, x.re s + x.im c)). cf32->cf32
+ * The oscillator tracks the reference recurrence (nco.rs:42-58) as the Rotator's does. */
 orion_block* orion_nco_new(float freq_hz, float fs);
 /* dsp/nco.rs:33-38 Nco::set_freq(freq_hz) (fs from orion_nco_new): the phase continues.
  * Synchronizes the device. */
@@ -101,6 +128,10 @@ orion_block* orion_fir_lowpass_new(float fs, float pass_hz, float trans_hz);
 orion_block* orion_fir_lowpass_iq_design(size_t num_taps, float cutoff_norm, float stopband_db);
 /* dsp/fir.rs:193-204 FirLowpassIq::from_taps(taps) (empty -> [1.0]). */
 orion_block* orion_fir_lowpass_iq_from_taps(const float* taps, size_t n);
+/* dsp/fir.rs:210-212 FirLowpassIq::num_taps, :216-218 group_delay = (num_taps - 1) / 2.
+ * ORION_E_TYPE if b is not a FirLowpassIq. */
+int orion_fir_lowpass_iq_num_taps(const orion_block* b, size_t* num_taps);
+int orion_fir_lowpass_iq_group_delay(const orion_block* b, size_t* group_delay);
 /* dsp/fir.rs:260-276 FirLowpassIq::filter_aligned(io) on device memory (resets state). */
 int orion_fir_lowpass_iq_filter_aligned_device(orion_block* b, void* io_dev, size_t n, void* stream);
 /* Host-memory variant of filter_aligned (synchronous). */
@@ -189,9 +220,9 @@ orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float*
  * cannot run on that path.
  * Residency: the segmented kernel launches one round of waves (at most the
  * device's resident capacity) and each segment waits, bounded, for the end state
- * its predecessor publishes. Predecessors are dispatched earlier except at the
- * seven XCD run boundaries, so a wait outlasts its bound only if other work holds
- * the CUs for longer than ~0.5 s; the handle then reports ORION_E_HIP (see
+ * its predecessor publishes. A predecessor is always the previous workgroup in
+ * dispatch order, so the wait ends even when other streams hold most CUs; a wait
+ * that still outlasts its bound (~0.5 s) makes the handle report ORION_E_HIP (see
  * orion_block_status) instead of returning the audio as valid. */
 #define ORION_WBFM_AUTO 0
 #define ORION_WBFM_SEGMENTED 1  /* one kernel, one round of segments (k_wbfm_seg) */
@@ -240,6 +271,9 @@ const char* orion_block_name(const orion_block* b);
                                    AM/CW demods): 0 single pass where the design allows (default), 1 the
                                    three-kernel scan */
 #define ORION_OPT_MOD_PASSES 2  /* FmPhaseAccumMod, SsbPhasingMod: 0 single pass (default), 3 three passes */
+#define ORION_OPT_NCO_TABLE 3   /* Rotator, Nco: outputs of the reference recurrence tabulated per (re)tune,
+                                   0 .. 2^28 (default 2^20; 0 = the closed-form ideal phasor of the f32 step).
+                                   The oscillator state carries on across the change. */
 int orion_block_configure(orion_block* b, int option, long long value);
 /* Designed coefficients, for parity tests: which = 0 primary taps, 1 audio taps. */
 int orion_block_taps(const orion_block* b, int which, float* out, size_t cap, size_t* n);

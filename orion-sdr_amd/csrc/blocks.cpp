@@ -1,11 +1,16 @@
 // blocks.cpp — Block implementations over the gfx950 kernels (host side).
 #include "blocks.hpp"
 
+#include "osc.hpp"
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 namespace orion {
 
@@ -60,6 +65,37 @@ uint32_t g_spin = kSpinDefault;
 uint32_t spin_limit() { return __atomic_load_n(&g_spin, __ATOMIC_RELAXED); }
 void set_spin_limit(uint32_t polls) { __atomic_store_n(&g_spin, polls, __ATOMIC_RELAXED); }
 
+namespace {
+std::mutex g_occ_mu;
+std::map<std::tuple<const void*, int, int>, int> g_occ;  // (kernel, threads, device) -> per CU
+std::map<int, int> g_cus;                                 // device -> CUs
+}  // namespace
+int resident_per_cu(const void* kernel, int threads) {
+  int dev = 0;
+  ORION_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(g_occ_mu);
+  const auto key = std::make_tuple(kernel, threads, dev);
+  auto it = g_occ.find(key);
+  if (it != g_occ.end()) return it->second;
+  int per_cu = 0;
+  ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0));
+  per_cu = std::max(1, per_cu);
+  g_occ.emplace(key, per_cu);
+  return per_cu;
+}
+int device_cus() {
+  int dev = 0;
+  ORION_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(g_occ_mu);
+  auto it = g_cus.find(dev);
+  if (it != g_cus.end()) return it->second;
+  int ncu = 0;
+  ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  ncu = std::max(1, ncu);
+  g_cus.emplace(dev, ncu);
+  return ncu;
+}
+
 WorkReport Block::process_host(const void* in, size_t n_in, void* out, size_t out_cap) {
   hipStream_t s = host_stream();
   const int nch = channels();
@@ -106,47 +142,34 @@ int padded_hist(int K) {
 }
 
 // ------------------------------------------------------ Rotator / Nco ----
-// The oscillator in closed form: after k steps the phasor is e^{j 2 pi ph(k) / 2^64},
-// ph(k) = base + k step (Q0.64, exact integer arithmetic), step = the exact angle of
-// the reference's f32 step phasor w (design.cpp oscillator). Retuning keeps the
-// phase (the reference keeps z and replaces w): base += k (step_old - step_new).
+// The oscillator (osc.hpp RefOsc): the reference's own phasor recurrence, tabulated
+// at every (re)tune — exact forever when it closes a cycle within the budget, else
+// for the budget's outputs, then the drift model; budget 0: the closed form.
 class OscBlock : public Block {
  public:
-  OscBlock(float f, float fs) : fs_(fs) { tune(f, fs); }
-  void reset() override {  // phasor back to 1 + 0j (Rotator::reset_phase, rotator.rs:28-31)
-    k_ = 0;
-    base_ = 0;
+  OscBlock(float f, float fs) : osc_(f, fs) {}
+  void reset() override { osc_.reset(); }  // phasor back to 1 + 0j (Rotator::reset_phase, rotator.rs:28-31)
+  std::vector<float> taps(int) const override { return {osc_.osc().w_re, osc_.osc().w_im}; }
+  void set_freq(float f, float fs) { osc_.retune(f, fs); }
+  float fs() const { return osc_.fs(); }
+  int configure(int option, long long value) override {
+    if (option != kOptNcoTable) return -4;
+    if (value < 0 || static_cast<unsigned long long>(value) > kNcoTableMax) return -3;
+    osc_.set_budget(static_cast<uint64_t>(value));
+    return 0;
   }
-  std::vector<float> taps(int) const override { return {osc_.w_re, osc_.w_im}; }
-  void set_freq(float f, float fs) {
-    const Oscillator o = oscillator(f, fs);
-    base_ += k_ * (osc_.step_q64 - o.step_q64);
-    ORION_HIP(hipDeviceSynchronize());  // kernels in flight may read the old table
-    tune(f, fs);
-  }
-  float fs() const { return fs_; }
   // One oscillator pass (launch_osc mode) over n samples, advancing the phase.
   void run(int mode, const void* in, void* out, size_t n, hipStream_t s) {
-    launch_osc(mode, static_cast<const f2*>(in), out, static_cast<long long>(n), k_, osc_.step_q64, base_,
-               tab_.as<f2>(), s);
-    k_ += n;
+    launch_osc(mode, static_cast<const f2*>(in), out, static_cast<long long>(n), osc_.count(), osc_.dev(), s);
+    osc_.advance(n);
   }
 
  private:
-  void tune(float f, float fs) {
-    osc_ = oscillator(f, fs);
-    fs_ = fs;
-    const auto tab = phasor_table(osc_.theta, kRotTile);
-    tab_.upload(tab.data(), tab.size() * sizeof(float));
-  }
-  float fs_;
-  Oscillator osc_{};
-  DevBuf tab_;
-  uint64_t k_ = 0, base_ = 0;
+  RefOsc osc_;
 };
 
-// dsp/rotator.rs:8-95: process = rotate_block (cf32 -> cf32); mix_usb_block on the
-// same phasor (osc_mix_usb).
+// dsp/rotator.rs:8-95: process = rotate_block (cf32 -> cf32); mix_usb_block and
+// next / next_cs on the same phasor (osc_mix_usb, osc_next_cs).
 class RotatorBlock final : public OscBlock {
  public:
   RotatorBlock(float f, float fs) : OscBlock(f, fs) {}
@@ -662,7 +685,9 @@ std::unique_ptr<Block> make_nco(float f, float fs) { return std::make_unique<Nco
 int osc_set_freq(Block* b, const char* kind, float f, float fs) {
   auto* o = dynamic_cast<OscBlock*>(b);
   if (!o || std::strcmp(b->name(), kind) != 0) return -4;
-  o->set_freq(f, fs > 0.0f ? fs : o->fs());
+  // Nco::set_freq keeps the fs it was built with (nco.rs:33-38); Rotator::set_freq takes
+  // one (rotator.rs:35-39): a non-finite step (fs = 0) is rejected (ORION_E_ARG).
+  o->set_freq(f, std::strcmp(kind, "Nco") == 0 ? o->fs() : fs);
   return 0;
 }
 int osc_reset_phase(Block* b) {
@@ -677,9 +702,9 @@ int osc_mix_usb(Block* b, const void* in, size_t n, float* out, hipStream_t s) {
   o->run(1, in, out, n, s);
   return 0;
 }
-int osc_next_cs(Block* b, void* out, size_t n, hipStream_t s) {
-  auto* o = dynamic_cast<NcoBlock*>(b);
-  if (!o) return -4;
+int osc_next_cs(Block* b, const char* kind, void* out, size_t n, hipStream_t s) {
+  auto* o = dynamic_cast<OscBlock*>(b);
+  if (!o || std::strcmp(b->name(), kind) != 0) return -4;
   o->run(3, nullptr, out, n, s);
   return 0;
 }

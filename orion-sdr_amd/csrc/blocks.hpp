@@ -21,7 +21,7 @@ namespace orion {
 
 enum class Dt : int { C32 = 0, F32 = 1 };
 // orion_block_configure options (include/orion_sdr_amd.h ORION_OPT_*).
-enum : int { kOptScanPath = 1, kOptModPasses = 2 };
+enum : int { kOptScanPath = 1, kOptModPasses = 2, kOptNcoTable = 3 };
 inline size_t dt_size(Dt d) { return d == Dt::C32 ? 8 : 4; }
 
 struct WorkReport {
@@ -96,13 +96,15 @@ std::unique_ptr<Block> make_rotator(float freq_hz, float fs);
 // dsp/nco.rs:11-66 (mix_with_nco per sample). C32 -> C32.
 std::unique_ptr<Block> make_nco(float freq_hz, float fs);
 // Oscillator controls (-4 if b is not of that kind): set_freq (Rotator: rotator.rs:35-39,
-// kind "Rotator"; Nco: nco.rs:33-38, kind "Nco", fs <= 0 keeps the block's fs), reset_phase
+// kind "Rotator"; Nco: nco.rs:33-38, kind "Nco", the block's own fs), reset_phase
 // (rotator.rs:28-31), mix_usb_block (rotator.rs:88-94, C32 -> F32 on device buffers) and
-// next_cs n times (nco.rs:42-58, C32 phasors on device buffers), asynchronous on s.
+// next / next_cs n times (rotator.rs:44-68 kind "Rotator", nco.rs:42-58 kind "Nco"; C32
+// phasors on device buffers), asynchronous on s. set_freq throws std::invalid_argument
+// for a non-finite step.
 int osc_set_freq(Block* b, const char* kind, float freq_hz, float fs);
 int osc_reset_phase(Block* b);
 int osc_mix_usb(Block* b, const void* in_dev, size_t n, float* out_dev, hipStream_t s);
-int osc_next_cs(Block* b, void* out_dev, size_t n, hipStream_t s);
+int osc_next_cs(Block* b, const char* kind, void* out_dev, size_t n, hipStream_t s);
 // dsp/decim.rs:10-77. C32 -> C32, out = ceil(n/m) (decimation phase restarts
 // every call, decim.rs:66-71 — reproduced).
 std::unique_ptr<Block> make_fir_decimator(float fs, size_t m, float cutoff_hz, float trans_hz,

@@ -6,8 +6,10 @@
 #include <exception>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "blocks.hpp"
+#include "osc.hpp"
 #include "scan_blocks.hpp"
 
 struct orion_block {
@@ -81,6 +83,44 @@ int orion_diag_stream_read(const void* dev, size_t bytes, void* stream) {
     return ORION_OK;
   });
 }
+int orion_device_cus(void) {
+  try {
+    return orion::device_cus();
+  } catch (const std::exception& e) {
+    return fail(ORION_E_HIP, e.what());
+  }
+}
+int orion_diag_spin(void* stream, uint32_t workgroups, uint32_t lds_bytes, double seconds) {
+  return guarded([&] {
+    orion::launch_spin(static_cast<int>(workgroups), static_cast<int>(lds_bytes), seconds,
+                       static_cast<hipStream_t>(stream));
+    return ORION_OK;
+  });
+}
+void* orion_diag_stream_create(uint32_t n_cus) {
+  hipStream_t st = nullptr;
+  try {
+    if (n_cus == 0) {
+      ORION_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    } else {
+      const int ncu = orion::device_cus();
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+      for (uint32_t c = 0; c < n_cus && c < static_cast<uint32_t>(ncu); ++c) mask[c / 32] |= 1u << (c % 32);
+      ORION_HIP(hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(mask.size()), mask.data()));
+    }
+  } catch (const std::exception& e) {
+    fail(ORION_E_HIP, e.what());
+    return nullptr;
+  }
+  return st;
+}
+int orion_diag_stream_destroy(void* stream) {
+  if (!stream) return fail(ORION_E_NULL, "null stream");
+  return guarded([&] {
+    ORION_HIP(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+    return ORION_OK;
+  });
+}
 int orion_synchronize(void* stream) {
   return guarded([&] {
     ORION_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
@@ -144,25 +184,37 @@ int orion_nco_set_freq(orion_block* b, float freq_hz) {
     return ORION_OK;
   });
 }
-int orion_nco_next_cs_block_device(orion_block* b, void* out, size_t n, void* stream) {
+namespace {
+int next_cs_device(orion_block* b, const char* kind, void* out, size_t n, void* stream) {
   if (!b) return fail(ORION_E_NULL, "null handle");
   if (!out && n) return fail(ORION_E_NULL, "null buffer");
   return guarded([&] {
-    if (orion::osc_next_cs(b->impl.get(), out, n, static_cast<hipStream_t>(stream))) return fail(ORION_E_TYPE, "not an Nco");
+    b->impl->check_device_errors();
+    if (orion::osc_next_cs(b->impl.get(), kind, out, n, static_cast<hipStream_t>(stream)))
+      return fail(ORION_E_TYPE, "wrong oscillator kind");
     return ORION_OK;
   });
 }
-int orion_nco_next_cs_block(orion_block* b, void* out, size_t n) {
+int next_cs_host(orion_block* b, const char* kind, void* out, size_t n) {
   if (!b) return fail(ORION_E_NULL, "null handle");
   if (!out && n) return fail(ORION_E_NULL, "null buffer");
   return guarded([&] {
     orion::DevBuf d(n * 8 + 16);
-    if (orion::osc_next_cs(b->impl.get(), d.as<void>(), n, nullptr)) return fail(ORION_E_TYPE, "not an Nco");
+    if (orion::osc_next_cs(b->impl.get(), kind, d.as<void>(), n, nullptr)) return fail(ORION_E_TYPE, "wrong oscillator kind");
     if (n) ORION_HIP(hipMemcpy(out, d.as<void>(), n * 8, hipMemcpyDeviceToHost));
     ORION_HIP(hipDeviceSynchronize());
     return ORION_OK;
   });
 }
+}  // namespace
+int orion_nco_next_cs_block_device(orion_block* b, void* out, size_t n, void* stream) {
+  return next_cs_device(b, "Nco", out, n, stream);
+}
+int orion_nco_next_cs_block(orion_block* b, void* out, size_t n) { return next_cs_host(b, "Nco", out, n); }
+int orion_rotator_next_cs_block_device(orion_block* b, void* out, size_t n, void* stream) {
+  return next_cs_device(b, "Rotator", out, n, stream);
+}
+int orion_rotator_next_cs_block(orion_block* b, void* out, size_t n) { return next_cs_host(b, "Rotator", out, n); }
 orion_block* orion_fir_decimator_new(float fs, size_t m, float cutoff_hz, float trans_hz) {
   return make([&] { return orion::make_fir_decimator(fs, m, cutoff_hz, trans_hz, 1); });
 }
@@ -177,6 +229,38 @@ orion_block* orion_fir_lowpass_iq_design(size_t num_taps, float cutoff_norm, flo
 }
 orion_block* orion_fir_lowpass_iq_from_taps(const float* taps, size_t n) {
   return make([&] { return orion::make_fir_lowpass_iq(std::vector<float>(taps, taps + (taps ? n : 0))); });
+}
+int orion_osc_table_phasors(float freq_hz, float fs, uint64_t max_out, void* out, size_t n, uint64_t* cyc_start,
+                            uint64_t* cyc_len, uint64_t* n_tab) {
+  if (!out && n) return fail(ORION_E_NULL, "null buffer");
+  return guarded([&] {
+    if (max_out > orion::kNcoTableMax) return fail(ORION_E_ARG, "budget above 2^28");
+    const orion::Oscillator o = orion::oscillator(freq_hz, fs);
+    const orion::RecTable t = orion::rec_table(o.w_re, o.w_im, orion::RecState{}, max_out, orion::kRotTile, o.step_q64);
+    float* z = static_cast<float*>(out);
+    for (size_t k = 0; k < n; ++k) {
+      const orion::RecState st = orion::rec_state_after(t, k);
+      z[2 * k] = st.zr;
+      z[2 * k + 1] = st.zi;
+    }
+    if (cyc_start) *cyc_start = t.cyc_start;
+    if (cyc_len) *cyc_len = t.cyc_len;
+    if (n_tab) *n_tab = t.n;
+    return ORION_OK;
+  });
+}
+int orion_fir_lowpass_iq_num_taps(const orion_block* b, size_t* n) {
+  if (!b || !n) return fail(ORION_E_NULL, "null argument");
+  if (std::strcmp(b->impl->name(), "FirLowpassIq") != 0) return fail(ORION_E_TYPE, "not a FirLowpassIq");
+  *n = b->impl->taps(0).size();  // fir.rs:210-212 taps.len()
+  return ORION_OK;
+}
+int orion_fir_lowpass_iq_group_delay(const orion_block* b, size_t* d) {
+  size_t n = 0;
+  const int rc = orion_fir_lowpass_iq_num_taps(b, &n);
+  if (rc) return rc;
+  *d = (n - 1) / 2;  // fir.rs:216-218 (taps.len() - 1) / 2; from_taps keeps len >= 1
+  return ORION_OK;
 }
 int orion_fir_lowpass_iq_filter_aligned_device(orion_block* b, void* io, size_t n, void* stream) {
   if (!b || (!io && n)) return fail(ORION_E_NULL, "null argument");

@@ -5,6 +5,8 @@
 
 #include <cfloat>
 #include <cmath>
+#include <cstring>
+#include <unordered_map>
 
 namespace orion {
 
@@ -147,6 +149,153 @@ std::vector<float> phasor_table(double theta, size_t n) {
     t[2 * k + 1] = static_cast<float>(std::sin(a));
   }
   return t;
+}
+
+// ---- the reference's phasor recurrence -----------------------------------------
+uint64_t q64_of_angle(long double rad) {
+  constexpr long double kTwoPi = 6.283185307179586476925286766559005768L;
+  long double rev = std::fmod(rad / kTwoPi, 1.0L);
+  if (rev < 0) rev += 1.0L;
+  long double scaled = rev * 18446744073709551616.0L;  // 2^64
+  if (scaled >= 18446744073709551616.0L) scaled -= 18446744073709551616.0L;
+  return static_cast<uint64_t>(scaled);
+}
+
+namespace {
+// One reference step (rotator.rs:44-62; nco.rs:42-58 is the same): Rust's mul_add is
+// a fused multiply-add, the products, the norm and 1/sqrt are plain f32 operations.
+template <class Fma>
+inline void rec_step(RecState& s, float wr, float wi, Fma fma) {
+  const float zr = fma(s.zr, wr, -s.zi * wi);
+  const float zi = fma(s.zi, wr, s.zr * wi);
+  s.zr = zr;
+  s.zi = zi;
+  s.ctr += 1u;
+  if ((s.ctr & 0x3FFu) == 0) {
+    const float r2 = s.zr * s.zr + s.zi * s.zi;
+    const float inv = 1.0f / std::sqrt(r2);
+    s.zr *= inv;
+    s.zi *= inv;
+  }
+}
+inline uint64_t state_key(const RecState& s) {
+  uint32_t a, b;
+  std::memcpy(&a, &s.zr, 4);
+  std::memcpy(&b, &s.zi, 4);
+  return (static_cast<uint64_t>(a) << 32) | b;
+}
+// The run: outputs into z until max_out or the first repeated renorm-point state.
+// Returns the step count of the earlier occurrence (cycle start) or UINT64_MAX.
+template <class Fma>
+uint64_t rec_run(float wr, float wi, RecState s, uint64_t max_out, std::vector<float>& z, Fma fma) {
+  std::unordered_map<uint64_t, uint64_t> seen;
+  seen.reserve(static_cast<size_t>(std::min<uint64_t>(max_out / 1024 + 2, 1u << 20)));
+  if ((s.ctr & 0x3FFu) == 0) seen.emplace(state_key(s), 0);
+  for (uint64_t k = 0; k < max_out; ++k) {
+    rec_step(s, wr, wi, fma);
+    z.push_back(s.zr);
+    z.push_back(s.zi);
+    if ((s.ctr & 0x3FFu) == 0) {
+      const auto ins = seen.emplace(state_key(s), k + 1);
+      if (!ins.second) return ins.first->second;
+    }
+  }
+  return UINT64_MAX;
+}
+__attribute__((target("fma"))) uint64_t rec_run_hw(float wr, float wi, RecState s, uint64_t max_out,
+                                                   std::vector<float>& z) {
+  return rec_run(wr, wi, s, max_out, z, [](float a, float b, float c) { return __builtin_fmaf(a, b, c); });
+}
+uint64_t rec_run_sw(float wr, float wi, RecState s, uint64_t max_out, std::vector<float>& z) {
+  return rec_run(wr, wi, s, max_out, z, [](float a, float b, float c) { return std::fma(a, b, c); });
+}
+}  // namespace
+
+RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t min_cycle, uint64_t step_q64) {
+  RecTable t;
+  t.ctr0 = s0.ctr;
+  t.mstep = step_q64;
+  t.z.reserve(static_cast<size_t>(2 * std::min<uint64_t>(max_out, 1u << 22)));
+  const uint64_t c0 = __builtin_cpu_supports("fma") ? rec_run_hw(wr, wi, s0, max_out, t.z)
+                                                    : rec_run_sw(wr, wi, s0, max_out, t.z);
+  t.n = t.z.size() / 2;
+  if (c0 != UINT64_MAX) {  // outputs c0 .. n-1 repeat forever
+    t.cyc_start = c0;
+    t.cyc_len = t.n - c0;
+    const uint64_t period = t.cyc_len;
+    while (t.cyc_len < min_cycle) {  // unroll
+      for (uint64_t k = 0; k < period; ++k) {
+        t.z.push_back(t.z[2 * (c0 + k)]);
+        t.z.push_back(t.z[2 * (c0 + k) + 1]);
+      }
+      t.cyc_len += period;
+    }
+    t.n = t.z.size() / 2;
+    return t;
+  }
+  // No cycle within the budget: outputs beyond n follow a model anchored at the last
+  // exact output: its phase, plus the mean step fitted (least squares over the renorm
+  // points of the run's last 7/8) and the mean magnitude by renorm-counter position.
+  t.prof.assign(1024, 1.0f);
+  if (t.n == 0) {
+    t.mbase = q64_of_angle(std::atan2(static_cast<long double>(s0.zi), static_cast<long double>(s0.zr)));
+    return t;
+  }
+  const long double th = std::atan2(static_cast<long double>(wi), static_cast<long double>(wr));
+  const long double a0 = std::atan2(static_cast<long double>(s0.zi), static_cast<long double>(s0.zr));
+  const uint64_t from = t.n / 8;
+  std::vector<double> msum(1024, 0.0);
+  std::vector<uint64_t> mcnt(1024, 0);
+  long double sx = 0, sy = 0, sxx = 0, sxy = 0;
+  uint64_t np = 0;
+  constexpr long double kTwoPi = 6.283185307179586476925286766559005768L;
+  for (uint64_t k = from; k < t.n; ++k) {
+    const double re = t.z[2 * k], im = t.z[2 * k + 1];
+    const uint32_t j = (t.ctr0 + static_cast<uint32_t>(k) + 1u) & 1023u;
+    msum[j] += std::sqrt(re * re + im * im);
+    mcnt[j] += 1;
+    if (j == 0) {  // drift of the phase against the closed form at this renorm point
+      const long double ideal = std::fmod(a0 + static_cast<long double>(k + 1) * th, kTwoPi);
+      long double e = std::atan2(static_cast<long double>(im), static_cast<long double>(re)) - ideal;
+      e = std::remainder(e, kTwoPi);
+      const long double x = static_cast<long double>(k + 1);
+      sx += x;
+      sy += e;
+      sxx += x * x;
+      sxy += x * e;
+      ++np;
+    }
+  }
+  for (int j = 0; j < 1024; ++j)
+    if (mcnt[j]) t.prof[j] = static_cast<float>(msum[j] / static_cast<double>(mcnt[j]));
+  long double slope = 0;
+  if (np >= 8) {
+    const long double den = static_cast<long double>(np) * sxx - sx * sx;
+    if (den > 0) slope = (static_cast<long double>(np) * sxy - sx * sy) / den;
+  }
+  t.mstep = q64_of_angle(th + slope);
+  const uint64_t l = t.n - 1;
+  t.mbase = q64_of_angle(std::atan2(static_cast<long double>(t.z[2 * l + 1]), static_cast<long double>(t.z[2 * l])));
+  return t;
+}
+
+RecState rec_state_after(const RecTable& t, uint64_t k) {
+  RecState s;
+  s.ctr = t.ctr0 + static_cast<uint32_t>(k) + 1u;
+  uint64_t j = k;
+  if (t.cyc_len && j >= t.n) j = t.cyc_start + (j - t.cyc_start) % t.cyc_len;
+  if (j < t.n) {
+    s.zr = t.z[2 * j];
+    s.zi = t.z[2 * j + 1];
+    return s;
+  }
+  constexpr long double kTwoPi = 6.283185307179586476925286766559005768L;
+  const uint64_t ph = t.mbase + (k + 1 - t.n) * t.mstep;
+  const long double a = static_cast<long double>(ph) / 18446744073709551616.0L * kTwoPi;
+  const long double m = t.prof.empty() ? 1.0L : static_cast<long double>(t.prof[s.ctr & 1023u]);
+  s.zr = static_cast<float>(m * std::cos(a));
+  s.zi = static_cast<float>(m * std::sin(a));
+  return s;
 }
 
 // ---- state-space extraction -------------------------------------------------

@@ -45,6 +45,39 @@ Oscillator oscillator(float freq_hz, float fs);
 // Phasor e^{j*theta*k} for k = 0..n-1, computed in f64 and rounded to f32 pairs.
 std::vector<float> phasor_table(double theta, size_t n);
 
+// ---- the reference's phasor recurrence (rotator.rs:44-62, nco.rs:42-58) ----------
+// z <- (fma(z.re, w.re, -(z.im w.im)), fma(z.im, w.re, z.re w.im)) in f32, then when
+// (++ctr & 0x3FF) == 0, z *= 1/sqrt(re^2 + im^2). A finite-state map: renormalised,
+// z stays in a thin annulus, so the trajectory is eventually periodic. Sampled at
+// the renorm points (where the state is z alone), the period is often short
+// (-1.5 MHz / 10 MHz: 16 renorms of tail, then a cycle of 5 renorms = 5120 steps),
+// and then a table of tail + cycle reproduces the reference bit for bit forever.
+struct RecState {
+  float zr = 1.0f, zi = 0.0f;  // the phasor (Rotator::z / Nco::z)
+  uint32_t ctr = 0;            // renorm_ctr
+};
+struct RecTable {
+  std::vector<float> z;        // exact outputs k < n: the phasor after k + 1 steps (re, im)
+  uint64_t n = 0;
+  uint64_t cyc_start = 0;      // cyc_len > 0: output k >= n equals output
+  uint64_t cyc_len = 0;        //   cyc_start + (k - cyc_start) mod cyc_len
+  // beyond n when there is no cycle (a model of the drift, not the reference):
+  uint64_t mbase = 0;          // Q0.64 phase of output n - 1 (the last exact one)
+  uint64_t mstep = 0;          // fitted mean step: phase(k) = mbase + (k + 1 - n) mstep
+  std::vector<float> prof;     // 1024 mean magnitudes by (ctr0 + k + 1) & 1023
+  uint32_t ctr0 = 0;           // renorm_ctr of the start state
+};
+// Runs the recurrence with step (wr, wi) from s0 for at most max_out outputs,
+// detecting a cycle at the renorm points; a cycle shorter than min_cycle outputs is
+// unrolled (replicated) to at least min_cycle, so a kernel wraps a tile with one
+// subtraction. step_q64: the closed-form step (the model's starting estimate).
+RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t min_cycle, uint64_t step_q64);
+// The phasor of output k of a table (exact, or the model beyond it) and the state
+// after output k (for set_freq: the reference keeps z and renorm_ctr).
+RecState rec_state_after(const RecTable& t, uint64_t k);
+// Q0.64 fraction of a turn of an angle in radians.
+uint64_t q64_of_angle(long double rad);
+
 // multicarrier/tx_lowpass.rs:88-185 TxLowpass: the spec and its sizing helpers (f32
 // arithmetic as the reference). filter() is FirLowpassIq::design(num_taps, cutoff, stopband).
 struct TxLowpassSpec { float cutoff_norm; size_t num_taps; float stopband_db; };

@@ -198,6 +198,13 @@ __device__ __forceinline__ float pm_disc(f2 z, f2 p, float k) {
 
 inline int div_up(long long a, long long b) { return static_cast<int>((a + b - 1) / b); }
 
+// Resident workgroups per CU of `kernel` at `threads` per workgroup, and the CU
+// count, of the CURRENT device; cached per (kernel, device) under a lock: segment and
+// one-round geometries are sized from them, so they must not leak across devices
+// with different CU counts or be torn by two first launches racing.
+int resident_per_cu(const void* kernel, int threads);
+int device_cus();
+
 // Cross-workgroup waits (WBFM segment hand-offs, decoupled look-backs) poll a flag
 // at most spin_limit() times before they give up and set the handle's device error
 // word (blocks.hpp Block::dev_err). Process-wide; orion_debug_set_spin_limit sets

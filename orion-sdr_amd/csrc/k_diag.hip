@@ -41,7 +41,31 @@ __global__ __launch_bounds__(64) void k_stream_read(const f4* __restrict__ x, lo
   (void)n4;
 }
 
+// Occupancy holder for residency tests: every workgroup sleeps until `ticks` of the
+// constant wall clock have passed since it started, holding its waves and its
+// dynamic LDS (which sets how many fit on a CU). Every wave reaches the exit.
+__global__ __launch_bounds__(64) void k_spin(long long ticks) {
+  extern __shared__ float hold[];
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+  hold[threadIdx.x] = 0.0f;
+}
+
 }  // namespace
+
+void launch_spin(int workgroups, int lds_bytes, double seconds, hipStream_t s) {
+  int dev = 0, khz = 0;
+  ORION_HIP(hipGetDevice(&dev));
+  ORION_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  if (khz <= 0 || workgroups < 1 || lds_bytes < 256 || lds_bytes > 160 * 1024 || !(seconds >= 0.0 && seconds <= 10.0))
+    throw HipError("spin: bad arguments");
+  const long long ticks = static_cast<long long>(seconds * 1e3 * khz);
+  if (lds_bytes > 64 * 1024)
+    ORION_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_spin), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  lds_bytes));
+  k_spin<<<workgroups, 64, static_cast<size_t>(lds_bytes), s>>>(ticks);
+  ORION_LAUNCH_CHECK();
+}
 
 long long stream_read_bytes(long long bytes) {
   const long long per_wave = static_cast<long long>(kDiagTile) * 16;

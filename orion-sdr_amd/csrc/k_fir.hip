@@ -16,32 +16,48 @@ constexpr int NT = 256;
 constexpr int kMaxGrid = 2048;  // memory-bound: cap and grid-stride (2048 = 8 WG per CU)
 
 // ------------------------------------------------------------------ NCO --
-// Output i of a call uses the oscillator phasor after k0 + i + 1 steps (the
-// reference's next() returns the post-multiply phasor, rotator.rs:44-62), of phase
-// base + (k0 + i + 1) step (Q0.64; base moves when the frequency is retuned, so the
-// phase continues). MODE: kRotate rotate_block (FMA form, rotator.rs:80-83), kUsb
-// mix_usb_block (cf32 -> f32, rotator.rs:88-94), kNcoMix mix_with_nco (non-FMA
-// product, nco.rs:63-66), kNcoGen the phasors themselves (nco.rs:42-58, no input).
+// Output i of a call is oscillator output k = k0 + i (kernels.hpp OscDev): the
+// reference's own phasor from the exact table (tail + unrolled cycle, or the exact
+// prefix), or beyond it the model (the closed form when there is no table). MODE:
+// kRotate rotate_block (FMA form, rotator.rs:80-83), kUsb mix_usb_block (cf32 -> f32,
+// rotator.rs:88-94), kNcoMix mix_with_nco (non-FMA product, nco.rs:63-66), kNcoGen
+// the phasors themselves (nco.rs:42-58 next_cs, no input).
 enum : int { kRotate = 0, kUsb = 1, kNcoMix = 2, kNcoGen = 3 };
 template <bool A16, int MODE>
-__global__ __launch_bounds__(NT) void k_rotator(const f2* __restrict__ x, void* __restrict__ yv,
-                                                long long n, uint64_t k0, uint64_t step, uint64_t base,
-                                                const f2* __restrict__ tab) {
+__global__ __launch_bounds__(NT) void k_rotator(const f2* __restrict__ x, void* __restrict__ yv, long long n,
+                                                uint64_t k0, const OscDev o) {
   constexpr int PER = kRotTile / (2 * NT);  // pairs per thread per tile (8)
   const int t = threadIdx.x;
-  f2 tb[PER][2];
+  f2 tb[PER][2];  // model steps e^{j 2 pi p mstep}, p = 2t + 2 NT i (+1): tile-invariant
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const f4 v = *reinterpret_cast<const f4*>(tab + 2 * t + 2 * NT * i);
+    const f4 v = *reinterpret_cast<const f4*>(o.mtab + 2 * t + 2 * NT * i);
     tb[i][0] = f2{v.x, v.y};
     tb[i][1] = f2{v.z, v.w};
   }
+  const bool cyc = o.cyc_len != 0;
   for (long long tile = static_cast<long long>(blockIdx.x) * kRotTile; tile < n;
        tile += static_cast<long long>(gridDim.x) * kRotTile) {
-    const f2 S = phasor_at(base + (k0 + static_cast<uint64_t>(tile) + 1) * step);
+    const uint64_t kt = k0 + static_cast<uint64_t>(tile);  // output index of the tile's first sample
+    // tile-uniform: every sample from the table (kind 0), none (1), or mixed (2)
+    const int kind = (cyc || kt + kRotTile <= o.n_tab) ? 0 : (kt >= o.n_tab ? 1 : 2);
+    uint64_t jt = kt;  // table index of kt (cycle: wrapped; a tile wraps at most once)
+    if (cyc && kt >= o.n_tab) jt = o.cyc_start + (kt - o.cyc_start) % o.cyc_len;
+    const f2 S = kind != 0 ? phasor_at(o.mbase + (kt + 1 - o.n_tab) * o.mstep) : f2{1.0f, 0.0f};
+    auto phasor = [&](int off, f2 tbv) -> f2 {  // off < kRotTile: the sample's offset in the tile
+      if (kind == 0 || (kind == 2 && kt + off < o.n_tab)) {
+        uint64_t j = jt + off;
+        if (cyc && j >= o.n_tab) j -= o.cyc_len;
+        return o.tab[j];
+      }
+      f2 p = cmul(S, tbv);
+      if (o.prof) p *= splat2(o.prof[(o.ctr0 + static_cast<uint32_t>(kt) + off + 1u) & 1023u]);
+      return p;
+    };
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const long long P = tile + 2 * t + 2 * NT * i;
+      const int off = 2 * t + 2 * NT * i;
+      const long long P = tile + off;
       if (P >= n) break;
       f2 v0 = f2{0.0f, 0.0f}, v1 = f2{0.0f, 0.0f};
       const bool full = P + 1 < n;
@@ -55,8 +71,8 @@ __global__ __launch_bounds__(NT) void k_rotator(const f2* __restrict__ x, void* 
           if (full) v1 = x[P + 1];
         }
       }
-      const f2 p0 = cmul(S, tb[i][0]);
-      const f2 p1 = cmul(S, tb[i][1]);
+      const f2 p0 = phasor(off, tb[i][0]);
+      const f2 p1 = phasor(off + 1, tb[i][1]);
       if constexpr (MODE == kUsb) {
         float* y = static_cast<float*>(yv);
         y[P] = __builtin_fmaf(v0.x, p0.x, v0.y * p0.y);
@@ -657,15 +673,15 @@ inline int grid_for(long long work, int per_block) {
 
 }  // namespace
 
-void launch_osc(int mode, const f2* x, void* y, long long n, uint64_t k0, uint64_t step, uint64_t base,
-                const f2* tab, hipStream_t s) {
+void launch_osc(int mode, const f2* x, void* y, long long n, uint64_t k0, const OscDev& o, hipStream_t s) {
   if (n <= 0) return;
+  if (o.cyc_len != 0 && o.cyc_len < static_cast<uint64_t>(kRotTile)) throw HipError("osc: cycle shorter than a tile");
   const int grid = grid_for(n, kRotTile);
   const bool a16 = (mode == kNcoGen || reinterpret_cast<uintptr_t>(x) % 16 == 0) &&
                    (mode == kUsb || reinterpret_cast<uintptr_t>(y) % 16 == 0);
 #define ORION_OSC(MD)                                                                          \
-  if (a16) k_rotator<true, MD><<<grid, NT, 0, s>>>(x, y, n, k0, step, base, tab);            \
-  else k_rotator<false, MD><<<grid, NT, 0, s>>>(x, y, n, k0, step, base, tab);
+  if (a16) k_rotator<true, MD><<<grid, NT, 0, s>>>(x, y, n, k0, o);                          \
+  else k_rotator<false, MD><<<grid, NT, 0, s>>>(x, y, n, k0, o);
   switch (mode) {
     case kRotate: ORION_OSC(kRotate) break;
     case kUsb: ORION_OSC(kUsb) break;
@@ -674,9 +690,6 @@ void launch_osc(int mode, const f2* x, void* y, long long n, uint64_t k0, uint64
   }
 #undef ORION_OSC
   ORION_LAUNCH_CHECK();
-}
-void launch_rotator(const f2* x, f2* y, long long n, uint64_t k0, uint64_t step, const f2* tab, hipStream_t s) {
-  launch_osc(kRotate, x, y, n, k0, step, 0, tab, s);
 }
 
 void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* hist, int hist_len,
@@ -687,14 +700,8 @@ void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* 
   // M = 8 with 129..256 taps (C3): k_decim_w4q, four waves per workgroup sharing one
   // tap table (three waves per SIMD); M = 8 with <= 128 taps: k_decim_w4.
   if (M == 8 && K > 128 && K <= 256 && hist_len >= 8 * 32) {
-    static int capq = 0;
-    if (capq == 0) {
-      int per_cu = 0, dev = 0, ncu = 0;
-      ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decim_w4q<32, true, false>, 256, 0));
-      ORION_HIP(hipGetDevice(&dev));
-      ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-      capq = std::max(1, per_cu) * 4 * std::max(1, ncu);  // waves
-    }
+    const int capq =
+        resident_per_cu(reinterpret_cast<const void*>(k_decim_w4q<32, true, false>), 256) * 4 * device_cus();  // waves
     const long long tiles_ch = (n_out + 127) / 128;
     const long long N = (tiles_ch * nch + capq - 1) / capq;  // tiles per wave
     const long long L = N * 128;
@@ -714,14 +721,8 @@ void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* 
     return;
   }
   if (M == 8 && K <= 256 && hist_len >= 8 * (K <= 128 ? 16 : 32)) {
-    static int cap = 0;
-    if (cap == 0) {
-      int per_cu = 0, dev = 0, ncu = 0;
-      ORION_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decim_w4<32, true, false>, 64, 0));
-      ORION_HIP(hipGetDevice(&dev));
-      ORION_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-      cap = std::max(4, per_cu & ~3) * std::max(1, ncu);  // a multiple of 4 per CU: balanced SIMDs
-    }
+    const int cap = std::max(4, resident_per_cu(reinterpret_cast<const void*>(k_decim_w4<32, true, false>), 64) & ~3) *
+                    device_cus();  // a multiple of 4 per CU: balanced SIMDs
     const long long tiles_ch = (n_out + 127) / 128;
     long long N = (tiles_ch * nch + cap - 1) / cap;
     N = (N + 1) & ~1LL;  // tiles per wave, even

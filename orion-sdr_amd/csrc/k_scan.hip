@@ -720,18 +720,26 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   }
   __syncthreads();
   constexpr int WR = 64 * SC;  // elements per wave
+  static_assert(WARM <= WR, "xcorr: lane 0 of a wave w > 0 must sit past the LP4 warm-up");
   const double rd = static_cast<double>(r);
   // the x_prev correction of wave w's pairs (lane 0 of a wave holds a valid sample iff
   // the wave does: its first element is past the warm-up)
   auto xcorr = [&](int w) -> double { return (w > 0 && w * WR < cnt) ? static_cast<double>(xlast[w - 1]) : 0.0; };
+  // r^(v - 1) from a pair's multiplier r^v over v >= 1 valid samples. r = 0 is a real
+  // design (dc.rs:17 / iir.rs:122 clamp a cut >= fs / 2 pi to 0): then only y_0 sees x_prev.
+  auto over_r = [&](double mprod, int v) -> double { return rd != 0.0 ? mprod / rd : (v == 1 ? 1.0 : 0.0); };
   {
     const double xw = xcorr(wave);
-    di -= xw * mi / rd;
+    if (xw != 0.0) di -= xw * over_r(mi, min((lane + 1) * C, cnt - wave * WR));
     if (xcross) xprev0 = static_cast<float>(xw);
   }
+  auto wave_pair_d = [&](int w) -> double {
+    const double xw = xcorr(w);
+    return xw != 0.0 ? dtot[w][1] - xw * over_r(dtot[w][0], min(WR, cnt - w * WR)) : dtot[w][1];
+  };
   double wm = 1.0, wd = 0.0;  // pairs of the waves before this one
   for (int w = 0; w < wave; ++w) {
-    double m2 = dtot[w][0], d2 = dtot[w][1] - xcorr(w) * dtot[w][0] / rd;
+    double m2 = dtot[w][0], d2 = wave_pair_d(w);
     dc_combine(wm, wd, m2, d2);
     wm = m2;
     wd = d2;
@@ -739,7 +747,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void 
   if (wave == 0) {  // chunk aggregate, look-back (one wave, 64 predecessors per step), prefix
     double bm = 1.0, bd = 0.0;
     for (int w = 0; w < 4; ++w) {
-      double m2 = dtot[w][0], d2 = dtot[w][1] - xcorr(w) * dtot[w][0] / rd;
+      double m2 = dtot[w][0], d2 = wave_pair_d(w);
       dc_combine(bm, bd, m2, d2);
       bm = m2;
       bd = d2;

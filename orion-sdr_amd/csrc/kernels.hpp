@@ -39,15 +39,27 @@ int fm_mod_rtab_len();
 void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, uint64_t* sums,
                    const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
                    hipStream_t s);
-void launch_rotator(const f2* x_dev, f2* y_dev, long long n, uint64_t k0, uint64_t step_q64,
-                    const f2* tab_dev, hipStream_t s);
-// Oscillator blocks (k_fir.hip k_rotator): output i uses the phasor of phase
-// base + (k0 + i + 1) step (Q0.64). mode: 0 Rotator::rotate_block (rotator.rs:74-85,
-// cf32 -> cf32), 1 Rotator::mix_usb_block (rotator.rs:88-94, cf32 -> f32), 2
-// mix_with_nco (nco.rs:63-66, cf32 -> cf32, non-FMA), 3 Nco::next_cs (nco.rs:42-58,
-// no input, cf32 phasors out).
-void launch_osc(int mode, const f2* x_dev, void* y_dev, long long n, uint64_t k0, uint64_t step_q64, uint64_t base,
-                const f2* tab_dev, hipStream_t s);
+// Oscillator on the device (k_fir.hip k_rotator; design.hpp RecTable). Output k of
+// the oscillator (k steps after the table's start state; the phasor after k + 1 steps):
+//   tab[k]                                            k < n_tab (the reference's own)
+//   tab[cyc_start + (k - cyc_start) mod cyc_len]      cyc_len > 0 (its cycle, forever)
+//   prof[(ctr0 + k + 1) & 1023] e^{j 2 pi ph / 2^64}, ph = mbase + (k + 1 - n_tab) mstep
+//                                                     otherwise (the model; prof null:
+//                                                     magnitude 1 — the closed form)
+// mtab: e^{j 2 pi p mstep / 2^64}, p < kRotTile (the model within a tile).
+// cyc_len is 0 or >= kRotTile (rec_table unrolls short cycles).
+struct OscDev {
+  const f2* tab;
+  const float* prof;
+  const f2* mtab;
+  uint64_t n_tab, cyc_start, cyc_len, mbase, mstep;
+  uint32_t ctr0;
+};
+// Oscillator blocks (k_fir.hip k_rotator): output i of a call is oscillator output
+// k0 + i. mode: 0 Rotator::rotate_block (rotator.rs:74-85, cf32 -> cf32), 1
+// Rotator::mix_usb_block (rotator.rs:88-94, cf32 -> f32), 2 mix_with_nco (nco.rs:63-66,
+// cf32 -> cf32, non-FMA), 3 Nco::next_cs / Rotator::next (no input, cf32 phasors out).
+void launch_osc(int mode, const f2* x_dev, void* y_dev, long long n, uint64_t k0, const OscDev& o, hipStream_t s);
 
 // ---------------------------------------------------------- FIR family --
 // Decimating FIR at the kept outputs only: out[j] = sum_k g[k] * x[M*j - k],
@@ -157,9 +169,11 @@ long long wbfm_seg_slots(long long n_dec, int nch);
 void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFusedConst& b, int nch,
                      int max_segments, hipStream_t s);
 
-int device_cus();
 // On-box bandwidth probe (k_diag.hip): a streaming read of the first
 // stream_read_bytes(bytes) bytes of x (16-B aligned) with the WBFM front's load shape.
 long long stream_read_bytes(long long bytes);
 void launch_stream_read(const void* x, long long bytes, float* sink, hipStream_t s);
+// Residency tests: `workgroups` one-wave workgroups holding lds_bytes of LDS each for
+// `seconds` of wall clock (bounded; every wave exits).
+void launch_spin(int workgroups, int lds_bytes, double seconds, hipStream_t s);
 }  // namespace orion

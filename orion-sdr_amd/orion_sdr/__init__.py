@@ -83,6 +83,12 @@ def _load():
         "orion_rotator_mix_usb_block_device": (i, [vp, vp, sz, vp, sz, vp, C.POINTER(WorkReport)]),
         "orion_nco_new": (vp, [f, f]), "orion_nco_set_freq": (i, [vp, f]),
         "orion_nco_next_cs_block": (i, [vp, vp, sz]), "orion_nco_next_cs_block_device": (i, [vp, vp, sz, vp]),
+        "orion_rotator_next_cs_block": (i, [vp, vp, sz]),
+        "orion_rotator_next_cs_block_device": (i, [vp, vp, sz, vp]),
+        "orion_osc_table_phasors": (i, [f, f, C.c_uint64, vp, sz, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_uint64)]),
+        "orion_fir_lowpass_iq_num_taps": (i, [vp, C.POINTER(sz)]),
+        "orion_fir_lowpass_iq_group_delay": (i, [vp, C.POINTER(sz)]),
         "orion_biquad_new": (vp, [f, f, f, f, f]),
         "orion_lp_dc_cascade_new": (vp, [f, f, f]), "orion_lp_dc_cascade_set_sqrt_map": (i, [vp, i]),
         "orion_pm_direct_phase_mod_new": (vp, [f, f, f]), "orion_pm_direct_phase_mod_set_gain": (i, [vp, f]),
@@ -144,6 +150,9 @@ def _load():
         "orion_lp_cascade_design": (None, [f, f, fp]),
         "orion_diag_stream_read_bytes": (sz, [sz]),
         "orion_diag_stream_read": (i, [vp, sz, vp]),
+        "orion_diag_spin": (i, [vp, C.c_uint32, C.c_uint32, C.c_double]),
+        "orion_diag_stream_create": (vp, [C.c_uint32]), "orion_diag_stream_destroy": (i, [vp]),
+        "orion_device_cus": (i, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -271,12 +280,13 @@ class _Block:
     def taps(self, which: int = 0) -> np.ndarray:
         return _taps_of(self._h, which)
 
-    _OPTS = {"scan_path": 1, "mod_passes": 2}
+    _OPTS = {"scan_path": 1, "mod_passes": 2, "nco_table": 3}
 
     def configure_option(self, option: str, value: int):
         """Engine options (no reference counterpart; include/orion_sdr_amd.h
         orion_block_configure): scan_path 0/1 (single pass / three-kernel scan),
-        mod_passes 0/3."""
+        mod_passes 0/3, nco_table 0..2^28 (outputs of the reference's oscillator
+        recurrence tabulated per tune; 0 = the closed-form ideal phasor)."""
         _check(_L.orion_block_configure(self._h, self._OPTS[option], int(value)))
         return self
 
@@ -301,6 +311,13 @@ class Rotator(_Block):
     def reset_phase(self):
         """rotator.rs:28-31: phasor back to 1 + j0."""
         _check(_L.orion_rotator_reset_phase(self._h))
+
+    def next_cs_block(self, n: int) -> np.ndarray:
+        """rotator.rs:44-68 next / next_cs, n times: complex64 phasors, advancing the
+        same oscillator as process / mix_usb_block."""
+        out = np.empty(int(n), np.complex64)
+        _check(_L.orion_rotator_next_cs_block(self._h, out.ctypes.data, out.size))
+        return out
 
     def mix_usb_block(self, x):
         """rotator.rs:88-94: I*cos + Q*sin on the same oscillator (complex64 -> float32).
@@ -391,10 +408,16 @@ class FirLowpassIq(_Block):
         return cls(_L.orion_fir_lowpass_iq_from_taps(_fptr(t) if t.size else None, t.size))
 
     def num_taps(self) -> int:
-        return len(self.taps())
+        """fir.rs:210-212."""
+        n = C.c_size_t(0)
+        _check(_L.orion_fir_lowpass_iq_num_taps(self._h, C.byref(n)))
+        return int(n.value)
 
     def group_delay(self) -> int:
-        return (self.num_taps() - 1) // 2
+        """fir.rs:216-218: (num_taps - 1) / 2."""
+        d = C.c_size_t(0)
+        _check(_L.orion_fir_lowpass_iq_group_delay(self._h, C.byref(d)))
+        return int(d.value)
 
     def filter_aligned(self, io: np.ndarray) -> np.ndarray:
         """fir.rs:260-276, returns the filtered copy (time-aligned, same length)."""
@@ -761,6 +784,30 @@ def diag_stream_read(x, stream: int = 0) -> int:
     return int(nb)
 
 
+def diag_spin(stream: int, workgroups: int, lds_bytes: int, seconds: float):
+    """Residency tests (no reference counterpart): `workgroups` one-wave workgroups each
+    holding lds_bytes of LDS for `seconds` of wall clock, asynchronous on `stream`."""
+    _check(_L.orion_diag_spin(C.c_void_p(stream), int(workgroups), int(lds_bytes), float(seconds)))
+
+
+def diag_stream_create(n_cus: int = 0) -> int:
+    """A HIP stream restricted to the first n_cus CUs (0: unrestricted); free it with
+    diag_stream_destroy."""
+    s = _L.orion_diag_stream_create(int(n_cus))
+    if not s:
+        raise OrionError(f"orion_sdr: stream creation failed: {_err()}")
+    return int(s)
+
+
+def diag_stream_destroy(stream: int):
+    _check(_L.orion_diag_stream_destroy(C.c_void_p(stream)))
+
+
+def device_cus() -> int:
+    """Compute units of the current device."""
+    return int(_L.orion_device_cus())
+
+
 def set_spin_limit(polls: int):
     """Test-only: polls a cross-workgroup wait makes before it times out (process-wide;
     0 makes every such wait time out at once). include/orion_sdr_amd.h."""
@@ -769,6 +816,17 @@ def set_spin_limit(polls: int):
 
 def spin_limit() -> int:
     return int(_L.orion_debug_spin_limit())
+
+
+def osc_table_phasors(freq_hz: float, fs: float, n: int, budget: int = 1 << 20):
+    """Host only: the first n phasors of Rotator(freq_hz, fs) as the engine tabulates
+    them (include/orion_sdr_amd.h orion_osc_table_phasors). Returns (phasors,
+    cyc_start, cyc_len, n_tab)."""
+    out = np.empty(int(n), np.complex64)
+    cs, cl, nt = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+    _check(_L.orion_osc_table_phasors(freq_hz, fs, int(budget), out.ctypes.data, out.size, C.byref(cs),
+                                      C.byref(cl), C.byref(nt)))
+    return out, int(cs.value), int(cl.value), int(nt.value)
 
 
 def device_count() -> int:
