@@ -200,66 +200,72 @@ class NcoBlock final : public OscBlock {
 
 // ------------------------------------------------------ analog modulators --
 constexpr float kTauF = 6.28318530717958647692f;  // core::f32::consts::TAU
-// modulate/am.rs:9-120. F32 audio -> C32 IQ.
+// ORION_OPT_NCO_TABLE on a block that owns one RefOsc.
+int configure_osc(RefOsc& o, int option, long long value) {
+  if (option != kOptNcoTable) return -4;
+  if (value < 0 || static_cast<unsigned long long>(value) > kNcoTableMax) return -3;
+  o.set_budget(static_cast<uint64_t>(value));
+  return 0;
+}
+
+// modulate/am.rs:9-120 (rf_nco: Rotator, am.rs:28). F32 audio -> C32 IQ.
 class AmModBlock final : public Block {
  public:
-  AmModBlock(float fs, float rf_hz, float cl, float mi) : osc_(oscillator(rf_hz, fs)), cl_(cl), mi_(mi) {}
+  AmModBlock(float fs, float rf_hz, float cl, float mi) : osc_(rf_hz, fs), cl_(cl), mi_(mi) {}
   const char* name() const override { return "AmDsbMod"; }
   Dt in_type() const override { return Dt::F32; }
   Dt out_type() const override { return Dt::C32; }
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const size_t n = std::min(n_in, out_cap);  // am.rs:45
-    launch_am_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), k_, osc_.step_q64,
-                  cl_, mi_, g_, clamp_, s);
-    k_ += n;
+    launch_am_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), osc_.count(),
+                  osc_.dev(), cl_, mi_, g_, clamp_, s);
+    osc_.advance(n);
     return {n, n};
   }
-  void reset() override { k_ = 0; }
+  void reset() override { osc_.reset(); }
   void set_gain(float g) { g_ = g; }        // am.rs:31-33
   void set_clamp(bool on) { clamp_ = on; }  // am.rs:34-36
-  std::vector<float> taps(int) const override { return {osc_.w_re, osc_.w_im}; }
+  int configure(int option, long long value) override { return configure_osc(osc_, option, value); }
+  std::vector<float> taps(int) const override { return {osc_.osc().w_re, osc_.osc().w_im}; }
 
  private:
-  Oscillator osc_;
+  RefOsc osc_;
   float cl_, mi_, g_ = 1.0f;
   bool clamp_ = false;
-  uint64_t k_ = 0;
 };
 
-// modulate/pm.rs:9-47 PmDirectPhaseMod. F32 audio -> C32 IQ.
+// modulate/pm.rs:9-47 PmDirectPhaseMod (rf_nco: Nco, pm.rs:20). F32 audio -> C32 IQ.
 class PmModBlock final : public Block {
  public:
-  PmModBlock(float fs, float kp, float rf_hz) : osc_(oscillator(rf_hz, fs)), kp_(kp) {}
+  PmModBlock(float fs, float kp, float rf_hz) : osc_(rf_hz, fs), kp_(kp) {}
   const char* name() const override { return "PmDirectPhaseMod"; }
   Dt in_type() const override { return Dt::F32; }
   Dt out_type() const override { return Dt::C32; }
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const size_t n = std::min(n_in, out_cap);  // pm.rs:37
-    launch_pm_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), k_, osc_.step_q64,
-                  kp_, g_, s);
-    k_ += n;
+    launch_pm_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), osc_.count(),
+                  osc_.dev(), kp_, g_, s);
+    osc_.advance(n);
     return {n, n};
   }
-  void reset() override { k_ = 0; }
+  void reset() override { osc_.reset(); }
   void set_gain(float g) { g_ = g; }          // pm.rs:24-26
   void set_sensitivity(float kp) { kp_ = kp; }  // pm.rs:27-29
-  std::vector<float> taps(int) const override { return {kp_, osc_.w_re, osc_.w_im}; }
+  int configure(int option, long long value) override { return configure_osc(osc_, option, value); }
+  std::vector<float> taps(int) const override { return {kp_, osc_.osc().w_re, osc_.osc().w_im}; }
 
  private:
-  Oscillator osc_;
+  RefOsc osc_;
   float kp_, g_ = 1.0f;
-  uint64_t k_ = 0;
 };
 
-// modulate/fm.rs:11-74. F32 audio -> C32 IQ; the running phase is carried on the
-// device (a Q0.64 turn count, exact mod 2 pi) so consecutive calls chain without a
-// host sync.
+// modulate/fm.rs:11-74 (rf_nco: Nco, fm.rs:27). F32 audio -> C32 IQ; the running phase
+// is carried on the device (a Q0.64 turn count, exact mod 2 pi) so consecutive calls
+// chain without a host sync.
 class FmModBlock final : public Block {
  public:
-  FmModBlock(float fs, float dev_hz, float rf_hz) : fs_(fs), dev_(dev_hz), osc_(oscillator(rf_hz, fs)) {
+  FmModBlock(float fs, float dev_hz, float rf_hz) : fs_(fs), dev_(dev_hz), osc_(rf_hz, fs) {
     for (auto& c : carry_) c.resize(sizeof(uint64_t));
-    const auto t = phasor_table(osc_.theta, static_cast<size_t>(fm_mod_rtab_len()));
-    rtab_.upload(t.data(), t.size() * sizeof(float));
     reset();
   }
   const char* name() const override { return "FmPhaseAccumMod"; }
@@ -282,42 +288,39 @@ class FmModBlock final : public Block {
         epoch_ = 1;
       }
       launch_fm_mod_sp(static_cast<const float*>(in), static_cast<f2*>(out), nn, kf, g_, rec_.as<uint32_t>(), epoch_,
-                       carry_[cur_].as<uint64_t>(), carry_[cur_ ^ 1].as<uint64_t>(), k_, osc_.step_q64,
-                       rtab_.as<f2>(), dev_err(), s);
-      cur_ ^= 1;
-      k_ += n;
-      return {n, n};
+                       carry_[cur_].as<uint64_t>(), carry_[cur_ ^ 1].as<uint64_t>(), osc_.count(), osc_.dev(),
+                       dev_err(), s);
+    } else {
+      sums_.resize(static_cast<size_t>(fm_mod_chunks(nn)) * sizeof(uint64_t));
+      launch_fm_mod(static_cast<const float*>(in), static_cast<f2*>(out), nn, kf, g_, sums_.as<uint64_t>(),
+                    carry_[cur_].as<uint64_t>(), carry_[cur_ ^ 1].as<uint64_t>(), osc_.count(), osc_.dev(), s);
     }
-    sums_.resize(static_cast<size_t>(fm_mod_chunks(static_cast<long long>(n))) * sizeof(uint64_t));
-    launch_fm_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), kf, g_,
-                  sums_.as<uint64_t>(), carry_[cur_].as<uint64_t>(), carry_[cur_ ^ 1].as<uint64_t>(), k_,
-                  osc_.step_q64, rtab_.as<f2>(), s);
     cur_ ^= 1;
-    k_ += n;
+    osc_.advance(n);
     return {n, n};
   }
   void reset() override {
     for (auto& c : carry_) c.zero();
     ORION_HIP(hipDeviceSynchronize());
     cur_ = 0;
-    k_ = 0;
+    osc_.reset();
   }
   void set_gain(float g) { g_ = g; }           // fm.rs:37-39
   void set_deviation(float d) { dev_ = d; }    // fm.rs:34-36
   int configure(int option, long long value) override {
+    if (option == kOptNcoTable) return configure_osc(osc_, option, value);
     if (option != kOptModPasses) return -4;
     if (value != 0 && value != 1 && value != 3) return -3;
     single_pass_ = value != 3;
     return 0;
   }
-  std::vector<float> taps(int) const override { return {kTauF * dev_ / fs_, osc_.w_re, osc_.w_im}; }
+  std::vector<float> taps(int) const override { return {kTauF * dev_ / fs_, osc_.osc().w_re, osc_.osc().w_im}; }
 
  private:
   float fs_, dev_, g_ = 1.0f;
-  Oscillator osc_;
-  DevBuf carry_[2], sums_, rtab_, rec_;
+  RefOsc osc_;
+  DevBuf carry_[2], sums_, rec_;
   int cur_ = 0;
-  uint64_t k_ = 0;
   uint32_t epoch_ = 0;
   bool single_pass_ = true;  // k_fm_mod_sp, or the three passes (orion_block_configure)
 };

@@ -236,7 +236,7 @@ int orion_osc_table_phasors(float freq_hz, float fs, uint64_t max_out, void* out
   return guarded([&] {
     if (max_out > orion::kNcoTableMax) return fail(ORION_E_ARG, "budget above 2^28");
     const orion::Oscillator o = orion::oscillator(freq_hz, fs);
-    const orion::RecTable t = orion::rec_table(o.w_re, o.w_im, orion::RecState{}, max_out, orion::kRotTile, o.step_q64);
+    const orion::RecTable t = orion::rec_table(o.w_re, o.w_im, orion::RecState{}, max_out, orion::kOscSpan, o.step_q64);
     float* z = static_cast<float*>(out);
     for (size_t k = 0; k < n; ++k) {
       const orion::RecState st = orion::rec_state_after(t, k);

@@ -191,15 +191,21 @@ uint64_t rec_run(float wr, float wi, RecState s, uint64_t max_out, std::vector<f
   std::unordered_map<uint64_t, uint64_t> seen;
   seen.reserve(static_cast<size_t>(std::min<uint64_t>(max_out / 1024 + 2, 1u << 20)));
   if ((s.ctr & 0x3FFu) == 0) seen.emplace(state_key(s), 0);
+  z.resize(static_cast<size_t>(2 * std::min<uint64_t>(max_out, 1u << 22)));
   for (uint64_t k = 0; k < max_out; ++k) {
+    if (2 * k + 2 > z.size()) z.resize(std::min<size_t>(2 * z.size(), static_cast<size_t>(2 * max_out)));
     rec_step(s, wr, wi, fma);
-    z.push_back(s.zr);
-    z.push_back(s.zi);
+    z[2 * k] = s.zr;
+    z[2 * k + 1] = s.zi;
     if ((s.ctr & 0x3FFu) == 0) {
       const auto ins = seen.emplace(state_key(s), k + 1);
-      if (!ins.second) return ins.first->second;
+      if (!ins.second) {
+        z.resize(static_cast<size_t>(2 * (k + 1)));
+        return ins.first->second;
+      }
     }
   }
+  z.resize(static_cast<size_t>(2 * max_out));
   return UINT64_MAX;
 }
 __attribute__((target("fma"))) uint64_t rec_run_hw(float wr, float wi, RecState s, uint64_t max_out,
@@ -215,7 +221,6 @@ RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t m
   RecTable t;
   t.ctr0 = s0.ctr;
   t.mstep = step_q64;
-  t.z.reserve(static_cast<size_t>(2 * std::min<uint64_t>(max_out, 1u << 22)));
   const uint64_t c0 = __builtin_cpu_supports("fma") ? rec_run_hw(wr, wi, s0, max_out, t.z)
                                                     : rec_run_sw(wr, wi, s0, max_out, t.z);
   t.n = t.z.size() / 2;
@@ -235,7 +240,8 @@ RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t m
   }
   // No cycle within the budget: outputs beyond n follow a model anchored at the last
   // exact output: its phase, plus the mean step fitted (least squares over the renorm
-  // points of the run's last 7/8) and the mean magnitude by renorm-counter position.
+  // points of the run's last half) and the mean magnitude by renorm-counter position
+  // (over its last quarter).
   t.prof.assign(1024, 1.0f);
   if (t.n == 0) {
     t.mbase = q64_of_angle(std::atan2(static_cast<long double>(s0.zi), static_cast<long double>(s0.zr)));
@@ -243,18 +249,22 @@ RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t m
   }
   const long double th = std::atan2(static_cast<long double>(wi), static_cast<long double>(wr));
   const long double a0 = std::atan2(static_cast<long double>(s0.zi), static_cast<long double>(s0.zr));
-  const uint64_t from = t.n / 8;
+  const uint64_t from = t.n / 2, from_mag = t.n - t.n / 4;
   std::vector<double> msum(1024, 0.0);
   std::vector<uint64_t> mcnt(1024, 0);
   long double sx = 0, sy = 0, sxx = 0, sxy = 0;
   uint64_t np = 0;
   constexpr long double kTwoPi = 6.283185307179586476925286766559005768L;
-  for (uint64_t k = from; k < t.n; ++k) {
+  for (uint64_t k = from_mag; k < t.n; ++k) {
     const double re = t.z[2 * k], im = t.z[2 * k + 1];
     const uint32_t j = (t.ctr0 + static_cast<uint32_t>(k) + 1u) & 1023u;
     msum[j] += std::sqrt(re * re + im * im);
     mcnt[j] += 1;
-    if (j == 0) {  // drift of the phase against the closed form at this renorm point
+  }
+  // renorm points: (ctr0 + k + 1) & 1023 == 0
+  for (uint64_t k = from + ((1023u - ((t.ctr0 + static_cast<uint32_t>(from)) & 1023u)) & 1023u); k < t.n; k += 1024) {
+    const double re = t.z[2 * k], im = t.z[2 * k + 1];
+    {  // drift of the phase against the closed form at this renorm point
       const long double ideal = std::fmod(a0 + static_cast<long double>(k + 1) * th, kTwoPi);
       long double e = std::atan2(static_cast<long double>(im), static_cast<long double>(re)) - ideal;
       e = std::remainder(e, kTwoPi);

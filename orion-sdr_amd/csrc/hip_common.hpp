@@ -85,6 +85,71 @@ __device__ __forceinline__ f2 phasor_at(uint64_t ph) {
   return f2{__builtin_fmaf(-s, d, c), __builtin_fmaf(c, d, s)};
 }
 
+// ---- the reference's oscillator on the device (osc.hpp RefOsc, design.hpp RecTable) ----
+// Output k of an oscillator (k steps after its table's start state; the phasor after
+// k + 1 steps, rotator.rs:44-62 / nco.rs:42-58):
+//   tab[k]                                            k < n_tab (the reference's own)
+//   tab[cyc_start + (k - cyc_start) mod cyc_len]      cyc_len > 0 (its cycle, forever)
+//   prof[(ctr0 + k + 1) & 1023] e^{j 2 pi ph / 2^64}, ph = mbase + (k + 1 - n_tab) mstep
+//                                                     otherwise (the drift model; prof
+//                                                     null: magnitude 1, the closed form)
+// mtab: e^{j 2 pi p mstep / 2^64}, p < kOscSpan (the model within a run).
+// cyc_len is 0 or >= kOscSpan (rec_table unrolls shorter cycles).
+constexpr int kOscSpan = 16384;  // longest run of consecutive outputs one cursor serves
+struct OscDev {
+  const f2* tab;
+  const float* prof;
+  const f2* mtab;
+  uint64_t n_tab, cyc_start, cyc_len, mbase, mstep;
+  uint32_t ctr0;
+};
+// A cursor over outputs k .. k + len - 1 (len <= kOscSpan): kind 0 all from the
+// table, 1 all modelled, 2 mixed; j = the table index of k (wrapped into the cycle:
+// with cyc_len >= kOscSpan a run wraps at most once); S = the model phasor of k.
+struct OscRun {
+  uint64_t k, j;
+  f2 S;
+  int kind;
+};
+__device__ __forceinline__ OscRun osc_run(const OscDev& o, uint64_t k, int len) {
+  OscRun r;
+  r.k = k;
+  const bool cyc = o.cyc_len != 0;
+  r.kind = (cyc || k + static_cast<uint64_t>(len) <= o.n_tab) ? 0 : (k >= o.n_tab ? 1 : 2);
+  r.j = (cyc && k >= o.n_tab) ? o.cyc_start + (k - o.cyc_start) % o.cyc_len : k;
+  r.S = r.kind != 0 ? phasor_at(o.mbase + (k + 1 - o.n_tab) * o.mstep) : f2{1.0f, 0.0f};
+  return r;
+}
+// Output r.k + off (off < the run's len), from the table or the model (tm: mtab[off]).
+__device__ __forceinline__ f2 osc_get_tm(const OscDev& o, const OscRun& r, int off, f2 tm) {
+  if (r.kind == 0 || (r.kind == 2 && r.k + static_cast<uint64_t>(off) < o.n_tab)) {
+    uint64_t j = r.j + static_cast<uint64_t>(off);
+    if (j >= o.n_tab) j -= o.cyc_len;  // (only with a cycle)
+    return o.tab[j];
+  }
+  f2 p = cmul(r.S, tm);
+  if (o.prof) p *= splat2(o.prof[(o.ctr0 + static_cast<uint32_t>(r.k) + static_cast<uint32_t>(off) + 1u) & 1023u]);
+  return p;
+}
+__device__ __forceinline__ f2 osc_get(const OscDev& o, const OscRun& r, int off) {
+  const bool model = !(r.kind == 0 || (r.kind == 2 && r.k + static_cast<uint64_t>(off) < o.n_tab));
+  return osc_get_tm(o, r, off, model ? o.mtab[off] : f2{1.0f, 0.0f});
+}
+
+// Output k alone (no cursor: kernels that visit samples in no run order).
+__device__ __forceinline__ f2 osc_at(const OscDev& o, uint64_t k) {
+  if (k < o.n_tab) return o.tab[k];
+  if (o.cyc_len) {
+    const uint64_t d = k - o.cyc_start;
+    const uint64_t j = ((d | o.cyc_len) >> 32) == 0 ? static_cast<uint32_t>(d) % static_cast<uint32_t>(o.cyc_len)
+                                                    : d % o.cyc_len;
+    return o.tab[o.cyc_start + j];
+  }
+  f2 p = phasor_at(o.mbase + (k + 1 - o.n_tab) * o.mstep);
+  if (o.prof) p *= splat2(o.prof[(o.ctr0 + static_cast<uint32_t>(k) + 1u) & 1023u]);
+  return p;
+}
+
 // f32 sin and cos, correctly rounded but for rare near-ties: the argument reduced by
 // pi/2 in f64 (two-part pi/2: exact enough for |x| < 2^20), then Taylor polynomials on
 // |r| <= pi/4 through r^15 / r^16 (truncation < 2^-45 relative), one rounding to f32.

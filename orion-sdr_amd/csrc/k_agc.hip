@@ -37,6 +37,7 @@
 
 #include "blocks.hpp"
 #include "hip_common.hpp"
+#include "osc.hpp"
 
 namespace orion {
 namespace {
@@ -53,7 +54,7 @@ struct AgcK {
 //     1e-6), gmin, gmax) * x.
 //   CwPol — modulate/cw.rs:45-87 CwKeyedMod: d = clamp(x, 0, 1), up = d >= env, no
 //     reseed, out = mix_with_nco((env * gain, 0), nco) (the non-FMA product, nco.rs:63-66)
-//     with the oscillator phasor of the sample's absolute index (closed form, as Rotator).
+//     with the tone Nco's phasor (osc.hpp RefOsc: the reference recurrence, tabulated).
 template <bool IQ>
 struct AgcPol {
   using In = typename std::conditional<IQ, float2, float>::type;
@@ -78,14 +79,15 @@ struct CwPol {
   using In = float;
   using Out = float2;
   float att, rel, oma, omr, gain;
-  uint64_t k0, step;  // sample i of the call: the phasor after k0 + i + 1 steps
+  uint64_t k0;  // sample i of the call: oscillator output k0 + i (the Nco, cw.rs:27)
+  OscDev osc;
   __device__ __forceinline__ float drive(In v) const { return v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v); }  // f32::clamp
   __device__ __forceinline__ bool up(float d, float env) const { return d >= env; }
   __device__ __forceinline__ float seed(float env, float) const { return env; }
   __device__ __forceinline__ float warm_seed(float d) const { return d; }
   __device__ __forceinline__ Out out(In, float env, long long i) const {
     const float m = env * gain;
-    const f2 p = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
+    const f2 p = osc_at(osc, k0 + static_cast<uint64_t>(i));
     return make_float2(m * p.x - 0.0f * p.y, m * p.y + 0.0f * p.x);
   }
 };
@@ -402,7 +404,7 @@ class AgcBlock final : public Block {
 class CwModBlock final : public Block {
  public:
   CwModBlock(float fs, float tone_hz, float rise_ms, float fall_ms)
-      : osc_(oscillator(tone_hz, fs)), runner_(std::max(alpha(fs, rise_ms), alpha(fs, fall_ms))) {
+      : osc_(tone_hz, fs), runner_(std::max(alpha(fs, rise_ms), alpha(fs, fall_ms))) {
     rise_ = alpha(fs, rise_ms);
     fall_ = alpha(fs, fall_ms);
   }
@@ -412,24 +414,29 @@ class CwModBlock final : public Block {
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const long long n = static_cast<long long>(std::min(n_in, out_cap));  // cw.rs:47
     if (n == 0) return {0, 0};
-    runner_.run(in, out, n, CwPol{rise_, fall_, 1.0f - rise_, 1.0f - fall_, g_, k_, osc_.step_q64}, s);
-    k_ += static_cast<uint64_t>(n);
+    runner_.run(in, out, n, CwPol{rise_, fall_, 1.0f - rise_, 1.0f - fall_, g_, osc_.count(), osc_.dev()}, s);
+    osc_.advance(static_cast<uint64_t>(n));
     return {static_cast<size_t>(n), static_cast<size_t>(n)};
   }
   void reset() override {
     runner_.reset();
-    k_ = 0;
+    osc_.reset();
   }
   void set_gain(float g) { g_ = g; }  // cw.rs:39-41
-  std::vector<float> taps(int) const override { return {rise_, fall_, osc_.w_re, osc_.w_im}; }
+  int configure(int option, long long value) override {
+    if (option != kOptNcoTable) return -4;
+    if (value < 0 || static_cast<unsigned long long>(value) > kNcoTableMax) return -3;
+    osc_.set_budget(static_cast<uint64_t>(value));
+    return 0;
+  }
+  std::vector<float> taps(int) const override { return {rise_, fall_, osc_.osc().w_re, osc_.osc().w_im}; }
 
  private:
   // cw.rs:27-30: tau = (max(ms, 0.1) * 1e-3) * fs; alpha = exp(-1 / tau)
   static float alpha(float fs, float ms) { return std::exp(-1.0f / ((std::max(ms, 0.1f) * 1e-3f) * fs)); }
-  Oscillator osc_;
+  RefOsc osc_;
   EnvelopeRunner runner_;
   float rise_ = 0, fall_ = 0, g_ = 1.0f;
-  uint64_t k_ = 0;
 };
 
 }  // namespace

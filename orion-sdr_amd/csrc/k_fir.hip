@@ -16,7 +16,7 @@ constexpr int NT = 256;
 constexpr int kMaxGrid = 2048;  // memory-bound: cap and grid-stride (2048 = 8 WG per CU)
 
 // ------------------------------------------------------------------ NCO --
-// Output i of a call is oscillator output k = k0 + i (kernels.hpp OscDev): the
+// Output i of a call is oscillator output k = k0 + i (hip_common.hpp OscDev): the
 // reference's own phasor from the exact table (tail + unrolled cycle, or the exact
 // prefix), or beyond it the model (the closed form when there is no table). MODE:
 // kRotate rotate_block (FMA form, rotator.rs:80-83), kUsb mix_usb_block (cf32 -> f32,
@@ -35,25 +35,9 @@ __global__ __launch_bounds__(NT) void k_rotator(const f2* __restrict__ x, void* 
     tb[i][0] = f2{v.x, v.y};
     tb[i][1] = f2{v.z, v.w};
   }
-  const bool cyc = o.cyc_len != 0;
   for (long long tile = static_cast<long long>(blockIdx.x) * kRotTile; tile < n;
        tile += static_cast<long long>(gridDim.x) * kRotTile) {
-    const uint64_t kt = k0 + static_cast<uint64_t>(tile);  // output index of the tile's first sample
-    // tile-uniform: every sample from the table (kind 0), none (1), or mixed (2)
-    const int kind = (cyc || kt + kRotTile <= o.n_tab) ? 0 : (kt >= o.n_tab ? 1 : 2);
-    uint64_t jt = kt;  // table index of kt (cycle: wrapped; a tile wraps at most once)
-    if (cyc && kt >= o.n_tab) jt = o.cyc_start + (kt - o.cyc_start) % o.cyc_len;
-    const f2 S = kind != 0 ? phasor_at(o.mbase + (kt + 1 - o.n_tab) * o.mstep) : f2{1.0f, 0.0f};
-    auto phasor = [&](int off, f2 tbv) -> f2 {  // off < kRotTile: the sample's offset in the tile
-      if (kind == 0 || (kind == 2 && kt + off < o.n_tab)) {
-        uint64_t j = jt + off;
-        if (cyc && j >= o.n_tab) j -= o.cyc_len;
-        return o.tab[j];
-      }
-      f2 p = cmul(S, tbv);
-      if (o.prof) p *= splat2(o.prof[(o.ctr0 + static_cast<uint32_t>(kt) + off + 1u) & 1023u]);
-      return p;
-    };
+    const OscRun r = osc_run(o, k0 + static_cast<uint64_t>(tile), kRotTile);  // tile-uniform
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int off = 2 * t + 2 * NT * i;
@@ -71,8 +55,8 @@ __global__ __launch_bounds__(NT) void k_rotator(const f2* __restrict__ x, void* 
           if (full) v1 = x[P + 1];
         }
       }
-      const f2 p0 = phasor(off, tb[i][0]);
-      const f2 p1 = phasor(off + 1, tb[i][1]);
+      const f2 p0 = osc_get_tm(o, r, off, tb[i][0]);
+      const f2 p1 = osc_get_tm(o, r, off + 1, tb[i][1]);
       if constexpr (MODE == kUsb) {
         float* y = static_cast<float*>(yv);
         y[P] = __builtin_fmaf(v0.x, p0.x, v0.y * p0.y);
@@ -675,7 +659,7 @@ inline int grid_for(long long work, int per_block) {
 
 void launch_osc(int mode, const f2* x, void* y, long long n, uint64_t k0, const OscDev& o, hipStream_t s) {
   if (n <= 0) return;
-  if (o.cyc_len != 0 && o.cyc_len < static_cast<uint64_t>(kRotTile)) throw HipError("osc: cycle shorter than a tile");
+  if (o.cyc_len != 0 && o.cyc_len < static_cast<uint64_t>(kOscSpan)) throw HipError("osc: cycle shorter than a run");
   const int grid = grid_for(n, kRotTile);
   const bool a16 = (mode == kNcoGen || reinterpret_cast<uintptr_t>(x) % 16 == 0) &&
                    (mode == kUsb || reinterpret_cast<uintptr_t>(y) % 16 == 0);

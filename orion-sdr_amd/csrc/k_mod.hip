@@ -4,11 +4,11 @@
 //   FmPhaseAccumMod::process   modulate/fm.rs:45-74 (+ mix_with_nco, dsp/nco.rs:62-66)
 //   SsbPhasingMod::process     modulate/ssb.rs:43-114 (front and back of the two
 //                              LpCascade scans, which run on the k_scan kernels)
-// Every oscillator is the closed form of the reference's phasor recurrence:
-// sample i of a call uses w^(k0 + i + 1) (Rotator::next / Nco::next_cs advance
-// before returning), evaluated by phasor_q64 from the stream index, so a call
-// never depends on its predecessor's rounding. Streaming, memory-bound kernels:
-// grid-stride over the samples, at most 8 workgroups per CU.
+// Every oscillator is the reference's own recurrence (hip_common.hpp OscDev, osc.hpp
+// RefOsc): sample i of a call uses oscillator output k0 + i (Rotator::next /
+// Nco::next_cs advance before returning) — the tabulated reference phasor, or past the
+// table the drift model. Streaming, memory-bound kernels: tiles of kModTile samples
+// (one oscillator cursor each), grid-stride, at most 8 workgroups per CU.
 #include <algorithm>
 
 #include "kernels.hpp"
@@ -21,58 +21,71 @@ constexpr int kMaxGrid = 2048;
 constexpr int kFmC = 16;             // FM phase scan: samples per thread
 constexpr int kFmCH = kFmC * NT;     // samples per workgroup chunk (4096)
 
-int grid_for(long long n) { return static_cast<int>(std::min<long long>(kMaxGrid, std::max(1LL, (n + NT - 1) / NT))); }
+constexpr int kModPer = 8;               // samples per thread per tile
+constexpr int kModTile = NT * kModPer;   // 2048
+static_assert(kModTile <= kOscSpan, "one oscillator cursor per tile");
 
-// am.rs:87-89 (clamp: :56): m = (cl + mi x) [clamped to +-1] * g; out = m * r.
+int grid_for(long long n) {
+  return static_cast<int>(std::min<long long>(kMaxGrid, std::max(1LL, (n + kModTile - 1) / kModTile)));
+}
+
+// Sample i of a call with its oscillator phasor (output k0 + i): f(i, r).
+template <class F>
+__device__ __forceinline__ void mod_tiles(long long n, uint64_t k0, const OscDev& o, F f) {
+  for (long long tile = static_cast<long long>(blockIdx.x) * kModTile; tile < n;
+       tile += static_cast<long long>(gridDim.x) * kModTile) {
+    const OscRun r = osc_run(o, k0 + static_cast<uint64_t>(tile), kModTile);
+#pragma unroll
+    for (int m = 0; m < kModPer; ++m) {
+      const int off = static_cast<int>(threadIdx.x) + NT * m;
+      const long long i = tile + off;
+      if (i < n) f(i, osc_get(o, r, off));
+    }
+  }
+}
+
+// am.rs:87-89 (clamp: :56): m = (cl + mi x) [clamped to +-1] * g; out = m * r (Rotator rf).
 __global__ __launch_bounds__(NT) void k_am_mod(const float* __restrict__ x, f2* __restrict__ y, long long n,
-                                               uint64_t k0, uint64_t step, float cl, float mi, float g, int clamp) {
-  for (long long i = blockIdx.x * static_cast<long long>(NT) + threadIdx.x; i < n;
-       i += static_cast<long long>(gridDim.x) * NT) {
+                                               uint64_t k0, const OscDev o, float cl, float mi, float g, int clamp) {
+  mod_tiles(n, k0, o, [&](long long i, f2 r) {
     float v = cl + mi * x[i];
     if (clamp) v = fminf(fmaxf(v, -1.0f), 1.0f);
     const float m = v * g;
-    const f2 r = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
     y[i] = f2{m * r.x, m * r.y};
-  }
+  });
 }
 
 // modulate/pm.rs:36-47 PmDirectPhaseMod: phi = kp x; base = (cos phi, sin phi) * gain
 // (num-complex Complex * f32); out = mix_with_nco(base, rf) (the non-FMA product,
-// nco.rs:63-66) with the RF phasor after k0 + i + 1 steps.
+// nco.rs:63-66).
 __global__ __launch_bounds__(NT) void k_pm_mod(const float* __restrict__ x, f2* __restrict__ y, long long n,
-                                               uint64_t k0, uint64_t step, float kp, float g) {
-  for (long long i = blockIdx.x * static_cast<long long>(NT) + threadIdx.x; i < n;
-       i += static_cast<long long>(gridDim.x) * NT) {
+                                               uint64_t k0, const OscDev o, float kp, float g) {
+  mod_tiles(n, k0, o, [&](long long i, f2 r) {
     const float phi = kp * x[i];
     float sn, cs;
     sincos_cr(phi, &sn, &cs);  // pm.rs:44 (phi.cos(), phi.sin())
     const float br = cs * g, bi = sn * g;
-    const f2 r = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
     y[i] = f2{br * r.x - bi * r.y, br * r.y + bi * r.x};
-  }
+  });
 }
 
 // ssb.rs:52-54: the two LpCascade inputs x p.re, x p.im (p = audio NCO), planar.
 __global__ __launch_bounds__(NT) void k_ssb_mod_front(const float* __restrict__ x, float* __restrict__ u,
-                                                      long long n, uint64_t k0, uint64_t step) {
-  for (long long i = blockIdx.x * static_cast<long long>(NT) + threadIdx.x; i < n;
-       i += static_cast<long long>(gridDim.x) * NT) {
-    const f2 p = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
+                                                      long long n, uint64_t k0, const OscDev o) {
+  mod_tiles(n, k0, o, [&](long long i, f2 p) {
     const float xi = x[i];
     u[i] = xi * p.x;
     u[n + i] = xi * p.y;
-  }
+  });
 }
 
 // ssb.rs:55-60: z = (I, side Q); out = z * r (rf NCO), FMA form of rotate_block.
 __global__ __launch_bounds__(NT) void k_ssb_mod_back(const float* __restrict__ v, f2* __restrict__ y, long long n,
-                                                     uint64_t k0, uint64_t step, float side) {
-  for (long long i = blockIdx.x * static_cast<long long>(NT) + threadIdx.x; i < n;
-       i += static_cast<long long>(gridDim.x) * NT) {
-    const f2 r = phasor_q64(k0 + static_cast<uint64_t>(i) + 1, step);
+                                                     uint64_t k0, const OscDev o, float side) {
+  mod_tiles(n, k0, o, [&](long long i, f2 r) {
     const f2 z = f2{v[i], side * v[n + i]};
     y[i] = cmul_rot(z, r);
-  }
+  });
 }
 
 // ---- FmPhaseAccumMod (fm.rs:45-74) ----------------------------------------------------
@@ -89,7 +102,7 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_back(const float* __restrict__ v
 //   * the thread's outputs: the phasor of its entering phase (phasor_at), then the
 //     reference's own recurrence z = z (dc, ds) (fm.rs:53-54, its op order) over its
 //     16 pairs; base = z gain (fm.rs:66); mix_with_nco's non-FMA product with the
-//     closed-form RF phasor (nco.rs:62-66).
+//     RF Nco's phasor (nco.rs:62-66; the oscillator cursor of the chunk).
 // Against an f64 phase and a per-sample sincosf of it this is ~3x less VALU per sample.
 constexpr double kTurnsPerRad = 2.9358905032820014e18;  // 2^64 / (2 pi)
 
@@ -123,8 +136,9 @@ __device__ __forceinline__ uint64_t fm_pairs(float kf, const float* __restrict__
 // conflict-free b64 stores), aliasing the input staging: every thread is past its
 // reads of it (the caller's barrier). Pass h covers the chunk's samples 16 t' + 8 h + j.
 constexpr int kFmYs = (kFmCH + kFmCH / 16) / 2;  // f2 slots (= the input staging's floats / 2)
-__device__ __forceinline__ void fm_out(const FmPairs& p, uint64_t ph, float gain, f2 R0, const f2* __restrict__ rtab,
+__device__ __forceinline__ void fm_out(const FmPairs& p, uint64_t ph, float gain, const OscDev& o, uint64_t k0,
                                        f2* ys, f2* __restrict__ y, long long base, long long n) {
+  const OscRun R = osc_run(o, k0 + static_cast<uint64_t>(base), kFmCH);  // RF Nco outputs of the chunk
   f2 z = phasor_at(ph);
   const int t = threadIdx.x;
   const bool full = base + kFmCH <= n;
@@ -136,7 +150,7 @@ __device__ __forceinline__ void fm_out(const FmPairs& p, uint64_t ph, float gain
       // fm.rs:53-54: zr = z.re.mul_add(dc, -z.im*ds); zi = z.im.mul_add(dc, z.re*ds)
       z = f2{__builtin_fmaf(z.x, p.c[k], -(z.y * p.s[k])), __builtin_fmaf(z.y, p.c[k], z.x * p.s[k])};
       const f2 bz = f2{z.x * gain, z.y * gain};  // fm.rs:66 base = z * gain
-      const f2 r = cmul(R0, rtab[k]);
+      const f2 r = osc_get(o, R, kFmC * t + k);
       const int e = 8 * t + j;
       ys[e + (e >> 4)] = f2{bz.x * r.x - bz.y * r.y, bz.x * r.y + bz.y * r.x};  // nco.rs:65 (no FMA)
     }
@@ -233,7 +247,7 @@ __global__ __launch_bounds__(NT) void k_fm_mod_carry(uint64_t* __restrict__ sums
 // Pass 3: the block scan of the thread sums from the chunk's entering phase, outputs.
 __global__ __launch_bounds__(NT) void k_fm_mod_apply(const float* __restrict__ x, f2* __restrict__ y, long long n,
                                                      float kf, float gain, const uint64_t* __restrict__ offs,
-                                                     uint64_t k0, uint64_t step, const f2* __restrict__ rtab) {
+                                                     uint64_t k0, const OscDev o) {
   __shared__ uint64_t tot[NT / 64];
   __shared__ __attribute__((aligned(16))) f2 ys[kFmYs];  // the input staging, then the outputs
   float* xs = reinterpret_cast<float*>(ys);
@@ -245,9 +259,7 @@ __global__ __launch_bounds__(NT) void k_fm_mod_apply(const float* __restrict__ x
   const uint64_t q = fm_pairs(kf, xs + e + (e >> 4), valid, p);
   uint64_t total;
   const uint64_t ph = offs[blockIdx.x] + wg_scan_u64(q, tot, total);  // (its barrier: xs is dead)
-  const long long i0 = base + e;
-  const f2 R0 = phasor_q64(k0 + static_cast<uint64_t>(i0) + 1, step);  // RF phasor of i0 + k = R0 rtab[k]
-  fm_out(p, ph, gain, R0, rtab, ys, y, base, n);
+  fm_out(p, ph, gain, o, k0, ys, y, base, n);
 }
 
 // Single pass (default): each chunk publishes its Q0.64 sum, takes the phase entering
@@ -275,8 +287,7 @@ __device__ __forceinline__ uint64_t fm_ld64(const uint32_t* p) {
 __global__ __launch_bounds__(NT) void k_fm_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
                                                   float kf, float gain, uint32_t* __restrict__ rec, uint32_t epoch,
                                                   const uint64_t* __restrict__ carry_in, uint64_t* __restrict__ carry_out,
-                                                  uint64_t k0, uint64_t step, const f2* __restrict__ rtab,
-                                                  int* __restrict__ err, uint32_t spin) {
+                                                  uint64_t k0, const OscDev o, int* __restrict__ err, uint32_t spin) {
   __shared__ uint64_t tot[NT / 64];
   __shared__ uint64_t excl_sh;
   __shared__ __attribute__((aligned(16))) f2 ys[kFmYs];  // the input staging, then the outputs
@@ -342,62 +353,58 @@ __global__ __launch_bounds__(NT) void k_fm_mod_sp(const float* __restrict__ x, f
     }
   }
   __syncthreads();
-  const long long i0 = base + e;
-  const f2 R0 = phasor_q64(k0 + static_cast<uint64_t>(i0) + 1, step);
-  fm_out(p, excl_sh + before, gain, R0, rtab, ys, y, base, n);
+  fm_out(p, excl_sh + before, gain, o, k0, ys, y, base, n);
 }
 
 }  // namespace
 
-void launch_am_mod(const float* x, f2* y, long long n, uint64_t k0, uint64_t step, float cl, float mi, float g,
+void launch_am_mod(const float* x, f2* y, long long n, uint64_t k0, const OscDev& o, float cl, float mi, float g,
                    bool clamp, hipStream_t s) {
   if (n <= 0) return;
-  k_am_mod<<<grid_for(n), NT, 0, s>>>(x, y, n, k0, step, cl, mi, g, clamp ? 1 : 0);
+  k_am_mod<<<grid_for(n), NT, 0, s>>>(x, y, n, k0, o, cl, mi, g, clamp ? 1 : 0);
   ORION_LAUNCH_CHECK();
 }
 
-void launch_ssb_mod_front(const float* x, float* u, long long n, uint64_t k0, uint64_t step, hipStream_t s) {
+void launch_ssb_mod_front(const float* x, float* u, long long n, uint64_t k0, const OscDev& o, hipStream_t s) {
   if (n <= 0) return;
-  k_ssb_mod_front<<<grid_for(n), NT, 0, s>>>(x, u, n, k0, step);
+  k_ssb_mod_front<<<grid_for(n), NT, 0, s>>>(x, u, n, k0, o);
   ORION_LAUNCH_CHECK();
 }
 
-void launch_pm_mod(const float* x, f2* y, long long n, uint64_t k0, uint64_t step, float kp, float g, hipStream_t s) {
+void launch_pm_mod(const float* x, f2* y, long long n, uint64_t k0, const OscDev& o, float kp, float g, hipStream_t s) {
   if (n <= 0) return;
-  k_pm_mod<<<grid_for(n), NT, 0, s>>>(x, y, n, k0, step, kp, g);
+  k_pm_mod<<<grid_for(n), NT, 0, s>>>(x, y, n, k0, o, kp, g);
   ORION_LAUNCH_CHECK();
 }
 
-void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, uint64_t step, float side, hipStream_t s) {
+void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, const OscDev& o, float side, hipStream_t s) {
   if (n <= 0) return;
-  k_ssb_mod_back<<<grid_for(n), NT, 0, s>>>(v, y, n, k0, step, side);
+  k_ssb_mod_back<<<grid_for(n), NT, 0, s>>>(v, y, n, k0, o, side);
   ORION_LAUNCH_CHECK();
 }
 
 long long fm_mod_chunks(long long n) { return (n + kFmCH - 1) / kFmCH; }
 
 void launch_fm_mod_sp(const float* x, f2* y, long long n, float kf, float gain, uint32_t* rec, uint32_t epoch,
-                      const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
-                      int* err, hipStream_t s) {
+                      const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, const OscDev& o, int* err,
+                      hipStream_t s) {
   if (n <= 0) return;
   const long long nchunk = fm_mod_chunks(n);
   if (nchunk > (1LL << 30)) throw HipError("FM modulator: input too long");
-  k_fm_mod_sp<<<static_cast<int>(nchunk), NT, 0, s>>>(x, y, n, kf, gain, rec, epoch, carry_in, carry_out, k0, step,
-                                                     rtab, err, spin_limit());
+  k_fm_mod_sp<<<static_cast<int>(nchunk), NT, 0, s>>>(x, y, n, kf, gain, rec, epoch, carry_in, carry_out, k0, o, err,
+                                                     spin_limit());
   ORION_LAUNCH_CHECK();
 }
-int fm_mod_rtab_len() { return kFmC; }
 
 void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, uint64_t* sums,
-                   const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
-                   hipStream_t s) {
+                   const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, const OscDev& o, hipStream_t s) {
   if (n <= 0) return;
   const long long nchunk = fm_mod_chunks(n);
   if (nchunk > (1LL << 30)) throw HipError("FM modulator: input too long");
   const int g = static_cast<int>(nchunk);
   k_fm_mod_sum<<<g, NT, 0, s>>>(x, n, kf, sums);
   k_fm_mod_carry<<<1, NT, 0, s>>>(sums, g, carry_in, carry_out);
-  k_fm_mod_apply<<<g, NT, 0, s>>>(x, y, n, kf, gain, sums, k0, step, rtab);
+  k_fm_mod_apply<<<g, NT, 0, s>>>(x, y, n, kf, gain, sums, k0, o);
   ORION_LAUNCH_CHECK();
 }
 

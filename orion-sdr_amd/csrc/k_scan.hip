@@ -25,9 +25,6 @@ constexpr int PADN = CH + CH / 16 + 16;
 #ifndef ORION_SP_TRUNC
 #define ORION_SP_TRUNC 1  // k_lpdc_sp: the LP4 lane scan truncated to the forgetting horizon (0: full two-scan form)
 #endif
-#ifndef ORION_SP_TAB2
-#define ORION_SP_TAB2 1  // SSB mixing phasor = (Swg tab[t]) tab[k NT]: one uniform table load per sample, not a per-lane one
-#endif
 
 __device__ __forceinline__ int pos(int e) { return e + (e >> 4); }
 
@@ -54,14 +51,15 @@ template <> struct RecSel<RecK::ONEPOLE> {
 };
 
 // Translated (fm.rs:48-49) or raw complex sample i of channel ch; i may be the
-// sample just before this workgroup. phasor(i) = e^{j theta (k0+i+1)}.
+// sample just before this workgroup. Sample i's phasor: oscillator output k0 + i (R:
+// the cursor of the workgroup's run from sample base).
 template <Pre PR>
-__device__ __forceinline__ f2 cin(const ScanArgs& a, const f2* x, long long i, long long base, f2 Swg) {
+__device__ __forceinline__ f2 cin(const ScanArgs& a, const f2* x, long long i, long long base, const OscRun& R) {
   const f2 z = x[i];
   if constexpr (PR == Pre::Fm) {
     if (a.translate) {
-      const f2 p = (i >= base) ? cmul(Swg, a.tab[i - base])
-                               : phasor_q64(static_cast<uint64_t>(a.k0 + i + 1), a.step);
+      const f2 p = (i >= base) ? osc_get(a.osc, R, static_cast<int>(i - base))
+                               : osc_at(a.osc, static_cast<uint64_t>(a.k0 + i));
       const float c = p.x, d = -p.y;  // num-complex z * conj(p)
       return f2{z.x * c - z.y * d, z.x * d + z.y * c};
     }
@@ -71,16 +69,16 @@ __device__ __forceinline__ f2 cin(const ScanArgs& a, const f2* x, long long i, l
 
 // Pre-map of sample i (base <= i < n) -> recurrence input.
 template <Pre PR>
-__device__ __forceinline__ float premap(const ScanArgs& a, int ch, long long i, long long base, f2 Swg) {
+__device__ __forceinline__ float premap(const ScanArgs& a, int ch, long long i, long long base, const OscRun& R) {
   if constexpr (PR == Pre::Real) {
     return static_cast<const float*>(a.x)[ch * a.x_stride + i];
   } else {
     const f2* x = static_cast<const f2*>(a.x) + ch * a.x_stride;
     if constexpr (PR == Pre::Fm || PR == Pre::Pm) {
-      const f2 z = cin<PR>(a, x, i, base, Swg);
+      const f2 z = cin<PR>(a, x, i, base, R);
       f2 p;
       if (i > 0) {
-        p = cin<PR>(a, x, i - 1, base, Swg);
+        p = cin<PR>(a, x, i - 1, base, R);
       } else {
         const float* cr = a.carry_in + ch * kScanCarry;
         p = f2{cr[6], cr[7]};
@@ -90,7 +88,7 @@ __device__ __forceinline__ float premap(const ScanArgs& a, int ch, long long i, 
     } else {
       const f2 z = x[i];
       if constexpr (PR == Pre::Ssb) {
-        const f2 p = cmul(Swg, a.tab[i - base]);
+        const f2 p = osc_get(a.osc, R, static_cast<int>(i - base));
         return __builtin_fmaf(z.x, p.x, z.y * p.y);  // ssb.rs:37
       } else if constexpr (PR == Pre::AmSqrt) {
         return __builtin_fmaf(z.x, z.x, z.y * z.y);  // am.rs:204
@@ -106,11 +104,11 @@ __device__ __forceinline__ float premap(const ScanArgs& a, int ch, long long i, 
 // premap with the samples already loaded: z = x[i], zp = x[i - 1] (any value when
 // i == 0: the carried previous sample is used), raw (untranslated) complex samples.
 template <Pre PR>
-__device__ __forceinline__ f2 cin_v(const ScanArgs& a, f2 z, long long i, long long base, f2 Swg) {
+__device__ __forceinline__ f2 cin_v(const ScanArgs& a, f2 z, long long i, long long base, const OscRun& R) {
   if constexpr (PR == Pre::Fm) {
     if (a.translate) {
-      const f2 p = (i >= base) ? cmul(Swg, a.tab[i - base])
-                               : phasor_q64(static_cast<uint64_t>(a.k0 + i + 1), a.step);
+      const f2 p = (i >= base) ? osc_get(a.osc, R, static_cast<int>(i - base))
+                               : osc_at(a.osc, static_cast<uint64_t>(a.k0 + i));
       const float c = p.x, d = -p.y;  // num-complex z * conj(p)
       return f2{z.x * c - z.y * d, z.x * d + z.y * c};
     }
@@ -118,13 +116,13 @@ __device__ __forceinline__ f2 cin_v(const ScanArgs& a, f2 z, long long i, long l
   return z;
 }
 template <Pre PR>
-__device__ __forceinline__ float premap_v(const ScanArgs& a, int ch, long long i, long long base, f2 Swg, f2 z,
-                                          f2 zp) {
+__device__ __forceinline__ float premap_v(const ScanArgs& a, int ch, long long i, long long base, const OscRun& R,
+                                          f2 z, f2 zp) {
   if constexpr (PR == Pre::Fm || PR == Pre::Pm) {
-    const f2 zc = cin_v<PR>(a, z, i, base, Swg);
+    const f2 zc = cin_v<PR>(a, z, i, base, R);
     f2 p;
     if (i > 0) {
-      p = cin_v<PR>(a, zp, i - 1, base, Swg);
+      p = cin_v<PR>(a, zp, i - 1, base, R);
     } else {
       const float* cr = a.carry_in + ch * kScanCarry;
       p = f2{cr[6], cr[7]};
@@ -142,11 +140,11 @@ __device__ __forceinline__ float premap_v(const ScanArgs& a, int ch, long long i
 
 template <Pre PR>
 __device__ __forceinline__ void stage(const ScanArgs& a, int ch, long long base, int cnt, float* sb) {
-  f2 Swg = f2{1.0f, 0.0f};
+  OscRun R{};
   if constexpr (PR == Pre::Ssb || PR == Pre::Fm)
-    Swg = phasor_q64(static_cast<uint64_t>(a.k0 + base + 1), a.step);
+    if (PR == Pre::Ssb || a.translate) R = osc_run(a.osc, static_cast<uint64_t>(a.k0 + base), cnt);
   if constexpr (PR == Pre::Fm || PR == Pre::Pm) {
-    for (int e = threadIdx.x; e < cnt; e += NT) sb[pos(e)] = premap<PR>(a, ch, base + e, base, Swg);
+    for (int e = threadIdx.x; e < cnt; e += NT) sb[pos(e)] = premap<PR>(a, ch, base + e, base, R);
   } else {
     // all of the thread's loads first (fixed trip count, unrolled): one memory
     // round trip per chunk instead of one per sample
@@ -163,10 +161,6 @@ __device__ __forceinline__ void stage(const ScanArgs& a, int ch, long long base,
       for (int k = 0; k < K; ++k) sb[pos(threadIdx.x + k * NT)] = v[k];
     } else {
       const f2* __restrict__ x = static_cast<const f2*>(a.x) + ch * a.x_stride + base;
-#if ORION_SP_TAB2
-      f2 St = f2{1.0f, 0.0f};
-      if constexpr (PR == Pre::Ssb) St = cmul(Swg, a.tab[threadIdx.x]);
-#endif
       f2 v[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -179,13 +173,7 @@ __device__ __forceinline__ void stage(const ScanArgs& a, int ch, long long base,
         const f2 z = v[k];
         float o;
         if constexpr (PR == Pre::Ssb) {
-#if ORION_SP_ABL & 1
-          const f2 p = Swg;
-#elif ORION_SP_TAB2
-          const f2 p = cmul(St, a.tab[k * NT]);
-#else
-          const f2 p = cmul(Swg, a.tab[e]);
-#endif
+          const f2 p = osc_get(a.osc, R, e);
           o = __builtin_fmaf(z.x, p.x, z.y * p.y);  // ssb.rs:37
         } else if constexpr (PR == Pre::AmSqrt) {
           o = __builtin_fmaf(z.x, z.x, z.y * z.y);  // am.rs:204
@@ -424,9 +412,10 @@ __global__ __launch_bounds__(NT) void k_scan_apply(const ScanArgs a) {
     for (int i = S; i < 6; ++i) co[i] = 0.0f;
     if constexpr (PR == Pre::Fm || PR == Pre::Pm) {
       const f2* x = static_cast<const f2*>(a.x) + ch * a.x_stride;
-      f2 Swg = f2{1.0f, 0.0f};
-      if constexpr (PR == Pre::Fm) Swg = phasor_q64(static_cast<uint64_t>(a.k0 + base + 1), a.step);
-      const f2 z = cin<PR>(a, x, a.n - 1, base, Swg);
+      OscRun R{};
+      if constexpr (PR == Pre::Fm)
+        if (a.translate) R = osc_run(a.osc, static_cast<uint64_t>(a.k0 + base), cnt);
+      const f2 z = cin<PR>(a, x, a.n - 1, base, R);
       co[6] = z.x;
       co[7] = z.y;
     } else {
@@ -492,9 +481,9 @@ __device__ __forceinline__ void dc_combine(double m1, double d1, double& m2, dou
 // elements [64 SC w, 64 SC (w + 1)) (lane l: e = 64 SC w + l + 64 k, coalesced), which
 // are exactly the lane runs its own lanes process, so no workgroup barrier separates
 // the staging, the LP4 re-run's rewrite and the output staging from their readers (a
-// wave's LDS operations execute in order). The SSB mixing phasor of element e is
-// (S_h tab[e mod kScanCH - 64 k]) tab[64 k], S_h the exact phasor of the chunk's
-// sample kScanCH h, h = e / kScanCH (uniform in the wave).
+// wave's LDS operations execute in order). The SSB mixing phasor of element e is the
+// BFO's output k0 + base + e: the reference's from its table, or in the drift model
+// (S mtab[64 SC w + l]) mtab[64 k] scaled by the magnitude profile.
 template <int SC>
 __device__ __forceinline__ int posS(int e) { return e + e / SC; }
 __device__ __forceinline__ void wave_order() { asm volatile("" ::: "memory"); }
@@ -517,11 +506,11 @@ __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long ba
     return;
   }
   const f2* __restrict__ x = static_cast<const f2*>(a.x) + ch * a.x_stride + base;
+  OscRun R{};
   f2 St = f2{1.0f, 0.0f};
   if constexpr (PR == Pre::Ssb) {
-    const int h = (w * WR) / kScanCH;
-    St = cmul(phasor_q64(static_cast<uint64_t>(a.k0 + base + 1 + static_cast<long long>(h) * kScanCH), a.step),
-              a.tab[(w * WR) % kScanCH + l]);
+    R = osc_run(a.osc, static_cast<uint64_t>(a.k0 + base), cnt);
+    if (R.kind == 1) St = cmul(R.S, a.osc.mtab[e0]);
   }
   f2 v[SC];
 #pragma unroll
@@ -534,7 +523,14 @@ __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long ba
     const f2 z = v[k];
     float o;
     if constexpr (PR == Pre::Ssb) {
-      const f2 p = cmul(St, a.tab[64 * k]);
+      const int e = e0 + 64 * k;
+      f2 p;
+      if (R.kind == 1) {
+        p = cmul(St, a.osc.mtab[64 * k]);
+        if (a.osc.prof) p *= splat2(a.osc.prof[(a.osc.ctr0 + static_cast<uint32_t>(R.k) + e + 1u) & 1023u]);
+      } else {
+        p = osc_get(a.osc, R, e);
+      }
       o = __builtin_fmaf(z.x, p.x, z.y * p.y);  // ssb.rs:37
     } else if constexpr (PR == Pre::AmSqrt) {
       o = __builtin_fmaf(z.x, z.x, z.y * z.y);  // am.rs:204
@@ -891,13 +887,9 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   const bool last = c == nchunk - 1;
   const float* __restrict__ ci = a.carry_in + ch * kScanCarry;
   const R rr = RecSel<RK>::make(a.c);
-  f2 Sw[2] = {f2{1.0f, 0.0f}, f2{1.0f, 0.0f}};  // oscillator at the chunk's samples 0 and kScanCH
-  if constexpr (PR == Pre::Fm) {
-    if (a.translate) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) Sw[h] = phasor_q64(static_cast<uint64_t>(a.k0 + base + 1 + h * kScanCH), a.step);
-    }
-  }
+  OscRun Ro{};  // the translator's outputs of the chunk
+  if constexpr (PR == Pre::Fm)
+    if (a.translate) Ro = osc_run(a.osc, static_cast<uint64_t>(a.k0 + base), cnt);
   // Batches of 8 samples per thread: every load of a batch issued before any is used
   // (unconditional, index clamped into [0, n)), then the pre-map. (A guarded load per
   // sample compiles to a branch around each, which waits for its load before the LDS
@@ -909,9 +901,6 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   const long long nl = a.n - 1;
 #pragma unroll 1
   for (int k0 = 0; k0 < SC; k0 += 8) {
-    const int h = k0 >= KT ? 1 : 0;
-    const long long bh = base + h * kScanCH;
-    const f2 Sh = h ? Sw[1] : Sw[0];
     f2 z[8], zp[8], zq = f2{0.0f, 0.0f};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -929,14 +918,14 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
       // sample: no second load, no second translation); lane 0 of the wave needs the sample before the wave's run of
       // row k0 + j: lane j of the wave loads and maps it for all eight j in one load.
       const long long iq = base + (t & ~63) + (k0 + (lane & 7)) * NT - 1;
-      zq = cin_v<PR>(a, (static_cast<const f2*>(a.x) + ch * a.x_stride)[max(min(iq, nl), 0LL)], iq, bh, Sh);
+      zq = cin_v<PR>(a, (static_cast<const f2*>(a.x) + ch * a.x_stride)[max(min(iq, nl), 0LL)], iq, base, Ro);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int e = t + (k0 + j) * NT;
       float o;
       if constexpr (kPair) {
-        const f2 zc = cin_v<PR>(a, z[j], base + e, bh, Sh);
+        const f2 zc = cin_v<PR>(a, z[j], base + e, base, Ro);
         f2 p = f2{wave_up<1>(zc.x), wave_up<1>(zc.y)};
         if (lane == 0) {
           p = f2{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(zq.x), j)),
@@ -945,7 +934,7 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
         }
         o = fm_disc(zc, p, a.c.k);
       } else {
-        o = premap_v<PR>(a, ch, base + e, bh, Sh, z[j], zp[j]);
+        o = premap_v<PR>(a, ch, base + e, base, Ro, z[j], zp[j]);
       }
       if (e < cnt) sb[posS<SC>(e)] = o;
     }
@@ -1062,8 +1051,7 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
     for (int i = S; i < 6; ++i) co[i] = 0.0f;
     if constexpr (PR == Pre::Fm || PR == Pre::Pm) {
       const f2* x = static_cast<const f2*>(a.x) + ch * a.x_stride;
-      const int h = (cnt - 1) / kScanCH;
-      const f2 z = cin<PR>(a, x, a.n - 1, base + h * kScanCH, Sw[h]);
+      const f2 z = cin<PR>(a, x, a.n - 1, base, Ro);
       co[6] = z.x;
       co[7] = z.y;
     } else {
@@ -1085,7 +1073,7 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
 // k_lpdc_sp: the host checks ||A^kSpWarm||), and (I, side Q) x RF NCO stored.
 // carry: [I state 4][Q state 4] floats.
 __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
-                                                   uint64_t k0, uint64_t step_aud, uint64_t step_rf, float side,
+                                                   uint64_t k0, const OscDev aud, const OscDev rf, float side,
                                                    ScanCoef cf, const double* __restrict__ mlp,
                                                    const float* __restrict__ carry_in, float* __restrict__ carry_out) {
   constexpr int S = 4;
@@ -1099,24 +1087,19 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
   const int cnt = static_cast<int>(min(static_cast<long long>(CH), n - base));
   const bool last = o0 + (cnt - warm) >= n;
   const RecLP4 lp{{cf.b0, cf.b1, cf.b2, cf.a1, cf.a2}};
-  // Oscillator phasors of element e = t + k NT (the coalesced order of the staging and
-  // of the stores): P_t tab[k], P_t the exact phasor of element t, tab[k] = e^{j theta k NT}
-  // (audio NCO: tab[0..16), RF NCO: tab[16..32)) — two phasor evaluations per thread
-  // instead of two per sample.
-  __shared__ f2 tab[2 * C];
-  if (t < 2 * C) tab[t] = phasor_q64(static_cast<uint64_t>(t & (C - 1)) * NT, t < C ? step_aud : step_rf);
-  const f2 Pa = phasor_q64(k0 + static_cast<uint64_t>(base + t) + 1, step_aud);
-  const f2 Pr = phasor_q64(k0 + static_cast<uint64_t>(base + t) + 1, step_rf);
+  // Oscillator outputs k0 + base + e of element e = t + k NT (the coalesced order of the
+  // staging and of the stores): the audio and RF Rotators' cursors over the chunk.
+  const OscRun Ra = osc_run(aud, k0 + static_cast<uint64_t>(base), cnt);
+  const OscRun Rr = osc_run(rf, k0 + static_cast<uint64_t>(base), cnt);
   {  // stage: x p.re, x p.im (ssb.rs:53-54), coalesced loads first (unconditional, clamped)
     float v[C];
 #pragma unroll
     for (int k = 0; k < C; ++k) v[k] = x[min(base + t + k * NT, n - 1)];
-    __syncthreads();  // tab
 #pragma unroll
     for (int k = 0; k < C; ++k) {
       const int e = t + k * NT;
       const float xv = e < cnt ? v[k] : 0.0f;
-      const f2 p = cmul(Pa, tab[k]);
+      const f2 p = e < cnt ? osc_get(aud, Ra, e) : f2{1.0f, 0.0f};
       sb[0][pos(e)] = xv * p.x;
       sb[1][pos(e)] = xv * p.y;
     }
@@ -1221,7 +1204,7 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
 #pragma unroll
   for (int k = 0; k < C; ++k) {  // ssb.rs:55-60
     const int e = t + k * NT;
-    if (e >= warm && e < cnt) y[base + e] = cmul_rot(zs[e + (e >> 4)], cmul(Pr, tab[C + k]));
+    if (e >= warm && e < cnt) y[base + e] = cmul_rot(zs[e + (e >> 4)], osc_get(rf, Rr, e));
   }
 }
 
@@ -1247,14 +1230,13 @@ int scan_state_dim(RecK rec) {
   }
 }
 
-void launch_ssb_mod_sp(const float* x, f2* y, long long n, uint64_t k0, uint64_t step_aud, uint64_t step_rf,
+void launch_ssb_mod_sp(const float* x, f2* y, long long n, uint64_t k0, const OscDev& aud, const OscDev& rf,
                        float side, const ScanCoef& c, const double* mats_lp, const float* carry_in, float* carry_out,
                        hipStream_t s) {
   if (n <= 0) return;
   const long long grid = lpdc_sp_chunks(n);
   if (grid > (1LL << 31) - 1) throw HipError("single-pass SSB modulator grid too large");
-  k_ssb_mod_sp<<<static_cast<int>(grid), NT, 0, s>>>(x, y, n, k0, step_aud, step_rf, side, c, mats_lp, carry_in,
-                                                     carry_out);
+  k_ssb_mod_sp<<<static_cast<int>(grid), NT, 0, s>>>(x, y, n, k0, aud, rf, side, c, mats_lp, carry_in, carry_out);
   ORION_LAUNCH_CHECK();
 }
 

@@ -11,50 +11,30 @@
 namespace orion {
 
 // ---------------------------------------------------------------- NCO --
-// Rotator::rotate_block (dsp/rotator.rs:74-85) in closed form: output i uses the
-// phasor after k0+i+1 steps, e^{j theta (k0+i+1)}. tab_dev = e^{j theta p},
-// p < kRotTile.
+// Rotator / Nco kernel tile (k_fir.hip k_rotator): samples per workgroup tile.
 constexpr int kRotTile = 4096;
 // ---- analog modulators (k_mod.hip; modulate/am.rs, fm.rs, ssb.rs) ----
-void launch_am_mod(const float* x, f2* y, long long n, uint64_t k0, uint64_t step, float cl, float mi, float g,
+// Every oscillator: o (hip_common.hpp OscDev), sample i of a call = output k0 + i.
+void launch_am_mod(const float* x, f2* y, long long n, uint64_t k0, const OscDev& o, float cl, float mi, float g,
                    bool clamp, hipStream_t s);
-// pm.rs:36-47: out = mix_with_nco((cos kp x, sin kp x) * g, rf phasor k0 + i + 1)
-void launch_pm_mod(const float* x, f2* y, long long n, uint64_t k0, uint64_t step, float kp, float g, hipStream_t s);
-// u = [x p.re | x p.im] (planar, 2n floats), p = audio NCO phasor k0 + i + 1
-void launch_ssb_mod_front(const float* x, float* u, long long n, uint64_t k0, uint64_t step, hipStream_t s);
-// y = (v[i], side v[n + i]) * rf phasor k0 + i + 1
-void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, uint64_t step, float side, hipStream_t s);
+// pm.rs:36-47: out = mix_with_nco((cos kp x, sin kp x) * g, rf phasor)
+void launch_pm_mod(const float* x, f2* y, long long n, uint64_t k0, const OscDev& o, float kp, float g, hipStream_t s);
+// u = [x p.re | x p.im] (planar, 2n floats), p = audio NCO phasor
+void launch_ssb_mod_front(const float* x, float* u, long long n, uint64_t k0, const OscDev& o, hipStream_t s);
+// y = (v[i], side v[n + i]) * rf phasor
+void launch_ssb_mod_back(const float* v, f2* y, long long n, uint64_t k0, const OscDev& o, float side, hipStream_t s);
 // FM phase accumulator: sums = fm_mod_chunks(n) uint64 of workspace; carry_in /
 // carry_out: the running phase as a Q0.64 turn count (one uint64 each, ping-pong
-// between calls; zero = phase 0)
-// rtab: e^{j theta k}, k < fm_mod_rtab_len(), of the RF oscillator
+// between calls; zero = phase 0); o: the RF Nco.
 long long fm_mod_chunks(long long n);
 // Single-pass form: rec = fm_mod_chunks(n) * 8 u32 look-back records (zeroed when
 // allocated), epoch = this launch's tag (never reused while a record may hold it).
 // err: the handle's host-visible error word (a look-back wait that timed out).
 void launch_fm_mod_sp(const float* x, f2* y, long long n, float kf, float gain, uint32_t* rec, uint32_t epoch,
-                      const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
-                      int* err, hipStream_t s);
-int fm_mod_rtab_len();
+                      const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, const OscDev& o, int* err,
+                      hipStream_t s);
 void launch_fm_mod(const float* x, f2* y, long long n, float kf, float gain, uint64_t* sums,
-                   const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, uint64_t step, const f2* rtab,
-                   hipStream_t s);
-// Oscillator on the device (k_fir.hip k_rotator; design.hpp RecTable). Output k of
-// the oscillator (k steps after the table's start state; the phasor after k + 1 steps):
-//   tab[k]                                            k < n_tab (the reference's own)
-//   tab[cyc_start + (k - cyc_start) mod cyc_len]      cyc_len > 0 (its cycle, forever)
-//   prof[(ctr0 + k + 1) & 1023] e^{j 2 pi ph / 2^64}, ph = mbase + (k + 1 - n_tab) mstep
-//                                                     otherwise (the model; prof null:
-//                                                     magnitude 1 — the closed form)
-// mtab: e^{j 2 pi p mstep / 2^64}, p < kRotTile (the model within a tile).
-// cyc_len is 0 or >= kRotTile (rec_table unrolls short cycles).
-struct OscDev {
-  const f2* tab;
-  const float* prof;
-  const f2* mtab;
-  uint64_t n_tab, cyc_start, cyc_len, mbase, mstep;
-  uint32_t ctr0;
-};
+                   const uint64_t* carry_in, uint64_t* carry_out, uint64_t k0, const OscDev& o, hipStream_t s);
 // Oscillator blocks (k_fir.hip k_rotator): output i of a call is oscillator output
 // k0 + i. mode: 0 Rotator::rotate_block (rotator.rs:74-85, cf32 -> cf32), 1
 // Rotator::mix_usb_block (rotator.rs:88-94, cf32 -> f32), 2 mix_with_nco (nco.rs:63-66,

@@ -72,12 +72,12 @@ void RefOsc::build(const RecState& st, uint64_t closed_anchor_q64) {
     tab_.mbase = closed_anchor_q64;
     tab_.mstep = osc_.step_q64;
   } else {
-    tab_ = rec_table(osc_.w_re, osc_.w_im, st, budget_, kRotTile, osc_.step_q64);
+    tab_ = rec_table(osc_.w_re, osc_.w_im, st, budget_, kOscSpan, osc_.step_q64);
   }
   if (tab_.n) dtab_.upload(tab_.z.data(), tab_.z.size() * sizeof(float));
   if (!tab_.prof.empty()) dprof_.upload(tab_.prof.data(), tab_.prof.size() * sizeof(float));
   const double th = static_cast<double>(static_cast<long double>(tab_.mstep) / 18446744073709551616.0L * kTwoPiL);
-  const auto mt = phasor_table(th, kRotTile);
+  const auto mt = phasor_table(th, kOscSpan);
   dmtab_.upload(mt.data(), mt.size() * sizeof(float));
 }
 

@@ -65,10 +65,9 @@ struct ScanArgs {
   const void* x;  long long x_stride;  // inputs: cf32 or f32, [ch][x_stride]
   void* y;        long long y_stride;  // outputs: f32, [ch][y_stride]
   long long n;                         // samples this call
-  long long k0;                        // samples consumed by earlier calls (oscillators)
+  long long k0;                        // oscillator output of sample 0 (translator / BFO)
   int translate;                       // Pre::Fm: apply the fm.rs:48-58 translator
-  uint64_t step;                       // oscillator Q0.64 step (translator / BFO)
-  const f2* tab;                       // e^{j theta p}, p < kScanCH (oscillator table)
+  OscDev osc;                          // the translator's / BFO's Rotator (hip_common.hpp)
   const double* mats;                  // ScanMatsLayout (f64: see iir.hpp matvec_acc)
   double* aggs;                        // [ch][nblk][S]
   double* sin;                         // [ch][nblk][S] state entering each workgroup
@@ -94,7 +93,7 @@ constexpr int kSpCH = kSpC * kScanNT;
 long long lpdc_sp_demod_chunks(long long n, int sc, int warm);  // warm: kSpWarm, or 0 for the DcBlocker alone
 // SsbPhasingMod in one pass (k_ssb_mod_sp): valid when ||A_lp^kSpWarm|| is
 // negligible; mats_lp = the LP4 scan matrices; carry = [I 4][Q 4] floats.
-void launch_ssb_mod_sp(const float* x, f2* y, long long n, uint64_t k0, uint64_t step_aud, uint64_t step_rf,
+void launch_ssb_mod_sp(const float* x, f2* y, long long n, uint64_t k0, const OscDev& aud, const OscDev& rf,
                        float side, const ScanCoef& c, const double* mats_lp, const float* carry_in, float* carry_out,
                        hipStream_t s);
 void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, uint32_t* rec, uint32_t epoch,

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "osc.hpp"
 #include "scan.hpp"
 
 namespace orion {
@@ -82,10 +83,12 @@ class ScanStage {
   // 0 auto (single pass where valid), 1 force the three-kernel scan (tests)
   void set_mode(int m) { mode_ = m; }
   bool lpdc_single_pass() const { return sp_ok_; }
-  void set_osc(const Oscillator& o) {
-    step_ = o.step_q64;
-    const auto t = phasor_table(o.theta, kScanCH);
-    tab_.upload(t.data(), t.size() * sizeof(float));
+  // The stage's Rotator (the SSB BFO, ssb.rs:18; the FM translator, fm.rs:35): the
+  // reference recurrence, tabulated (osc.hpp RefOsc); its outputs advance with the samples.
+  void set_osc(float freq_hz, float fs) { osc_ = std::make_unique<RefOsc>(freq_hz, fs); }
+  RefOsc* osc() { return osc_.get(); }
+  void reset_osc() {
+    if (osc_) osc_->reset();
   }
   void set_carry(const std::vector<float>& per_ch) {  // kScanCarry floats, same for every channel
     std::vector<float> c(static_cast<size_t>(nch_) * kScanCarry);
@@ -105,10 +108,9 @@ class ScanStage {
     a.y = y;
     a.y_stride = y_stride;
     a.n = n;
-    a.k0 = k0;
+    a.k0 = osc_ ? static_cast<long long>(osc_->count()) : k0;
     a.translate = translate_ ? 1 : 0;
-    a.step = step_;
-    a.tab = tab_.size() ? tab_.as<f2>() : nullptr;
+    if (osc_) a.osc = osc_->dev();
     a.mats = mats_.as<double>();
     a.aggs = ws_.as<double>();
     a.sin = ws_.as<double>() + nblk * nch_ * S_;
@@ -134,6 +136,7 @@ class ScanStage {
     } else {
       launch_scan(rec_, pre_, post_, a, nch_, s);
     }
+    if (osc_) osc_->advance(static_cast<uint64_t>(n));
     cur_ ^= 1;
   }
 
@@ -144,8 +147,8 @@ class ScanStage {
   ScanCoef c_;
   int nch_, S_;
   bool translate_ = false;
-  uint64_t step_ = 0;
-  DevBuf mats_, tab_, carry_[2], ws_, mats_lp_, rec_buf_;
+  std::unique_ptr<RefOsc> osc_;
+  DevBuf mats_, carry_[2], ws_, mats_lp_, rec_buf_;
   int cur_ = 0;
   bool sp_ok_ = false;   // k_lpdc_sp (LpDcCascade after SSB / AM-abs)
   bool sp1_ok_ = false;  // k_scan_sp (stages that forget within one chunk)
@@ -200,6 +203,11 @@ class OneStageBlock : public ScanBlock {
   ScanStage& stage() { return *st_; }
   std::vector<float> taps(int) const override { return coef_; }
   int configure(int option, long long value) override {
+    if (option == kOptNcoTable && st_->osc()) {  // the BFO / translator Rotator's table budget
+      if (value < 0 || static_cast<unsigned long long>(value) > kNcoTableMax) return -3;
+      st_->osc()->set_budget(static_cast<uint64_t>(value));
+      return 0;
+    }
     if (option != kOptScanPath) return -4;
     if (value != 0 && value != 1) return -3;
     st_->set_mode(static_cast<int>(value));
@@ -212,7 +220,10 @@ class OneStageBlock : public ScanBlock {
     st_->run(in, static_cast<long long>(stride), static_cast<long long>(n), out, static_cast<long long>(out_stride),
              static_cast<long long>(k0_), dev_err(), s);
   }
-  void reset_state() override { st_->set_carry(carry0_); }
+  void reset_state() override {
+    st_->set_carry(carry0_);
+    st_->reset_osc();
+  }
   std::unique_ptr<ScanStage> st_;
   std::vector<float> carry0_;
 };
@@ -350,7 +361,7 @@ class LpDcBlock final : public ScanBlock {
 class SsbModBlock final : public Block {
  public:
   SsbModBlock(float fs, float bw, float if_hz, float rf_hz, bool usb)
-      : aud_(oscillator(if_hz, fs)), rf_(oscillator(rf_hz, fs)), side_(usb ? 1.0f : -1.0f) {
+      : aud_(if_hz, fs), rf_(rf_hz, fs), side_(usb ? 1.0f : -1.0f) {  // ssb.rs:32-33: two Rotators
     b_ = lp_cascade_design(fs, bw * 0.9f);  // ssb.rs:25
     const StateSpace ss = lp_cascade_ss(b_);
     st_ = std::make_unique<ScanStage>(RecK::LP4, Pre::Real, Post::Id, ss, coef_lp(b_), 2);
@@ -375,27 +386,35 @@ class SsbModBlock final : public Block {
     if (n == 0) return {0, 0};
     const long long nn = static_cast<long long>(n);
     if (sp_ok_ && mode_ == 0) {
-      launch_ssb_mod_sp(static_cast<const float*>(in), static_cast<f2*>(out), nn, k_, aud_.step_q64, rf_.step_q64,
+      launch_ssb_mod_sp(static_cast<const float*>(in), static_cast<f2*>(out), nn, aud_.count(), aud_.dev(), rf_.dev(),
                         side_, coef_lp(b_), mats_.as<double>(), carry_[cur_].as<float>(), carry_[cur_ ^ 1].as<float>(),
                         s);
       cur_ ^= 1;
     } else {
       u_.resize(2 * n * sizeof(float));
       v_.resize(2 * n * sizeof(float));
-      launch_ssb_mod_front(static_cast<const float*>(in), u_.as<float>(), nn, k_, aud_.step_q64, s);
-      st_->run(u_.as<void>(), nn, nn, v_.as<void>(), nn, static_cast<long long>(k_), dev_err(), s);
-      launch_ssb_mod_back(v_.as<float>(), static_cast<f2*>(out), nn, k_, rf_.step_q64, side_, s);
+      launch_ssb_mod_front(static_cast<const float*>(in), u_.as<float>(), nn, aud_.count(), aud_.dev(), s);
+      st_->run(u_.as<void>(), nn, nn, v_.as<void>(), nn, 0, dev_err(), s);
+      launch_ssb_mod_back(v_.as<float>(), static_cast<f2*>(out), nn, rf_.count(), rf_.dev(), side_, s);
     }
-    k_ += n;
+    aud_.advance(n);
+    rf_.advance(n);
     return {n, n};
   }
   void reset() override {
-    k_ = 0;
+    aud_.reset();
+    rf_.reset();
     st_->set_carry(carry_zero());
     reset_sp();
     ORION_HIP(hipDeviceSynchronize());
   }
   int configure(int option, long long value) override {  // single pass where valid, or the three passes
+    if (option == kOptNcoTable) {  // both Rotators' table budgets
+      if (value < 0 || static_cast<unsigned long long>(value) > kNcoTableMax) return -3;
+      aud_.set_budget(static_cast<uint64_t>(value));
+      rf_.set_budget(static_cast<uint64_t>(value));
+      return 0;
+    }
     if (option != kOptModPasses) return -4;
     if (value != 0 && value != 1 && value != 3) return -3;
     mode_ = value == 3 ? 1 : 0;
@@ -410,14 +429,13 @@ class SsbModBlock final : public Block {
     for (auto& c : carry_) c.upload(z.data(), z.size() * sizeof(float));
     cur_ = 0;
   }
-  Oscillator aud_, rf_;
+  RefOsc aud_, rf_;
   float side_;
   BiquadCoeffs b_;
   std::unique_ptr<ScanStage> st_;
   DevBuf u_, v_, mats_, carry_[2];
   bool sp_ok_ = false;
   int mode_ = 0, cur_ = 0;
-  uint64_t k_ = 0;
 };
 
 }  // namespace
@@ -476,7 +494,7 @@ std::unique_ptr<Block> make_fm_demod(float fs, float dev_hz, float audio_bw) {
 int fm_demod_with_translate(Block* b, float freq_hz) {
   auto* o = dynamic_cast<OneStageBlock*>(b);
   if (!o || std::strcmp(b->name(), "FmQuadratureDemod") != 0) return -4;
-  o->stage().set_osc(oscillator(freq_hz, o->coef_[6]));  // Rotator::new(freq_hz, fs), fm.rs:35
+  o->stage().set_osc(freq_hz, o->coef_[6]);  // Rotator::new(freq_hz, fs), fm.rs:35
   o->stage().set_translate(true);
   return 0;
 }
@@ -496,7 +514,7 @@ std::unique_ptr<Block> make_ssb_demod(float fs, float bfo_hz, float audio_bw, in
   ScanCoef c = coef_lp(d.bq);
   c.r = d.r;
   auto st = std::make_unique<ScanStage>(RecK::LPDC, Pre::Ssb, Post::Id, lpdc_ss(d), c, nch);
-  st->set_osc(oscillator(bfo_hz, fs));  // ssb.rs:18 Rotator::new(bfo_hz, fs)
+  st->set_osc(bfo_hz, fs);  // ssb.rs:18 Rotator::new(bfo_hz, fs)
   auto blk = std::make_unique<OneStageBlock>("SsbProductDemod", Dt::C32, nch, std::move(st), carry_zero());
   blk->coef_ = {d.bq.b0, d.bq.b1, d.bq.b2, d.bq.a1, d.bq.a2, d.r};
   return blk;

@@ -94,7 +94,7 @@ def test_osc_table_is_the_reference_recurrence(oracle, f, fs, cyc):
     got, cs, cl, nt = orion_sdr.osc_table_phasors(f, fs, n, 1 << 20)
     ref = oracle.nco(np.zeros(n, np.complex64), f, fs, gen=True)
     if cyc:
-        assert cs == cyc[0] and cl % cyc[1] == 0 and cl >= 4096
+        assert cs == cyc[0] and cl % cyc[1] == 0 and cl >= 16384
         assert nt == cs + cl
     else:
         assert cl == 0 and nt == 1 << 20
