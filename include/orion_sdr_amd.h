@@ -54,6 +54,10 @@ const char* orion_last_error(void);          /* thread-local message of the last
 int orion_device_count(void);
 int orion_set_device(int device);
 int orion_synchronize(void* stream);
+/* Pinned (page-locked) host memory for the host-buffer path (no reference counterpart):
+ * orion_block_process DMAs it without staging copies. NULL on failure. */
+void* orion_host_alloc(size_t bytes);
+int orion_host_free(void* p);
 int orion_device_cus(void);                 /* compute units of the current device (< 0: error) */
 /* On-box bandwidth probe (no reference counterpart; bench.py's measured read
  * peak): one streaming read of the first orion_diag_stream_read_bytes(bytes)
@@ -236,7 +240,15 @@ int orion_wbfm_chain_configure(orion_block* b, int path, int max_segments);
 int orion_wbfm_chain_seek(orion_block* b, uint64_t index);
 
 /* ---- Block contract (core.rs:12-22) ------------------------------------ */
-/* Host buffers (synchronous). */
+/* Host buffers (synchronous): the path Block::process with host slices takes.
+ * Pinned host memory (orion_host_alloc, or hipHostRegister'ed) moves by DMA directly;
+ * pageable memory through the handle's pinned staging buffers, the CPU copy of one
+ * chunk overlapping the DMA of the next. Blocks whose output does not depend on how a
+ * call is cut (Rotator, Nco, FirLowpass, FirLowpassIq, FirDecimator at multiples of m,
+ * the AM / PM / FM modulators, AgcRms(Iq), CwKeyedMod) run calls >= 2^21 samples as a
+ * pipeline of chunks on three streams (H2D, kernel, D2H overlapped); the others upload,
+ * run one device call and download. Either way the output equals one
+ * orion_block_process_device call on the same input, bit for bit. */
 int orion_block_process(orion_block* b, const void* in, size_t n_in, void* out, size_t out_cap,
                         orion_work_report* wr);
 /* Device buffers (asynchronous on `stream`). Overlapping in/out ranges are

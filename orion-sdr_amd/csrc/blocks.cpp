@@ -36,10 +36,6 @@ void DevBuf::upload(const void* h, size_t bytes, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------- Block --
-Block::~Block() {
-  if (hs_) (void)hipStreamDestroy(hs_);
-  if (err_) (void)hipHostFree(err_);
-}
 hipStream_t Block::host_stream() {
   if (!hs_) ORION_HIP(hipStreamCreateWithFlags(&hs_, hipStreamNonBlocking));
   return hs_;
@@ -96,24 +92,197 @@ int device_cus() {
   return ncu;
 }
 
+// ---------------------------------------------------------- host path ----
+constexpr size_t kPinBytes = 8u << 20;        // one pinned staging buffer (two per direction)
+constexpr size_t kPipeSamples = 1u << 20;     // calls of >= 2 kPipeSamples take the chunked pipeline
+
+struct Block::HostPipe {
+  hipStream_t s_in = nullptr, s_out = nullptr;
+  void* pin_in[2] = {nullptr, nullptr};
+  void* pin_out[2] = {nullptr, nullptr};
+  hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr}, ev_k[2] = {nullptr, nullptr};
+  DevBuf din[2], dout[2];
+  ~HostPipe() {
+    for (int b = 0; b < 2; ++b) {
+      if (pin_in[b]) (void)hipHostFree(pin_in[b]);
+      if (pin_out[b]) (void)hipHostFree(pin_out[b]);
+      if (ev_in[b]) (void)hipEventDestroy(ev_in[b]);
+      if (ev_out[b]) (void)hipEventDestroy(ev_out[b]);
+      if (ev_k[b]) (void)hipEventDestroy(ev_k[b]);
+    }
+    if (s_in) (void)hipStreamDestroy(s_in);
+    if (s_out) (void)hipStreamDestroy(s_out);
+  }
+  // host -> device on stream s: DMA from pinned memory directly, else through the two
+  // pinned buffers (the CPU copy of chunk c + 1 overlaps the DMA of chunk c).
+  void h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    if (host_is_pinned(src)) {
+      ORION_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+      return;
+    }
+    for (size_t off = 0, c = 0; off < bytes; off += kPinBytes, ++c) {
+      const int b = static_cast<int>(c & 1);
+      const size_t len = std::min(kPinBytes, bytes - off);
+      ORION_HIP(hipEventSynchronize(ev_in[b]));  // the DMA of chunk c - 2 has read pin_in[b]
+      std::memcpy(pin_in[b], static_cast<const char*>(src) + off, len);
+      ORION_HIP(hipMemcpyAsync(static_cast<char*>(dst) + off, pin_in[b], len, hipMemcpyHostToDevice, s));
+      ORION_HIP(hipEventRecord(ev_in[b], s));
+    }
+  }
+  // device -> host after everything enqueued on s; synchronous.
+  void d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (!bytes) {
+      ORION_HIP(hipStreamSynchronize(s));
+      return;
+    }
+    if (host_is_pinned(dst)) {
+      ORION_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+      ORION_HIP(hipStreamSynchronize(s));
+      return;
+    }
+    size_t prev_off = 0, prev_len = 0;
+    int prev_b = -1;
+    for (size_t off = 0, c = 0; off < bytes; off += kPinBytes, ++c) {
+      const int b = static_cast<int>(c & 1);
+      const size_t len = std::min(kPinBytes, bytes - off);
+      ORION_HIP(hipMemcpyAsync(pin_out[b], static_cast<const char*>(src) + off, len, hipMemcpyDeviceToHost, s));
+      ORION_HIP(hipEventRecord(ev_out[b], s));
+      if (prev_b >= 0) {  // the CPU copy of chunk c - 1 overlaps the DMA of chunk c
+        ORION_HIP(hipEventSynchronize(ev_out[prev_b]));
+        std::memcpy(static_cast<char*>(dst) + prev_off, pin_out[prev_b], prev_len);
+      }
+      prev_b = b;
+      prev_off = off;
+      prev_len = len;
+    }
+    ORION_HIP(hipEventSynchronize(ev_out[prev_b]));
+    std::memcpy(static_cast<char*>(dst) + prev_off, pin_out[prev_b], prev_len);
+  }
+};
+
+Block::~Block() {
+  delete pipe_;
+  if (hs_) (void)hipStreamDestroy(hs_);
+  if (err_) (void)hipHostFree(err_);
+}
+
+Block::HostPipe& Block::pipe() {
+  if (!pipe_) {
+    auto p = std::make_unique<HostPipe>();
+    ORION_HIP(hipStreamCreateWithFlags(&p->s_in, hipStreamNonBlocking));
+    ORION_HIP(hipStreamCreateWithFlags(&p->s_out, hipStreamNonBlocking));
+    for (int b = 0; b < 2; ++b) {
+      ORION_HIP(hipHostMalloc(&p->pin_in[b], kPinBytes, hipHostMallocDefault));
+      ORION_HIP(hipHostMalloc(&p->pin_out[b], kPinBytes, hipHostMallocDefault));
+      ORION_HIP(hipEventCreateWithFlags(&p->ev_in[b], hipEventDisableTiming));
+      ORION_HIP(hipEventCreateWithFlags(&p->ev_out[b], hipEventDisableTiming));
+      ORION_HIP(hipEventCreateWithFlags(&p->ev_k[b], hipEventDisableTiming));
+    }
+    pipe_ = p.release();
+  }
+  return *pipe_;
+}
+
+void* host_alloc(size_t bytes) {
+  void* p = nullptr;
+  ORION_HIP(hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault));
+  return p;
+}
+void host_free(void* p) {
+  if (p) ORION_HIP(hipHostFree(p));
+}
+bool host_is_pinned(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: not an error of ours
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
 WorkReport Block::process_host(const void* in, size_t n_in, void* out, size_t out_cap) {
   hipStream_t s = host_stream();
   const int nch = channels();
+  const size_t q = chunk_quantum();
+  if (q && nch == 1 && n_in >= 2 * kPipeSamples) return host_chunked(in, n_in, out, out_cap, q);
+  HostPipe& P = pipe();
   const size_t ib = dt_size(in_type()), ob = dt_size(out_type());
   stage_in_.resize(std::max<size_t>(1, n_in * nch * ib));
   stage_out_.resize(std::max<size_t>(1, out_cap * nch * ob));
-  if (n_in) ORION_HIP(hipMemcpyAsync(stage_in_.as<void>(), in, n_in * nch * ib, hipMemcpyHostToDevice, s));
+  P.h2d(stage_in_.as<void>(), in, n_in * nch * ib, s);
   WorkReport w = process_device(stage_in_.as<void>(), n_in, stage_out_.as<void>(), out_cap, s);
   if (nch == 1) {
+    P.d2h(out, stage_out_.as<void>(), w.out_written * ob, s);
+  } else {
     if (w.out_written)
-      ORION_HIP(hipMemcpyAsync(out, stage_out_.as<void>(), w.out_written * ob, hipMemcpyDeviceToHost, s));
-  } else if (w.out_written) {
-    ORION_HIP(hipMemcpy2DAsync(out, out_cap * ob, stage_out_.as<void>(), out_cap * ob,
-                               w.out_written * ob, nch, hipMemcpyDeviceToHost, s));
+      ORION_HIP(hipMemcpy2DAsync(out, out_cap * ob, stage_out_.as<void>(), out_cap * ob, w.out_written * ob, nch,
+                                 hipMemcpyDeviceToHost, s));
+    ORION_HIP(hipStreamSynchronize(s));
   }
-  ORION_HIP(hipStreamSynchronize(s));
   check_device_errors();
   return w;
+}
+
+// Chunks of Q samples (a multiple of q; a chunk's input and output each fit one pinned
+// staging buffer) through two device buffer pairs: chunk c's H2D on s_in, its kernel on
+// the handle's stream, its D2H on s_out, each waiting on an event of the stage before;
+// buffers of parity c & 1 are reused by chunk c + 2 only after its copy-out. The CPU
+// copies of pageable memory (into pin_in, out of pin_out) run between the enqueues, so
+// they overlap the DMA and the kernels of the neighbouring chunks.
+WorkReport Block::host_chunked(const void* in, size_t n_in, void* out, size_t out_cap, size_t q) {
+  HostPipe& P = pipe();
+  hipStream_t sc = host_stream();
+  const size_t ib = dt_size(in_type()), ob = dt_size(out_type());
+  const size_t Q = std::max<size_t>(q, kPinBytes / std::max(ib, ob) / q * q);
+  const size_t n = consumes_all() ? n_in : std::min(n_in, out_cap);  // decim.rs:72-75 / 1:1 min()
+  const size_t n_out = std::min(out_len(n), out_cap);
+  const bool pin_i = host_is_pinned(in), pin_o = host_is_pinned(out);
+  for (int b = 0; b < 2; ++b) {
+    P.din[b].resize(Q * ib);
+    P.dout[b].resize(std::max<size_t>(1, out_len(Q)) * ob);
+  }
+  size_t pend_off[2] = {0, 0}, pend_len[2] = {0, 0};
+  bool used[2] = {false, false};
+  auto retire = [&](int b) {  // chunk c - 2's copy-out: its buffers of parity b are free after it
+    if (!used[b]) return;
+    ORION_HIP(hipEventSynchronize(P.ev_out[b]));
+    if (pend_len[b] && !pin_o) std::memcpy(static_cast<char*>(out) + pend_off[b] * ob, P.pin_out[b], pend_len[b] * ob);
+    used[b] = false;
+  };
+  size_t written = 0;
+  int c = 0;
+  for (size_t off = 0; off < n; off += Q, ++c) {
+    const int b = c & 1;
+    const size_t len = std::min(Q, n - off);
+    retire(b);
+    const char* src = static_cast<const char*>(in) + off * ib;
+    if (pin_i) {
+      ORION_HIP(hipMemcpyAsync(P.din[b].as<void>(), src, len * ib, hipMemcpyHostToDevice, P.s_in));
+    } else {
+      std::memcpy(P.pin_in[b], src, len * ib);  // pin_in[b]'s previous DMA (chunk c - 2) is done: retire(b)
+      ORION_HIP(hipMemcpyAsync(P.din[b].as<void>(), P.pin_in[b], len * ib, hipMemcpyHostToDevice, P.s_in));
+    }
+    ORION_HIP(hipEventRecord(P.ev_in[b], P.s_in));
+    ORION_HIP(hipStreamWaitEvent(sc, P.ev_in[b], 0));
+    const WorkReport w = process_device(P.din[b].as<void>(), len, P.dout[b].as<void>(), out_len(len), sc);
+    ORION_HIP(hipEventRecord(P.ev_k[b], sc));
+    ORION_HIP(hipStreamWaitEvent(P.s_out, P.ev_k[b], 0));
+    const size_t keep = written < n_out ? std::min(w.out_written, n_out - written) : 0;
+    if (keep)
+      ORION_HIP(hipMemcpyAsync(pin_o ? static_cast<void*>(static_cast<char*>(out) + written * ob) : P.pin_out[b],
+                               P.dout[b].as<void>(), keep * ob, hipMemcpyDeviceToHost, P.s_out));
+    ORION_HIP(hipEventRecord(P.ev_out[b], P.s_out));
+    pend_off[b] = written;
+    pend_len[b] = keep;
+    used[b] = true;
+    written += w.out_written;
+  }
+  retire(c & 1);  // the older of the two chunks in flight first
+  retire((c + 1) & 1);
+  ORION_HIP(hipStreamSynchronize(sc));
+  check_device_errors();
+  return {n, n_out};
 }
 
 namespace {
@@ -152,6 +321,7 @@ class OscBlock : public Block {
   std::vector<float> taps(int) const override { return {osc_.osc().w_re, osc_.osc().w_im}; }
   void set_freq(float f, float fs) { osc_.retune(f, fs); }
   float fs() const { return osc_.fs(); }
+  size_t chunk_quantum() const override { return kRotTile; }  // tiles keep their alignment
   int configure(int option, long long value) override {
     if (option != kOptNcoTable) return -4;
     if (value < 0 || static_cast<unsigned long long>(value) > kNcoTableMax) return -3;
@@ -215,6 +385,7 @@ class AmModBlock final : public Block {
   const char* name() const override { return "AmDsbMod"; }
   Dt in_type() const override { return Dt::F32; }
   Dt out_type() const override { return Dt::C32; }
+  size_t chunk_quantum() const override { return 4096; }
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const size_t n = std::min(n_in, out_cap);  // am.rs:45
     launch_am_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), osc_.count(),
@@ -241,6 +412,7 @@ class PmModBlock final : public Block {
   const char* name() const override { return "PmDirectPhaseMod"; }
   Dt in_type() const override { return Dt::F32; }
   Dt out_type() const override { return Dt::C32; }
+  size_t chunk_quantum() const override { return 4096; }
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const size_t n = std::min(n_in, out_cap);  // pm.rs:37
     launch_pm_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), osc_.count(),
@@ -271,6 +443,7 @@ class FmModBlock final : public Block {
   const char* name() const override { return "FmPhaseAccumMod"; }
   Dt in_type() const override { return Dt::F32; }
   Dt out_type() const override { return Dt::C32; }
+  size_t chunk_quantum() const override { return 4096; }  // thread groups and chunks keep their alignment
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const size_t n = std::min(n_in, out_cap);  // fm.rs:47
     if (n == 0) return {0, 0};
@@ -352,6 +525,8 @@ class DecimBlock final : public Block {
   const char* name() const override { return "FirDecimator"; }
   Dt in_type() const override { return Dt::C32; }
   Dt out_type() const override { return Dt::C32; }
+  size_t chunk_quantum() const override { return 512 * m_; }  // the phase restarts at every call: cut at multiples of m
+  bool consumes_all() const override { return true; }
   int channels() const override { return nch_; }
   size_t out_len(size_t n) const override { return (n + m_ - 1) / m_; }
   WorkReport process_device(const void* in, size_t n, void* out, size_t out_cap, hipStream_t s) override {
@@ -402,6 +577,7 @@ class FirRealBlock final : public Block {
   const char* name() const override { return "FirLowpass"; }
   Dt in_type() const override { return Dt::F32; }
   Dt out_type() const override { return Dt::F32; }
+  size_t chunk_quantum() const override { return 4096; }
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const size_t n = std::min(n_in, out_cap);  // fir.rs:48
     if (n == 0) return {0, 0};
@@ -447,6 +623,7 @@ class FirIqBlock final : public Block {
   const char* name() const override { return "FirLowpassIq"; }
   Dt in_type() const override { return Dt::C32; }
   Dt out_type() const override { return Dt::C32; }
+  size_t chunk_quantum() const override { return 4096; }
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const size_t n = std::min(n_in, out_cap);  // fir.rs:288
     if (n == 0) return {0, 0};
@@ -573,6 +750,7 @@ class WbfmBlock final : public Block {
   const char* name() const override { return "WbfmChain"; }
   Dt in_type() const override { return Dt::C32; }
   Dt out_type() const override { return Dt::F32; }
+  bool consumes_all() const override { return true; }
   int channels() const override { return nch_; }
   size_t out_len(size_t n) const override { return (n + p_.m - 1) / p_.m; }
   WorkReport process_device(const void* in, size_t n, void* out, size_t out_cap, hipStream_t s) override {

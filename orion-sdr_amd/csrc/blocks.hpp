@@ -61,8 +61,22 @@ class Block {
   // in[ch*n_in + i] and write out[ch*out_cap + j].
   virtual WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap,
                                     hipStream_t s) = 0;
-  // Host buffers: stage through device memory, synchronous.
+  // Host buffers (the Block contract a host caller drives, core.rs:12-22), synchronous.
+  // Host memory that is pinned (orion_host_alloc / hipHostRegister) moves by DMA
+  // directly; pageable memory through two pinned staging buffers per direction, the
+  // CPU copy of one chunk overlapping the DMA of the other. Blocks whose output is
+  // bitwise independent of how a call is cut (chunk_quantum() > 0: the oscillators,
+  // FIRs, decimators, elementwise modulators) run as a pipeline of chunks on three
+  // streams (H2D, kernel, D2H overlapped); every other block (the IIR scans, the WBFM
+  // chain) uploads the call, runs ONE device call and downloads: in both cases the
+  // result equals one orion_block_process_device call on the same input bit for bit.
   WorkReport process_host(const void* in, size_t n_in, void* out, size_t out_cap);
+  // Sample granularity at which k calls on consecutive chunks give bit-identical
+  // results to one call (0: none; a decimator: m, whose phase restarts every call).
+  virtual size_t chunk_quantum() const { return 0; }
+  // All n_in inputs are consumed whatever out_cap is (FirDecimator, decim.rs:72-75; the
+  // WBFM chain); otherwise n = min(n_in, out_cap) (1:1 blocks).
+  virtual bool consumes_all() const { return false; }
   // Errors a kernel flagged in the handle's device error word (a cross-workgroup
   // wait that timed out): throws HipError and clears the word if one is set. The
   // word is host-visible (pinned, coherent), so this needs no sync; it sees every
@@ -87,9 +101,19 @@ class Block {
   DevBuf stage_in_, stage_out_;
 
  private:
+  struct HostPipe;  // pinned staging, copy streams and events of process_host
+  HostPipe& pipe();
+  WorkReport host_chunked(const void* in, size_t n_in, void* out, size_t out_cap, size_t q);
   hipStream_t hs_ = nullptr;
   int* err_ = nullptr;
+  HostPipe* pipe_ = nullptr;  // owned (deleted in ~Block, where HostPipe is complete)
 };
+
+// Pinned host memory for callers (orion_host_alloc): process_host then moves it by DMA
+// without staging copies.
+void* host_alloc(size_t bytes);
+void host_free(void* p);
+bool host_is_pinned(const void* p);
 
 // dsp/rotator.rs:8-95 (rotate_block). C32 -> C32.
 std::unique_ptr<Block> make_rotator(float freq_hz, float fs);

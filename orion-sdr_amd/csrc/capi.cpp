@@ -83,6 +83,20 @@ int orion_diag_stream_read(const void* dev, size_t bytes, void* stream) {
     return ORION_OK;
   });
 }
+void* orion_host_alloc(size_t bytes) {
+  try {
+    return orion::host_alloc(bytes);
+  } catch (const std::exception& e) {
+    fail(ORION_E_HIP, e.what());
+    return nullptr;
+  }
+}
+int orion_host_free(void* p) {
+  return guarded([&] {
+    orion::host_free(p);
+    return ORION_OK;
+  });
+}
 int orion_device_cus(void) {
   try {
     return orion::device_cus();

@@ -367,6 +367,7 @@ class AgcBlock final : public Block {
   const char* name() const override { return iq_ ? "AgcRmsIq" : "AgcRms"; }
   Dt in_type() const override { return iq_ ? Dt::C32 : Dt::F32; }
   Dt out_type() const override { return iq_ ? Dt::C32 : Dt::F32; }
+  size_t chunk_quantum() const override { return 1; }  // outputs are the sequential recurrence's, bit for bit
   bool alias_ok() const override { return true; }  // overlapping in/out: staged through a copy
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const long long n = static_cast<long long>(std::min(n_in, out_cap));  // agc.rs:49
@@ -411,6 +412,7 @@ class CwModBlock final : public Block {
   const char* name() const override { return "CwKeyedMod"; }
   Dt in_type() const override { return Dt::F32; }
   Dt out_type() const override { return Dt::C32; }
+  size_t chunk_quantum() const override { return 1; }  // outputs are the sequential recurrence's, bit for bit
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const long long n = static_cast<long long>(std::min(n_in, out_cap));  // cw.rs:47
     if (n == 0) return {0, 0};

@@ -153,6 +153,7 @@ def _load():
         "orion_diag_spin": (i, [vp, C.c_uint32, C.c_uint32, C.c_double]),
         "orion_diag_stream_create": (vp, [C.c_uint32]), "orion_diag_stream_destroy": (i, [vp]),
         "orion_device_cus": (i, []),
+        "orion_host_alloc": (vp, [sz]), "orion_host_free": (i, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -827,6 +828,21 @@ def osc_table_phasors(freq_hz: float, fs: float, n: int, budget: int = 1 << 20):
     _check(_L.orion_osc_table_phasors(freq_hz, fs, int(budget), out.ctypes.data, out.size, C.byref(cs),
                                       C.byref(cl), C.byref(nt)))
     return out, int(cs.value), int(cl.value), int(nt.value)
+
+
+def pinned_empty(shape, dtype) -> np.ndarray:
+    """A numpy array in pinned host memory (orion_host_alloc): the host-buffer path
+    (orion_block_process) DMAs it without staging copies. Freed with the array."""
+    import weakref
+
+    dt = np.dtype(dtype)
+    nbytes = int(np.prod(shape)) * dt.itemsize
+    p = _L.orion_host_alloc(max(1, nbytes))
+    if not p:
+        raise OrionError(f"orion_sdr: pinned allocation failed: {_err()}")
+    buf = (C.c_char * max(1, nbytes)).from_address(p)
+    weakref.finalize(buf, _L.orion_host_free, C.c_void_p(p))
+    return np.frombuffer(buf, dt, count=int(np.prod(shape))).reshape(shape)
 
 
 def device_count() -> int:

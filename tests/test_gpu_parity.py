@@ -710,6 +710,71 @@ def test_cross_workgroup_waits_under_contention(gpu_lib, oracle):
             gpu_lib.diag_stream_destroy(sm)
 
 
+# ---- host-buffer path (orion_block_process: pinned staging, chunked pipeline) --------
+def _host_path_cases(gpu_lib, oracle):
+    a = _speech(1 << 22)
+    return [
+        ("Rotator", lambda: gpu_lib.Rotator(1.234e6, 10e6), "c"),
+        ("Nco", lambda: gpu_lib.Nco(12e3, 48e3), "c"),
+        ("FirLowpassIq", lambda: gpu_lib.FirLowpassIq.design(127, 0.2, 60.0), "c"),
+        ("FirLowpass", lambda: gpu_lib.FirLowpass(1.25e6, 15e3, 10e3), "r"),
+        ("FirDecimator m=8", lambda: gpu_lib.FirDecimator(10e6, 8, 200e3, 79e3), "c"),
+        ("FirDecimator m=3", lambda: gpu_lib.FirDecimator(48e3, 3, 7e3, 1.5e3), "c"),
+        ("AmDsbMod", lambda: gpu_lib.AmDsbMod(FS, 5e3, 1.0, 0.5), "r"),
+        ("FmPhaseAccumMod", lambda: gpu_lib.FmPhaseAccumMod(10e6, 75e3, 1.5e6), "r"),
+        ("AgcRmsIq", lambda: gpu_lib.AgcRmsIq(FS, 1.0, 20.0, 0.3), "c"),
+        ("WbfmChain", lambda: gpu_lib.WbfmChain(), "c"),
+        ("FmQuadratureDemod", lambda: gpu_lib.FmQuadratureDemod(FS, 2500.0, 5000.0), "c"),
+        ("SsbProductDemod", lambda: gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0), "c"),
+    ], a
+
+
+def test_host_path_equals_device_call(gpu_lib, oracle):
+    """orion_block_process on host buffers (pageable and pinned) gives
+    what one orion_block_process_device call gives on the same input, bit for bit:
+    chunk-invariant blocks through the 3-stream chunked pipeline (calls >= 2^21
+    samples, ragged tails), the others through one staged device call. Then a ragged
+    call sequence (the decimator's per-call phase restart, decim.rs:66-71) and an output
+    capacity below the call's output (out_written = min, all input consumed)."""
+    import torch
+
+    cases, a = _host_path_cases(gpu_lib, oracle)
+    n = (1 << 21) + 12_345
+    xc = cnoise(n, 0.5)
+    xr = a[:n]
+    for name, mk, kind in cases:
+        x = xc if kind == "c" else xr
+        xd = torch.from_numpy(x).cuda()
+        dev = mk().process_device(xd).cpu().numpy()
+        torch.cuda.synchronize()
+        host = mk().process(x)
+        assert _bits_equal(host, dev), f"{name}: pageable host path differs from one device call"
+        pin_in = gpu_lib.pinned_empty(x.shape, x.dtype)
+        pin_in[:] = x
+        b = mk()
+        pin_out = gpu_lib.pinned_empty((b.out_len(n),), host.dtype)
+        wr = b.process_into(pin_in, pin_out)
+        assert (wr.in_read, wr.out_written) == (n, len(host)) and _bits_equal(pin_out, host), f"{name}: pinned"
+        print(f"[parity] host path {name}: pageable and pinned == one device call, bit for bit ({n} samples)")
+    # ragged call sequences: host calls == device calls, call by call
+    cuts = [0, 3, 1_000_003, 1_000_010, (1 << 21) + 17, n]
+    for name, mk, kind in cases[:6]:
+        x = xc if kind == "c" else xr
+        hb, db = mk(), mk()
+        for i0, i1 in zip(cuts[:-1], cuts[1:]):
+            h = hb.process(x[i0:i1])
+            d = db.process_device(torch.from_numpy(x[i0:i1]).cuda()).cpu().numpy()
+            assert _bits_equal(h, d), f"{name}: ragged call [{i0}, {i1})"
+    # out_cap below the call's output: the decimator consumes everything and writes the head
+    for name, mk, kind in cases[4:6]:
+        hb, db = mk(), mk()
+        full = db.process(xc[: (1 << 21) + 5])
+        out = np.zeros(1000, np.complex64)
+        wr = hb.process_into(xc[: (1 << 21) + 5], out)
+        assert (wr.in_read, wr.out_written) == ((1 << 21) + 5, 1000) and _bits_equal(out, full[:1000])
+        assert _bits_equal(hb.process(xc[: 80_000]), db.process(xc[: 80_000]))  # the state advanced through all input
+
+
 # ---- device-resident path (orion_block_process_device) ---------------------------------
 def test_device_path_alignment_and_capacity(gpu_lib, oracle):
     """process_device on torch tensors: 16-B aligned and 8-B aligned (x[1:], the
