@@ -17,6 +17,10 @@ single-threaded) timed on this host on a bounded prefix of the same input; the
 multi-channel configs time the oracle on min(channels, 16) host threads, one
 channel per thread, on a bounded prefix of that many channels.
 
+At N = 1 the C2 line also carries "host_fed" (SURVEY §8d's H2D-inclusive figure): the
+same chain driven from host memory through orion_block_process, pinned and pageable,
+beside the box's raw pinned H2D rate. It is never `value`.
+
 Other workloads (--config c1|c3|c4|c5) are available for DESIGN.md tables; the
 driver's default line is c2. C1 (BASELINE configs[0], the reference's CPU block
 graph: 127-tap FirLowpassIq over 2^20 cf32) is compute-bound (508 flop per 16 B),
@@ -261,6 +265,50 @@ def cpu_baseline(x_dev, cfg, seconds_target, max_samples):
                 seconds=round(dt, 2)), xh[:n], ref
 
 
+def host_fed(x_dev, passes=3):
+    """SURVEY §8(d)'s second figure: the C2 chain fed from HOST memory through the
+    path a host caller takes (orion_block_process: Block::process on host slices,
+    core.rs:12-22). The same rank-0 input, copied to (a) pinned host memory
+    (orion_host_alloc: DMA straight from it) and (b) ordinary pageable memory (the
+    handle's pinned staging, CPU copies overlapping the DMA); a fresh chain handle,
+    `passes` timed calls each after one warm-up call. Beside them the box's raw
+    pinned H2D rate for the same bytes (hipMemcpy through torch's copy_), and the
+    fraction of it the pinned path reaches (8 B in per sample)."""
+    n = x_dev.shape[-1]
+    pin = orion_sdr.pinned_empty((n,), np.complex64)
+    pin[:] = x_dev.cpu().numpy()
+    res = {}
+    for mode, src in (("pinned", pin), ("pageable", None)):
+        if src is None:
+            src = np.array(pin, copy=True)
+        blk = orion_sdr.WbfmChain(f_off=OFFSETS[0])
+        out = (orion_sdr.pinned_empty((blk.out_len(n),), np.float32) if mode == "pinned"
+               else np.empty(blk.out_len(n), np.float32))
+        blk.process_into(src, out)
+        t0 = time.perf_counter()
+        for _ in range(passes):
+            blk.process_into(src, out)
+        dt = time.perf_counter() - t0
+        res[mode] = passes * n / dt / 1e6
+        del src, out, blk
+    dst = torch.empty_like(x_dev)
+    src_t = torch.from_numpy(pin)
+    torch.cuda.synchronize()
+    dst.copy_(src_t)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        dst.copy_(src_t)
+    torch.cuda.synchronize()
+    h2d = passes * n * 8 / (time.perf_counter() - t0) / 1e9
+    del dst, src_t, pin
+    return {"value": round(res["pinned"], 2), "unit": "Msamples/s", "input": "pinned host memory (orion_host_alloc)",
+            "pageable_value": round(res["pageable"], 2), "h2d_gbs_measured": round(h2d, 2),
+            "frac_of_h2d": round(res["pinned"] * 8e6 / (h2d * 1e9), 4), "passes": passes,
+            "path": "orion_block_process (host buffers): upload, one device call, download; bytes 8 B in + 0.5 B out "
+                    "per sample"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -271,6 +319,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-max-samples", type=int, default=1 << 24)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-h2d", action="store_true", help="skip the host-fed (H2D-inclusive) C2 figure")
     ap.add_argument("--rest", type=float, default=0.0, help="idle seconds between input synthesis and the warm-up")
     ap.add_argument("--shard", default="stream", choices=["stream", "channels"],
                     help="C2 on several GPUs: one stream cut in time (with a halo), or a channel per GPU")
@@ -365,6 +414,11 @@ def main():
         tr = json.load(open(traffic_file))
         if tr.get("samples_per_launch") == samples:
             line["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
+    if rank == 0 and world == 1 and args.config == "c2" and not args.no_h2d:
+        try:
+            line["host_fed"] = host_fed(x)
+        except Exception as e:  # noqa: BLE001  (the bench line must still print)
+            line["host_fed"] = {"error": str(e)[:160]}
     if rank == 0 and world == 1 and not args.no_cpu and args.config in ("c1", "c2"):
         res = cpu_baseline(x, args.config, args.cpu_seconds, args.cpu_max_samples)
         if res:

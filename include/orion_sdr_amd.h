@@ -219,9 +219,10 @@ orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float*
 /* Engine tuning and tests (no reference counterpart): the kernel path of a WBFM
  * chain handle. ORION_WBFM_AUTO picks the segmented single kernel when the
  * LpCascade decays fast enough for it (the WBFM defaults), else two kernels;
- * max_segments > 0 caps the segmented kernel's waves (0 = the resident
- * capacity). ORION_E_TYPE if b is not a WBFM chain, ORION_E_ARG if the design
- * cannot run on that path.
+ * max_segments > 0 sets the segmented kernel's segments (waves; more than the
+ * resident capacity runs several rounds), 0 = one round at the resident capacity.
+ * ORION_E_TYPE if b is not a WBFM chain, ORION_E_ARG if the design cannot run on
+ * that path.
  * Residency: the segmented kernel launches one round of waves (at most the
  * device's resident capacity) and each segment waits, bounded, for the end state
  * its predecessor publishes. A predecessor is always the previous workgroup in

@@ -1355,7 +1355,10 @@ void launch_wbfm_seg(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmFused
   static_assert(sg::L == kSgL, "sub-range geometry");
   if (a.n_dec <= 0 || nch <= 0) return;
   const int cap = resident_per_cu(reinterpret_cast<const void*>(k_wbfm_seg<true, false>), 64) * device_cus();
-  const long long capx = max_segments > 0 ? std::min<long long>(max_segments, cap) : cap;
+  // max_segments > 0: that many segments, also beyond one round of resident waves: every
+  // segment waits only on the previous blockIdx, dispatched before it, so a grid of
+  // several rounds cannot deadlock (later rounds start as earlier segments retire)
+  const long long capx = max_segments > 0 ? max_segments : cap;
   const long long nsub_ch = (a.n_dec + kSgL - 1) / kSgL;
   long long spc = std::max<long long>(1, std::min<long long>(capx / nch, nsub_ch));
   const long long S = (nsub_ch + spc - 1) / spc * kSgL;

@@ -562,6 +562,24 @@ def test_wbfm_kernel_paths(gpu_lib, oracle, path, max_seg, n):
     report(f"wbfm path={path} max_segments={max_seg} n={n} nrmse", nrmse(got, oracle.wbfm(x)), 1e-5)
 
 
+def test_wbfm_multi_round_segments(gpu_lib, oracle):
+    """More segments than resident waves (several rounds of the grid): safe because a
+    segment's predecessor is always the previous blockIdx. 2^25 samples = 4096
+    sub-ranges as 4096 and 8192-capped segments (2+ rounds) against the default one
+    round, and the causal prefix against the oracle."""
+    import torch
+
+    n = 1 << 25
+    x = wbfm_input(n)
+    xd = torch.from_numpy(x).cuda()
+    base = gpu_lib.WbfmChain().process_device(xd).cpu().numpy()
+    ref = oracle.wbfm(x[: 1 << 20])
+    for segs in (4096, 6000):
+        got = gpu_lib.WbfmChain().configure("segmented", segs).process_device(xd).cpu().numpy()
+        report(f"wbfm {segs} segments (multi-round) vs one round nrmse", nrmse(got, base), 1e-5)
+        report(f"wbfm {segs} segments causal prefix vs oracle nrmse", nrmse(got[: len(ref)], ref), 1e-5)
+
+
 @pytest.mark.parametrize("path,max_seg", [("segmented", 2), ("segmented", 5), ("segmented", 8), ("split", 0)])
 def test_wbfm_segmented_streaming_and_channels(gpu_lib, oracle, path, max_seg):
     """Carried state across calls and independent channels with several
