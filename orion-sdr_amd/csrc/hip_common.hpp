@@ -103,37 +103,46 @@ struct OscDev {
   uint64_t n_tab, cyc_start, cyc_len, mbase, mstep;
   uint32_t ctr0;
 };
-// A cursor over outputs k .. k + len - 1 (len <= kOscSpan): kind 0 all from the
-// table, 1 all modelled, 2 mixed; j = the table index of k (wrapped into the cycle:
-// with cyc_len >= kOscSpan a run wraps at most once); S = the model phasor of k.
+// A cursor over outputs k .. k + len - 1 (len <= kOscSpan), all fields wave-uniform:
+// kind 0 every output from the table, 1 every output modelled, 2 mixed (the first
+// `rem` from the table); j = the table index of k, wrapped into the cycle (with
+// cyc_len >= kOscSpan a run wraps at most once; tables hold < 2^31 outputs, so table
+// indices are 32-bit); S = the model phasor of k; klo = k mod 2^32 (profile index).
 struct OscRun {
-  uint64_t k, j;
-  f2 S;
+  uint32_t j, rem, klo;
   int kind;
+  f2 S;
 };
 __device__ __forceinline__ OscRun osc_run(const OscDev& o, uint64_t k, int len) {
   OscRun r;
-  r.k = k;
   const bool cyc = o.cyc_len != 0;
   r.kind = (cyc || k + static_cast<uint64_t>(len) <= o.n_tab) ? 0 : (k >= o.n_tab ? 1 : 2);
-  r.j = (cyc && k >= o.n_tab) ? o.cyc_start + (k - o.cyc_start) % o.cyc_len : k;
+  r.j = static_cast<uint32_t>((cyc && k >= o.n_tab) ? o.cyc_start + (k - o.cyc_start) % o.cyc_len : k);
+  r.rem = r.kind == 2 ? static_cast<uint32_t>(o.n_tab - k) : 0u;
+  r.klo = static_cast<uint32_t>(k);
   r.S = r.kind != 0 ? phasor_at(o.mbase + (k + 1 - o.n_tab) * o.mstep) : f2{1.0f, 0.0f};
   return r;
 }
-// Output r.k + off (off < the run's len), from the table or the model (tm: mtab[off]).
-__device__ __forceinline__ f2 osc_get_tm(const OscDev& o, const OscRun& r, int off, f2 tm) {
-  if (r.kind == 0 || (r.kind == 2 && r.k + static_cast<uint64_t>(off) < o.n_tab)) {
-    uint64_t j = r.j + static_cast<uint64_t>(off);
-    if (j >= o.n_tab) j -= o.cyc_len;  // (only with a cycle)
-    return o.tab[j];
-  }
+// Table output r.k + off (kind 0, or kind 2 with off < rem).
+__device__ __forceinline__ f2 osc_tab(const OscDev& o, const OscRun& r, int off) {
+  uint32_t j = r.j + static_cast<uint32_t>(off);
+  if (j >= static_cast<uint32_t>(o.n_tab)) j -= static_cast<uint32_t>(o.cyc_len);  // (only with a cycle)
+  return o.tab[j];
+}
+// Model output r.k + off from tm = mtab[off] (or any equal product of step phasors).
+__device__ __forceinline__ f2 osc_model(const OscDev& o, const OscRun& r, int off, f2 tm) {
   f2 p = cmul(r.S, tm);
-  if (o.prof) p *= splat2(o.prof[(o.ctr0 + static_cast<uint32_t>(r.k) + static_cast<uint32_t>(off) + 1u) & 1023u]);
+  if (o.prof) p *= splat2(o.prof[(o.ctr0 + r.klo + static_cast<uint32_t>(off) + 1u) & 1023u]);
   return p;
 }
+// Output r.k + off (off < the run's len), from the table or the model (tm: mtab[off]).
+__device__ __forceinline__ f2 osc_get_tm(const OscDev& o, const OscRun& r, int off, f2 tm) {
+  if (r.kind == 0 || (r.kind == 2 && static_cast<uint32_t>(off) < r.rem)) return osc_tab(o, r, off);
+  return osc_model(o, r, off, tm);
+}
 __device__ __forceinline__ f2 osc_get(const OscDev& o, const OscRun& r, int off) {
-  const bool model = !(r.kind == 0 || (r.kind == 2 && r.k + static_cast<uint64_t>(off) < o.n_tab));
-  return osc_get_tm(o, r, off, model ? o.mtab[off] : f2{1.0f, 0.0f});
+  if (r.kind == 0 || (r.kind == 2 && static_cast<uint32_t>(off) < r.rem)) return osc_tab(o, r, off);
+  return osc_model(o, r, off, o.mtab[off]);
 }
 
 // Output k alone (no cursor: kernels that visit samples in no run order).

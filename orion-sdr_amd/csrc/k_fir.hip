@@ -23,65 +23,67 @@ constexpr int kMaxGrid = 2048;  // memory-bound: cap and grid-stride (2048 = 8 W
 // rotator.rs:88-94), kNcoMix mix_with_nco (non-FMA product, nco.rs:63-66), kNcoGen
 // the phasors themselves (nco.rs:42-58 next_cs, no input).
 enum : int { kRotate = 0, kUsb = 1, kNcoMix = 2, kNcoGen = 3 };
+#ifndef ORION_ROT_MINW
+#define ORION_ROT_MINW 6  // waves per SIMD k_rotator is compiled for (8: <= 64 VGPRs, 6 B of spills)
+#endif
 template <bool A16, int MODE>
-__global__ __launch_bounds__(NT) void k_rotator(const f2* __restrict__ x, void* __restrict__ yv, long long n,
+__global__ __launch_bounds__(NT, ORION_ROT_MINW) void k_rotator(const f2* __restrict__ x, void* __restrict__ yv, long long n,
                                                 uint64_t k0, const OscDev o) {
   constexpr int PER = kRotTile / (2 * NT);  // pairs per thread per tile (8)
   const int t = threadIdx.x;
-  f2 tb[PER][2];  // model steps e^{j 2 pi p mstep}, p = 2t + 2 NT i (+1): tile-invariant
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const f4 v = *reinterpret_cast<const f4*>(o.mtab + 2 * t + 2 * NT * i);
-    tb[i][0] = f2{v.x, v.y};
-    tb[i][1] = f2{v.z, v.w};
-  }
   for (long long tile = static_cast<long long>(blockIdx.x) * kRotTile; tile < n;
        tile += static_cast<long long>(gridDim.x) * kRotTile) {
     const OscRun r = osc_run(o, k0 + static_cast<uint64_t>(tile), kRotTile);  // tile-uniform
+    // one tile-uniform branch per form of the phasor: table, model, mixed
+    auto body = [&](auto get) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int off = 2 * t + 2 * NT * i;
-      const long long P = tile + off;
-      if (P >= n) break;
-      f2 v0 = f2{0.0f, 0.0f}, v1 = f2{0.0f, 0.0f};
-      const bool full = P + 1 < n;
-      if constexpr (MODE != kNcoGen) {
-        if (A16 && full) {
-          const f4 v = *reinterpret_cast<const f4*>(x + P);
-          v0 = f2{v.x, v.y};
-          v1 = f2{v.z, v.w};
+      for (int i = 0; i < PER; ++i) {
+        const int off = 2 * t + 2 * NT * i;
+        const long long P = tile + off;
+        if (P >= n) break;
+        f2 v0 = f2{0.0f, 0.0f}, v1 = f2{0.0f, 0.0f};
+        const bool full = P + 1 < n;
+        if constexpr (MODE != kNcoGen) {
+          if (A16 && full) {
+            const f4 v = *reinterpret_cast<const f4*>(x + P);
+            v0 = f2{v.x, v.y};
+            v1 = f2{v.z, v.w};
+          } else {
+            v0 = x[P];
+            if (full) v1 = x[P + 1];
+          }
+        }
+        const f2 p0 = get(off);
+        const f2 p1 = get(off + 1);
+        if constexpr (MODE == kUsb) {
+          float* y = static_cast<float*>(yv);
+          y[P] = __builtin_fmaf(v0.x, p0.x, v0.y * p0.y);
+          if (full) y[P + 1] = __builtin_fmaf(v1.x, p1.x, v1.y * p1.y);
         } else {
-          v0 = x[P];
-          if (full) v1 = x[P + 1];
+          f2* y = static_cast<f2*>(yv);
+          f2 o0, o1;
+          if constexpr (MODE == kRotate) {
+            o0 = cmul_rot(v0, p0);
+            o1 = cmul_rot(v1, p1);
+          } else if constexpr (MODE == kNcoMix) {  // (x.re c - x.im s, x.re s + x.im c), no FMA
+            o0 = f2{v0.x * p0.x - v0.y * p0.y, v0.x * p0.y + v0.y * p0.x};
+            o1 = f2{v1.x * p1.x - v1.y * p1.y, v1.x * p1.y + v1.y * p1.x};
+          } else {
+            o0 = p0;
+            o1 = p1;
+          }
+          if (A16 && full) {
+            *reinterpret_cast<f4*>(y + P) = f4{o0.x, o0.y, o1.x, o1.y};
+          } else {
+            y[P] = o0;
+            if (full) y[P + 1] = o1;
+          }
         }
       }
-      const f2 p0 = osc_get_tm(o, r, off, tb[i][0]);
-      const f2 p1 = osc_get_tm(o, r, off + 1, tb[i][1]);
-      if constexpr (MODE == kUsb) {
-        float* y = static_cast<float*>(yv);
-        y[P] = __builtin_fmaf(v0.x, p0.x, v0.y * p0.y);
-        if (full) y[P + 1] = __builtin_fmaf(v1.x, p1.x, v1.y * p1.y);
-      } else {
-        f2* y = static_cast<f2*>(yv);
-        f2 o0, o1;
-        if constexpr (MODE == kRotate) {
-          o0 = cmul_rot(v0, p0);
-          o1 = cmul_rot(v1, p1);
-        } else if constexpr (MODE == kNcoMix) {  // (x.re c - x.im s, x.re s + x.im c), no FMA
-          o0 = f2{v0.x * p0.x - v0.y * p0.y, v0.x * p0.y + v0.y * p0.x};
-          o1 = f2{v1.x * p1.x - v1.y * p1.y, v1.x * p1.y + v1.y * p1.x};
-        } else {
-          o0 = p0;
-          o1 = p1;
-        }
-        if (A16 && full) {
-          *reinterpret_cast<f4*>(y + P) = f4{o0.x, o0.y, o1.x, o1.y};
-        } else {
-          y[P] = o0;
-          if (full) y[P + 1] = o1;
-        }
-      }
-    }
+    };
+    if (r.kind == 0) body([&](int off) { return osc_tab(o, r, off); });
+    else if (r.kind == 1) body([&](int off) { return osc_model(o, r, off, o.mtab[off]); });
+    else body([&](int off) { return osc_get(o, r, off); });
   }
 }
 

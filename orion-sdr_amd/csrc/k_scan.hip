@@ -13,11 +13,11 @@ constexpr int PADN = CH + CH / 16 + 16;
 #ifndef ORION_SP_ABL
 #define ORION_SP_ABL 0  // timing experiments only: 1 no phasor table, 2 no look-back, 4 no LP scan, 8 staging + stores only
 #endif
-#ifndef ORION_SP_WAVES
-#define ORION_SP_WAVES 1  // occupancy hint for k_lpdc_sp (experiments: 6)
-#endif
 #ifndef ORION_SP_MINW
 #define ORION_SP_MINW 4  // waves per SIMD k_lpdc_sp is compiled for at kSpC samples per lane (<= 128 VGPRs)
+#endif
+#ifndef ORION_SP_MINW16
+#define ORION_SP_MINW16 6  // the same at 16 samples per lane (ORION_LPDC_SC=16 experiments)
 #endif
 #ifndef ORION_SCAN_SP_MINW
 #define ORION_SCAN_SP_MINW 4  // waves per SIMD k_scan_sp is compiled for (4: <= 128 VGPRs, spills 52-132 B)
@@ -506,33 +506,39 @@ __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long ba
     return;
   }
   const f2* __restrict__ x = static_cast<const f2*>(a.x) + ch * a.x_stride + base;
-  OscRun R{};
-  f2 St = f2{1.0f, 0.0f};
-  if constexpr (PR == Pre::Ssb) {
-    R = osc_run(a.osc, static_cast<uint64_t>(a.k0 + base), cnt);
-    if (R.kind == 1) St = cmul(R.S, a.osc.mtab[e0]);
-  }
   f2 v[SC];
 #pragma unroll
   for (int k = 0; k < SC; ++k) {
     const int e = e0 + 64 * k;
     v[k] = e < cnt ? x[e] : f2{0.0f, 0.0f};
   }
+  if constexpr (PR == Pre::Ssb) {
+    // the BFO's outputs over the chunk: one tile-uniform branch per form, so only one
+    // form's temporaries are live beside v[]
+    const OscRun R = osc_run(a.osc, static_cast<uint64_t>(a.k0 + base), cnt);
+    auto put = [&](int k, f2 p) {
+      sb[posS<SC>(e0 + 64 * k)] = __builtin_fmaf(v[k].x, p.x, v[k].y * p.y);  // ssb.rs:37
+    };
+    if (R.kind == 0) {
+#pragma unroll
+      for (int k = 0; k < SC; ++k) put(k, osc_tab(a.osc, R, e0 + 64 * k));
+    } else if (R.kind == 1) {
+      const f2 St = cmul(R.S, a.osc.mtab[e0]);  // the model: (S mtab[e0]) mtab[64 k]
+      OscRun Rt = R;
+      Rt.S = St;
+#pragma unroll
+      for (int k = 0; k < SC; ++k) put(k, osc_model(a.osc, Rt, e0 + 64 * k, a.osc.mtab[64 * k]));
+    } else {
+#pragma unroll
+      for (int k = 0; k < SC; ++k) put(k, osc_get(a.osc, R, e0 + 64 * k));
+    }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < SC; ++k) {
     const f2 z = v[k];
     float o;
-    if constexpr (PR == Pre::Ssb) {
-      const int e = e0 + 64 * k;
-      f2 p;
-      if (R.kind == 1) {
-        p = cmul(St, a.osc.mtab[64 * k]);
-        if (a.osc.prof) p *= splat2(a.osc.prof[(a.osc.ctr0 + static_cast<uint32_t>(R.k) + e + 1u) & 1023u]);
-      } else {
-        p = osc_get(a.osc, R, e);
-      }
-      o = __builtin_fmaf(z.x, p.x, z.y * p.y);  // ssb.rs:37
-    } else if constexpr (PR == Pre::AmSqrt) {
+    if constexpr (PR == Pre::AmSqrt) {
       o = __builtin_fmaf(z.x, z.x, z.y * z.y);  // am.rs:204
     } else {
       o = __builtin_fmaf(a.c.k1, fabsf(z.x), a.c.k2 * fabsf(z.y));  // am.rs:238
@@ -542,7 +548,7 @@ __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long ba
 }
 
 template <Pre PR, int SC>
-__global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_WAVES) void k_lpdc_sp(const ScanArgs a, const double* __restrict__ mlp, int nch,
+__global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void k_lpdc_sp(const ScanArgs a, const double* __restrict__ mlp, int nch,
                                                uint32_t* __restrict__ rec, uint32_t epoch) {
   constexpr int S = 4;
   constexpr int C = SC, CH = SC * NT, PADN = CH + CH / SC + SC;
@@ -1252,21 +1258,21 @@ long long lpdc_sp_demod_chunks(long long n, int sc, int warm) {
 void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, uint32_t* rec, uint32_t epoch,
                     hipStream_t s) {
   if (a.n <= 0 || nch <= 0) return;
-  const long long grid = lpdc_sp_demod_chunks(a.n, kSpC, pre == Pre::Real ? 0 : kSpWarm) * nch;
+  const long long grid = lpdc_sp_demod_chunks(a.n, kLpdcSC, pre == Pre::Real ? 0 : kSpWarm) * nch;
   if (grid > (1LL << 31) - 1) throw HipError("single-pass scan grid too large");
   const int g = static_cast<int>(grid);
   if (pre == Pre::Ssb) {
-    k_lpdc_sp<Pre::Ssb, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    k_lpdc_sp<Pre::Ssb, kLpdcSC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else if (pre == Pre::AmAbs) {
-    k_lpdc_sp<Pre::AmAbs, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    k_lpdc_sp<Pre::AmAbs, kLpdcSC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else if (pre == Pre::Real) {
-    k_lpdc_sp<Pre::Real, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    k_lpdc_sp<Pre::Real, kLpdcSC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else if (pre == Pre::AmSqrt) {
-    k_lpdc_sp<Pre::AmSqrt, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    k_lpdc_sp<Pre::AmSqrt, kLpdcSC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else if (pre == Pre::RealLp) {
-    k_lpdc_sp<Pre::RealLp, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    k_lpdc_sp<Pre::RealLp, kLpdcSC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else if (pre == Pre::RealLpSqrt) {
-    k_lpdc_sp<Pre::RealLpSqrt, kSpC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+    k_lpdc_sp<Pre::RealLpSqrt, kLpdcSC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else {
     throw std::invalid_argument("single-pass LpDc scan: unsupported front end");
   }

@@ -121,7 +121,7 @@ class ScanStage {
     a.spin = spin_limit();
     if ((sp_ok_ || sp1_ok_) && mode_ == 0) {
       const size_t words = sp1_ok_ ? static_cast<size_t>(scan_sp_chunks(n)) * nch_ * 16
-                                   : static_cast<size_t>(lpdc_sp_demod_chunks(n, kSpC, dc_only_ ? 0 : kSpWarm)) * nch_ * 8;
+                                   : static_cast<size_t>(lpdc_sp_demod_chunks(n, kLpdcSC, dc_only_ ? 0 : kSpWarm)) * nch_ * 8;
       if (words * 4 > rec_buf_.size()) {
         rec_buf_.resize(words * 4);
         rec_buf_.zero(s);
