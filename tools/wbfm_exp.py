@@ -42,10 +42,14 @@ def multi(names, k, w, nch, n, maxseg=0):
     import importlib.util
     import torch
     mods = {}
-    for nm in names:
-        os.environ["ORION_SDR_LIB"] = (os.path.join(ROOT, "orion-sdr_amd", "lib", "liborion_sdr_amd.so") if nm == "base"
-                                       else os.path.join(ROOT, "orion-sdr_amd", "exp", nm, "liborion_sdr_amd.so"))
-        spec = importlib.util.spec_from_file_location(f"orion_sdr_{nm}",
+    for nm in names:  # "lib" or "lib@segments" (the segmented kernel's segment count)
+        lib = nm.split("@")[0]
+        if lib in {k.split("@")[0]: 0 for k in mods}:
+            mods[nm] = next(v for k, v in mods.items() if k.split("@")[0] == lib)
+            continue
+        os.environ["ORION_SDR_LIB"] = (os.path.join(ROOT, "orion-sdr_amd", "lib", "liborion_sdr_amd.so") if lib == "base"
+                                       else os.path.join(ROOT, "orion-sdr_amd", "exp", lib, "liborion_sdr_amd.so"))
+        spec = importlib.util.spec_from_file_location(f"orion_sdr_{lib}",
                                                       os.path.join(ROOT, "orion-sdr_amd", "orion_sdr", "__init__.py"))
         m = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(m)
@@ -55,9 +59,10 @@ def multi(names, k, w, nch, n, maxseg=0):
     x = torch.randn((nch, n) if nch > 1 else (n,), dtype=torch.complex64, device=dev, generator=g)
     out = torch.empty((nch, n // 8) if nch > 1 else (n // 8,), dtype=torch.float32, device=dev)
     blks = {nm: m.WbfmChain(f_off=[0.0] * nch if nch > 1 else 0.0) for nm, m in mods.items()}
-    if maxseg:
-        for b in blks.values():
-            b.configure("segmented", maxseg)
+    for nm, b in blks.items():
+        segs = int(nm.split("@")[1]) if "@" in nm else maxseg
+        if segs:
+            b.configure("segmented", segs)
     s = torch.cuda.current_stream(dev)
     for _ in range(w):
         for b in blks.values():
