@@ -242,7 +242,6 @@ RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t m
   // exact output: its phase, plus the mean step fitted (least squares over the renorm
   // points of the run's last half) and the mean magnitude by renorm-counter position
   // (over its last quarter).
-  t.prof.assign(1024, 1.0f);
   if (t.n == 0) {
     t.mbase = q64_of_angle(std::atan2(static_cast<long double>(s0.zi), static_cast<long double>(s0.zr)));
     return t;
@@ -276,8 +275,24 @@ RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t m
       ++np;
     }
   }
-  for (int j = 0; j < 1024; ++j)
-    if (mcnt[j]) t.prof[j] = static_cast<float>(msum[j] / static_cast<double>(mcnt[j]));
+  {  // least-squares line through the mean magnitude at each renorm position
+    double s0 = 0, s1 = 0, s2 = 0, t0 = 0, t1 = 0;
+    for (int j = 0; j < 1024; ++j) {
+      if (!mcnt[j]) continue;
+      const double m = msum[j] / static_cast<double>(mcnt[j]);
+      s0 += 1;
+      s1 += j;
+      s2 += static_cast<double>(j) * j;
+      t0 += m;
+      t1 += j * m;
+    }
+    const double den = s0 * s2 - s1 * s1;
+    if (s0 >= 2 && den > 0) {
+      const double b = (s0 * t1 - s1 * t0) / den;
+      t.mag1 = static_cast<float>(b);
+      t.mag0 = static_cast<float>((t0 - b * s1) / s0);
+    }
+  }
   long double slope = 0;
   if (np >= 8) {
     const long double den = static_cast<long double>(np) * sxx - sx * sx;
@@ -302,7 +317,7 @@ RecState rec_state_after(const RecTable& t, uint64_t k) {
   constexpr long double kTwoPi = 6.283185307179586476925286766559005768L;
   const uint64_t ph = t.mbase + (k + 1 - t.n) * t.mstep;
   const long double a = static_cast<long double>(ph) / 18446744073709551616.0L * kTwoPi;
-  const long double m = t.prof.empty() ? 1.0L : static_cast<long double>(t.prof[s.ctr & 1023u]);
+  const long double m = static_cast<long double>(t.mag0) + static_cast<long double>(t.mag1) * (s.ctr & 1023u);
   s.zr = static_cast<float>(m * std::cos(a));
   s.zi = static_cast<float>(m * std::sin(a));
   return s;

@@ -64,7 +64,8 @@ struct RecTable {
   // beyond n when there is no cycle (a model of the drift, not the reference):
   uint64_t mbase = 0;          // Q0.64 phase of output n - 1 (the last exact one)
   uint64_t mstep = 0;          // fitted mean step: phase(k) = mbase + (k + 1 - n) mstep
-  std::vector<float> prof;     // 1024 mean magnitudes by (ctr0 + k + 1) & 1023
+  float mag0 = 1.0f, mag1 = 0.0f;  // mean magnitude mag0 + mag1 ((ctr0 + k + 1) & 1023): within a
+                                   // renorm period |z| moves linearly to ~1e-8 (|w| != 1 in f32)
   uint32_t ctr0 = 0;           // renorm_ctr of the start state
 };
 // Runs the recurrence with step (wr, wi) from s0 for at most max_out outputs,

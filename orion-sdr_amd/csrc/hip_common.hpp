@@ -90,19 +90,22 @@ __device__ __forceinline__ f2 phasor_at(uint64_t ph) {
 // k + 1 steps, rotator.rs:44-62 / nco.rs:42-58):
 //   tab[k]                                            k < n_tab (the reference's own)
 //   tab[cyc_start + (k - cyc_start) mod cyc_len]      cyc_len > 0 (its cycle, forever)
-//   prof[(ctr0 + k + 1) & 1023] e^{j 2 pi ph / 2^64}, ph = mbase + (k + 1 - n_tab) mstep
-//                                                     otherwise (the drift model; prof
-//                                                     null: magnitude 1, the closed form)
+//   (mag0 + mag1 ((ctr0 + k + 1) & 1023)) e^{j 2 pi ph / 2^64}, ph = mbase + (k + 1 - n_tab) mstep
+//                                                     otherwise (the drift model; the
+//                                                     closed form: mag0 = 1, mag1 = 0)
 // mtab: e^{j 2 pi p mstep / 2^64}, p < kOscSpan (the model within a run).
 // cyc_len is 0 or >= kOscSpan (rec_table unrolls shorter cycles).
 constexpr int kOscSpan = 16384;  // longest run of consecutive outputs one cursor serves
 struct OscDev {
   const f2* tab;
-  const float* prof;
   const f2* mtab;
   uint64_t n_tab, cyc_start, cyc_len, mbase, mstep;
   uint32_t ctr0;
+  float mag0, mag1;  // the model's magnitude, linear in the renorm-counter position
 };
+__device__ __forceinline__ float osc_mag(const OscDev& o, uint32_t pos) {
+  return __builtin_fmaf(o.mag1, static_cast<float>(pos & 1023u), o.mag0);
+}
 // A cursor over outputs k .. k + len - 1 (len <= kOscSpan), all fields wave-uniform:
 // kind 0 every output from the table, 1 every output modelled, 2 mixed (the first
 // `rem` from the table); j = the table index of k, wrapped into the cycle (with
@@ -123,17 +126,18 @@ __device__ __forceinline__ OscRun osc_run(const OscDev& o, uint64_t k, int len) 
   r.S = r.kind != 0 ? phasor_at(o.mbase + (k + 1 - o.n_tab) * o.mstep) : f2{1.0f, 0.0f};
   return r;
 }
-// Table output r.k + off (kind 0, or kind 2 with off < rem).
+// Table output r.k + off (kind 0, or kind 2 with off < rem). Offsets past the run's
+// valid outputs (the padding lanes of its last tile) may reach past a table without a
+// cycle: they read its last entry instead (their values are never used).
 __device__ __forceinline__ f2 osc_tab(const OscDev& o, const OscRun& r, int off) {
   uint32_t j = r.j + static_cast<uint32_t>(off);
-  if (j >= static_cast<uint32_t>(o.n_tab)) j -= static_cast<uint32_t>(o.cyc_len);  // (only with a cycle)
+  const uint32_t nt = static_cast<uint32_t>(o.n_tab);
+  if (j >= nt) j = o.cyc_len ? j - static_cast<uint32_t>(o.cyc_len) : nt - 1u;
   return o.tab[j];
 }
 // Model output r.k + off from tm = mtab[off] (or any equal product of step phasors).
 __device__ __forceinline__ f2 osc_model(const OscDev& o, const OscRun& r, int off, f2 tm) {
-  f2 p = cmul(r.S, tm);
-  if (o.prof) p *= splat2(o.prof[(o.ctr0 + r.klo + static_cast<uint32_t>(off) + 1u) & 1023u]);
-  return p;
+  return cmul(r.S, tm) * splat2(osc_mag(o, o.ctr0 + r.klo + static_cast<uint32_t>(off) + 1u));
 }
 // Output r.k + off (off < the run's len), from the table or the model (tm: mtab[off]).
 __device__ __forceinline__ f2 osc_get_tm(const OscDev& o, const OscRun& r, int off, f2 tm) {
@@ -154,9 +158,8 @@ __device__ __forceinline__ f2 osc_at(const OscDev& o, uint64_t k) {
                                                     : d % o.cyc_len;
     return o.tab[o.cyc_start + j];
   }
-  f2 p = phasor_at(o.mbase + (k + 1 - o.n_tab) * o.mstep);
-  if (o.prof) p *= splat2(o.prof[(o.ctr0 + static_cast<uint32_t>(k) + 1u) & 1023u]);
-  return p;
+  return phasor_at(o.mbase + (k + 1 - o.n_tab) * o.mstep) *
+         splat2(osc_mag(o, o.ctr0 + static_cast<uint32_t>(k) + 1u));
 }
 
 // f32 sin and cos, correctly rounded but for rare near-ties: the argument reduced by

@@ -14,9 +14,6 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int kMaxGrid = 2048;  // memory-bound: cap and grid-stride (2048 = 8 WG per CU)
-#ifndef ORION_FIR_SPLIT
-#define ORION_FIR_SPLIT 0  // FirLowpassIq streaming on the tap-split kernel (k_fir_iq8s; A/B builds)
-#endif
 
 // ------------------------------------------------------------------ NCO --
 // Output i of a call is oscillator output k = k0 + i (hip_common.hpp OscDev): the
@@ -408,12 +405,12 @@ __device__ __forceinline__ void hist_next(const V* __restrict__ x, long long n, 
 // entries 16..23, kk = 1 entry 15, ...): LDS reads return in order, so the first FMAs
 // wait for 8 reads, not for all 16 and a scalar tap load (lgkmcnt(0)). The summation
 // order (kk ascending: the reference's) is unchanged.
-template <int KP, int KB0 = 0, int KB1 = KP / 16>
+template <int KP>
 __device__ __forceinline__ void fir8_blocks(const f2* __restrict__ L, const float* __restrict__ Gt, int t,
                                             f2 (&acc)[8]) {
   const f2* __restrict__ Lt = L + 10 * t + 10 * (KP - 16) / 8;
 #pragma unroll 1
-  for (int kb = KB0; kb < KB1; ++kb) {
+  for (int kb = 0; kb < KP / 16; ++kb) {
     const f2* __restrict__ Lb = Lt - 20 * kb;
     const f4* __restrict__ tq = reinterpret_cast<const f4*>(Gt + 16 * kb);
     float tp[16];
@@ -602,71 +599,6 @@ __global__ __launch_bounds__(NT) void k_fir_iq8(const f2* x, long long n,
   }
 }
 
-// Tap-split form (small calls: twice the waves of k_fir_iq8 for the same outputs). A
-// workgroup's 1024 outputs are computed by its two thread halves over the two halves
-// of the taps (16-tap blocks [0, KP/32) and [KP/32, KP/16), each summed in tap order
-// from zero) and added through LDS: y = (taps 0 .. KP/2-1) + (taps KP/2 .. KP-1). With
-// the upper half all padding (<= KP/2 taps) that is k_fir_iq8's sum exactly.
-template <int KP>
-__global__ __launch_bounds__(NT) void k_fir_iq8s(const f2* x, long long n, const f2* __restrict__ hist,
-                                                 int hist_len, f2* y, long long n_out, long long off,
-                                                 const Taps256 g, f2* __restrict__ hist_out) {
-  hist_next(x, n, hist, hist_out, hist_len);
-  constexpr int HN = NT / 2, TT = 8 * HN;  // 1024 outputs per tile
-  constexpr int W = TT + KP + 2, PER = (W + NT - 1) / NT;
-  constexpr int WP = W + 2 * (W / 8) + 2;
-  static_assert(KP % 32 == 0, "two halves of 16-tap blocks");
-  __shared__ __attribute__((aligned(16))) f2 L[WP];
-  __shared__ __attribute__((aligned(16))) f2 Rs[HN * 9];  // the upper half's partial sums (9 per thread: no conflicts)
-  __shared__ __attribute__((aligned(16))) float Gt[KP];
-  auto pidx = [](int p) { return p + 2 * (p >> 3); };
-  const int t = threadIdx.x, u = t & (HN - 1), hh = t / HN;
-  for (int k = t; k < KP; k += NT) Gt[k] = g.g[k];
-  for (long long J = static_cast<long long>(blockIdx.x) * TT; J < n_out;
-       J += static_cast<long long>(gridDim.x) * TT) {
-    const long long org = J + off - KP;  // staged sample p <-> element org + p
-    if (org >= 0 && org + W <= n) {
-      f2 v[PER];
-#pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const int p = t + k * NT;
-        v[k] = p < W ? x[org + p] : f2{0.0f, 0.0f};
-      }
-#pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const int p = t + k * NT;
-        if (p < W) L[pidx(p)] = v[k];
-      }
-    } else {
-      for (int p = t; p < W; p += NT) L[pidx(p)] = load_hist(x, n, hist, hist_len, org + p);
-    }
-    __syncthreads();
-    f2 acc[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) acc[r] = f2{0.0f, 0.0f};
-    if (hh == 0) fir8_blocks<KP, 0, KP / 32>(L, Gt, u, acc);
-    else fir8_blocks<KP, KP / 32, KP / 16>(L, Gt, u, acc);
-    if (hh == 1)
-#pragma unroll
-      for (int r = 0; r < 8; ++r) Rs[9 * u + r] = acc[r];
-    __syncthreads();  // (also: every read of L is done before the next tile's staging)
-    if (hh == 0) {
-#pragma unroll
-      for (int r = 0; r < 8; ++r) acc[r] += Rs[9 * u + r];
-      const long long j0 = J + 8 * u;
-      if (j0 + 8 <= n_out && (reinterpret_cast<uintptr_t>(y + j0) & 15) == 0) {
-        f4* yo = reinterpret_cast<f4*>(y + j0);
-#pragma unroll
-        for (int r = 0; r < 8; r += 2) yo[r / 2] = f4{acc[r].x, acc[r].y, acc[r + 1].x, acc[r + 1].y};
-      } else {
-#pragma unroll
-        for (int r = 0; r < 8; ++r)
-          if (j0 + r < n_out) y[j0 + r] = acc[r];
-      }
-    }
-  }
-}
-
 __global__ __launch_bounds__(NT) void k_fir_iq_generic(const f2* __restrict__ x, long long n,
                                                        const f2* __restrict__ hist, int hist_len,
                                                        f2* __restrict__ y, long long n_out,
@@ -826,12 +758,7 @@ void launch_fir_real(const float* x, long long n, const float* hist, int hist_le
 void launch_fir_iq(const f2* x, long long n, const f2* hist, int hist_len, f2* y, long long n_out,
                    long long off, int K, const Taps256& g, const float* g_dev, hipStream_t s, f2* hist_out) {
   if (n_out <= 0) return;
-  if (ORION_FIR_SPLIT && off == 0 && K <= 256 && hist_len >= (K <= 64 ? 64 : K <= 128 ? 128 : 256)) {
-    const int gs = grid_for(n_out, 4 * NT);
-    if (K <= 64) k_fir_iq8s<64><<<gs, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, hist_out);
-    else if (K <= 128) k_fir_iq8s<128><<<gs, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, hist_out);
-    else k_fir_iq8s<256><<<gs, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, hist_out);
-  } else if (K <= 256 && hist_len >= (K <= 64 ? 64 : K <= 128 ? 128 : 256)) {
+  if (K <= 256 && hist_len >= (K <= 64 ? 64 : K <= 128 ? 128 : 256)) {
     const int g8 = grid_for(n_out, 8 * NT);
     if (K <= 64) k_fir_iq8<64><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
     else if (K <= 128) k_fir_iq8<128><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);

@@ -75,7 +75,6 @@ void RefOsc::build(const RecState& st, uint64_t closed_anchor_q64) {
     tab_ = rec_table(osc_.w_re, osc_.w_im, st, budget_, kOscSpan, osc_.step_q64);
   }
   if (tab_.n) dtab_.upload(tab_.z.data(), tab_.z.size() * sizeof(float));
-  if (!tab_.prof.empty()) dprof_.upload(tab_.prof.data(), tab_.prof.size() * sizeof(float));
   const double th = static_cast<double>(static_cast<long double>(tab_.mstep) / 18446744073709551616.0L * kTwoPiL);
   const auto mt = phasor_table(th, kOscSpan);
   dmtab_.upload(mt.data(), mt.size() * sizeof(float));
@@ -84,7 +83,6 @@ void RefOsc::build(const RecState& st, uint64_t closed_anchor_q64) {
 OscDev RefOsc::dev() const {
   OscDev d{};
   d.tab = tab_.n ? dtab_.as<f2>() : nullptr;
-  d.prof = tab_.prof.empty() ? nullptr : dprof_.as<float>();
   d.mtab = dmtab_.as<f2>();
   d.n_tab = tab_.n;
   d.cyc_start = tab_.cyc_start;
@@ -92,6 +90,8 @@ OscDev RefOsc::dev() const {
   d.mbase = tab_.mbase;
   d.mstep = tab_.mstep;
   d.ctr0 = tab_.ctr0;
+  d.mag0 = tab_.mag0;
+  d.mag1 = tab_.mag1;
   return d;
 }
 

@@ -50,7 +50,7 @@ class RefOsc {
   RecTable tab_;
   RecState org_;  // start state of tab_
   uint64_t k_ = 0;
-  DevBuf dtab_, dprof_, dmtab_;
+  DevBuf dtab_, dmtab_;
 };
 
 }  // namespace orion

@@ -943,7 +943,8 @@ def test_ssb_phasing_mod(gpu_lib, oracle, usb, rf, fs):
     if rf == 0.0:
         d = gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0).process(got)
         fd = lambda v: oracle.ssb_demod(v, FS, 1500.0, 2800.0)  # noqa: E731
-        report("ssb mod -> demod round trip vs oracle nrmse", nrmse(d, fd(ref)), floor_tol(1e-6, fd, ref))
+        # two stages' roundings (the modulator's LP4, then the demodulator's LpDc): 2e-5
+        report("ssb mod -> demod round trip vs oracle nrmse", nrmse(d, fd(ref)), floor_tol(2e-5, fd, ref))
 
 
 @pytest.mark.parametrize("rf,kp,gain", [(0.0, 0.9, 1.0), (12e3, 2.5, 0.7), (1.5e6, 1.2, 1.0)])
