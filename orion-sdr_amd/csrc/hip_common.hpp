@@ -126,27 +126,36 @@ __device__ __forceinline__ OscRun osc_run(const OscDev& o, uint64_t k, int len) 
   r.S = r.kind != 0 ? phasor_at(o.mbase + (k + 1 - o.n_tab) * o.mstep) : f2{1.0f, 0.0f};
   return r;
 }
-// Table output r.k + off (kind 0, or kind 2 with off < rem). Offsets past the run's
-// valid outputs (the padding lanes of its last tile) may reach past a table without a
-// cycle: they read its last entry instead (their values are never used).
+// Table output r.k + off (kind 0, or kind 2 with off < rem). The device table holds
+// kOscSpan entries past n_tab (the cycle's continuation, or the last entry repeated:
+// osc.cpp), so a run reads tab[j + off] without a wrap; the padding lanes of a run's
+// last tile read valid memory whose values are never used.
 __device__ __forceinline__ f2 osc_tab(const OscDev& o, const OscRun& r, int off) {
-  uint32_t j = r.j + static_cast<uint32_t>(off);
-  const uint32_t nt = static_cast<uint32_t>(o.n_tab);
-  if (j >= nt) j = o.cyc_len ? j - static_cast<uint32_t>(o.cyc_len) : nt - 1u;
-  return o.tab[j];
+  return o.tab[r.j + static_cast<uint32_t>(off)];
 }
 // Model output r.k + off from tm = mtab[off] (or any equal product of step phasors).
 __device__ __forceinline__ f2 osc_model(const OscDev& o, const OscRun& r, int off, f2 tm) {
   return cmul(r.S, tm) * splat2(osc_mag(o, o.ctr0 + r.klo + static_cast<uint32_t>(off) + 1u));
 }
+__device__ __forceinline__ bool osc_in_tab(const OscRun& r, int off) {
+  return r.kind == 0 || (r.kind == 2 && static_cast<uint32_t>(off) < r.rem);
+}
+// Output r.k + off in two steps, so that a kernel can issue every load first: osc_ld
+// reads the table entry or mtab[off], osc_fin turns a model read into the output.
+__device__ __forceinline__ f2 osc_ld(const OscDev& o, const OscRun& r, int off) {
+  const f2* b = osc_in_tab(r, off) ? o.tab + r.j : o.mtab;
+  return b[off];
+}
+__device__ __forceinline__ f2 osc_fin(const OscDev& o, const OscRun& r, int off, f2 v) {
+  return osc_in_tab(r, off) ? v : osc_model(o, r, off, v);
+}
 // Output r.k + off (off < the run's len), from the table or the model (tm: mtab[off]).
 __device__ __forceinline__ f2 osc_get_tm(const OscDev& o, const OscRun& r, int off, f2 tm) {
-  if (r.kind == 0 || (r.kind == 2 && static_cast<uint32_t>(off) < r.rem)) return osc_tab(o, r, off);
+  if (osc_in_tab(r, off)) return osc_tab(o, r, off);
   return osc_model(o, r, off, tm);
 }
 __device__ __forceinline__ f2 osc_get(const OscDev& o, const OscRun& r, int off) {
-  if (r.kind == 0 || (r.kind == 2 && static_cast<uint32_t>(off) < r.rem)) return osc_tab(o, r, off);
-  return osc_model(o, r, off, o.mtab[off]);
+  return osc_fin(o, r, off, osc_ld(o, r, off));
 }
 
 // Output k alone (no cursor: kernels that visit samples in no run order).

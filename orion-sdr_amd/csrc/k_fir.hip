@@ -5,6 +5,7 @@
 //   FirLowpassIq::process / filter_aligned  dsp/fir.rs:229-297 (complex, real taps)
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "kernels.hpp"
 #include "poly.hpp"
@@ -26,16 +27,82 @@ enum : int { kRotate = 0, kUsb = 1, kNcoMix = 2, kNcoGen = 3 };
 #ifndef ORION_ROT_MINW
 #define ORION_ROT_MINW 6  // waves per SIMD k_rotator is compiled for (8: <= 64 VGPRs, 6 B of spills)
 #endif
+#ifndef ORION_ROT_HP
+#define ORION_ROT_HP 2  // pairs per thread whose loads a full tile issues together
+#endif
 template <bool A16, int MODE>
 __global__ __launch_bounds__(NT, ORION_ROT_MINW) void k_rotator(const f2* __restrict__ x, void* __restrict__ yv, long long n,
                                                 uint64_t k0, const OscDev o) {
   constexpr int PER = kRotTile / (2 * NT);  // pairs per thread per tile (8)
+  constexpr int HP = ORION_ROT_HP;
   const int t = threadIdx.x;
+  // output pair P, P + 1 (only P when P + 1 == n) from inputs v0, v1 and phasors p0, p1
+  auto emit = [&](long long P, bool full, f2 v0, f2 v1, f2 p0, f2 p1) {
+    if constexpr (MODE == kUsb) {
+      float* y = static_cast<float*>(yv);
+      if (A16 && full) {
+        *reinterpret_cast<float2*>(y + P) = float2{__builtin_fmaf(v0.x, p0.x, v0.y * p0.y),
+                                                   __builtin_fmaf(v1.x, p1.x, v1.y * p1.y)};
+      } else {
+        y[P] = __builtin_fmaf(v0.x, p0.x, v0.y * p0.y);
+        if (full) y[P + 1] = __builtin_fmaf(v1.x, p1.x, v1.y * p1.y);
+      }
+    } else {
+      f2* y = static_cast<f2*>(yv);
+      f2 o0, o1;
+      if constexpr (MODE == kRotate) {
+        o0 = cmul_rot(v0, p0);
+        o1 = cmul_rot(v1, p1);
+      } else if constexpr (MODE == kNcoMix) {  // (x.re c - x.im s, x.re s + x.im c), no FMA
+        o0 = f2{v0.x * p0.x - v0.y * p0.y, v0.x * p0.y + v0.y * p0.x};
+        o1 = f2{v1.x * p1.x - v1.y * p1.y, v1.x * p1.y + v1.y * p1.x};
+      } else {
+        o0 = p0;
+        o1 = p1;
+      }
+      if (A16 && full) {
+        *reinterpret_cast<f4*>(y + P) = f4{o0.x, o0.y, o1.x, o1.y};
+      } else {
+        y[P] = o0;
+        if (full) y[P + 1] = o1;
+      }
+    }
+  };
   for (long long tile = static_cast<long long>(blockIdx.x) * kRotTile; tile < n;
        tile += static_cast<long long>(gridDim.x) * kRotTile) {
     const OscRun r = osc_run(o, k0 + static_cast<uint64_t>(tile), kRotTile);  // tile-uniform
-    // one tile-uniform branch per form of the phasor: table, model, mixed
-    auto body = [&](auto get) {
+    // ld2: the raw reads of a pair's phasors (table entries or mtab), fin2: the phasors
+    auto body = [&](auto ld2, auto fin2, auto batched) {
+      if (decltype(batched)::value && tile + kRotTile <= n) {  // a full tile, in groups of HP pairs: a group's loads issued together
+#pragma unroll
+        for (int h = 0; h < PER; h += HP) {
+        f2 v0[HP], v1[HP], q0[HP], q1[HP];
+#pragma unroll
+        for (int i = 0; i < HP; ++i) {
+          const int off = 2 * t + 2 * NT * (h + i);
+          const long long P = tile + off;
+          v0[i] = v1[i] = f2{0.0f, 0.0f};
+          if constexpr (MODE != kNcoGen) {
+            if (A16) {
+              const f4 v = *reinterpret_cast<const f4*>(x + P);
+              v0[i] = f2{v.x, v.y};
+              v1[i] = f2{v.z, v.w};
+            } else {
+              v0[i] = x[P];
+              v1[i] = x[P + 1];
+            }
+          }
+          ld2(off, q0[i], q1[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < HP; ++i) {
+          const int off = 2 * t + 2 * NT * (h + i);
+          fin2(off, q0[i], q1[i]);
+          emit(tile + off, true, v0[i], v1[i], q0[i], q1[i]);
+        }
+        }
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int off = 2 * t + 2 * NT * i;
@@ -44,46 +111,45 @@ __global__ __launch_bounds__(NT, ORION_ROT_MINW) void k_rotator(const f2* __rest
         f2 v0 = f2{0.0f, 0.0f}, v1 = f2{0.0f, 0.0f};
         const bool full = P + 1 < n;
         if constexpr (MODE != kNcoGen) {
-          if (A16 && full) {
-            const f4 v = *reinterpret_cast<const f4*>(x + P);
-            v0 = f2{v.x, v.y};
-            v1 = f2{v.z, v.w};
-          } else {
-            v0 = x[P];
-            if (full) v1 = x[P + 1];
-          }
+          v0 = x[P];
+          if (full) v1 = x[P + 1];
         }
-        const f2 p0 = get(off);
-        const f2 p1 = get(off + 1);
-        if constexpr (MODE == kUsb) {
-          float* y = static_cast<float*>(yv);
-          y[P] = __builtin_fmaf(v0.x, p0.x, v0.y * p0.y);
-          if (full) y[P + 1] = __builtin_fmaf(v1.x, p1.x, v1.y * p1.y);
-        } else {
-          f2* y = static_cast<f2*>(yv);
-          f2 o0, o1;
-          if constexpr (MODE == kRotate) {
-            o0 = cmul_rot(v0, p0);
-            o1 = cmul_rot(v1, p1);
-          } else if constexpr (MODE == kNcoMix) {  // (x.re c - x.im s, x.re s + x.im c), no FMA
-            o0 = f2{v0.x * p0.x - v0.y * p0.y, v0.x * p0.y + v0.y * p0.x};
-            o1 = f2{v1.x * p1.x - v1.y * p1.y, v1.x * p1.y + v1.y * p1.x};
-          } else {
-            o0 = p0;
-            o1 = p1;
-          }
-          if (A16 && full) {
-            *reinterpret_cast<f4*>(y + P) = f4{o0.x, o0.y, o1.x, o1.y};
-          } else {
-            y[P] = o0;
-            if (full) y[P + 1] = o1;
-          }
-        }
+        f2 p0, p1;
+        ld2(off, p0, p1);
+        fin2(off, p0, p1);
+        emit(P, full, v0, v1, p0, p1);
       }
     };
-    if (r.kind == 0) body([&](int off) { return osc_tab(o, r, off); });
-    else if (r.kind == 1) body([&](int off) { return osc_model(o, r, off, o.mtab[off]); });
-    else body([&](int off) { return osc_get(o, r, off); });
+    auto none = [](int, f2&, f2&) {};
+    if (r.kind == 0 && (r.j & 1u) == 0) {  // a 16-B load per pair (the table is padded: no wrap)
+      body([&](int off, f2& p0, f2& p1) {
+        const f4 v = *reinterpret_cast<const f4*>(o.tab + r.j + off);
+        p0 = f2{v.x, v.y};
+        p1 = f2{v.z, v.w};
+      }, none, std::true_type{});
+    } else if (r.kind == 0) {
+      body([&](int off, f2& p0, f2& p1) {
+        p0 = osc_tab(o, r, off);
+        p1 = osc_tab(o, r, off + 1);
+      }, none, std::true_type{});
+    } else if (r.kind == 1) {
+      body([&](int off, f2& p0, f2& p1) {
+        const f4 m = *reinterpret_cast<const f4*>(o.mtab + off);
+        p0 = f2{m.x, m.y};
+        p1 = f2{m.z, m.w};
+      }, [&](int off, f2& p0, f2& p1) {
+        p0 = osc_model(o, r, off, p0);
+        p1 = osc_model(o, r, off + 1, p1);
+      }, std::true_type{});
+    } else {
+      body([&](int off, f2& p0, f2& p1) {
+        p0 = osc_ld(o, r, off);
+        p1 = osc_ld(o, r, off + 1);
+      }, [&](int off, f2& p0, f2& p1) {
+        p0 = osc_fin(o, r, off, p0);
+        p1 = osc_fin(o, r, off + 1, p1);
+      }, std::false_type{});  // one tile per call at most
+    }
   }
 }
 
@@ -524,8 +590,10 @@ __global__ __launch_bounds__(NT) void k_fir_real_generic(const float* __restrict
 }
 
 // ------------------------------------------------------ complex FIR -------
-// HT halves of 512 outputs per tile: one load round trip (behind one barrier)
-// feeds HT x 512 outputs, so a workgroup keeps HT times the bytes in flight.
+// y[i] = sum_{k<KP} g[k] x[i-k] on I/Q pairs: a tile of 8*NT outputs, 8 consecutive
+// per lane; the tile plus its KP-sample halo is staged once in LDS (padded 2 per 8
+// against bank conflicts) behind one barrier. INPLACE (y == x): the halo comes from
+// boundary copies E taken before the launch, so no tile reads a neighbour's output.
 template <int KP, bool INPLACE = false>
 __global__ __launch_bounds__(NT) void k_fir_iq8(const f2* x, long long n,
                                                 const f2* __restrict__ hist, int hist_len,
@@ -664,7 +732,7 @@ void launch_osc(int mode, const f2* x, void* y, long long n, uint64_t k0, const 
   if (o.cyc_len != 0 && o.cyc_len < static_cast<uint64_t>(kOscSpan)) throw HipError("osc: cycle shorter than a run");
   const int grid = grid_for(n, kRotTile);
   const bool a16 = (mode == kNcoGen || reinterpret_cast<uintptr_t>(x) % 16 == 0) &&
-                   (mode == kUsb || reinterpret_cast<uintptr_t>(y) % 16 == 0);
+                   reinterpret_cast<uintptr_t>(y) % (mode == kUsb ? 8 : 16) == 0;
 #define ORION_OSC(MD)                                                                          \
   if (a16) k_rotator<true, MD><<<grid, NT, 0, s>>>(x, y, n, k0, o);                          \
   else k_rotator<false, MD><<<grid, NT, 0, s>>>(x, y, n, k0, o);

@@ -29,17 +29,39 @@ int grid_for(long long n) {
   return static_cast<int>(std::min<long long>(kMaxGrid, std::max(1LL, (n + kModTile - 1) / kModTile)));
 }
 
-// Sample i of a call with its oscillator phasor (output k0 + i): f(i, r).
-template <class F>
-__device__ __forceinline__ void mod_tiles(long long n, uint64_t k0, const OscDev& o, F f) {
+// Sample i of a call with its oscillator phasor (output k0 + i): f(i, ld(i), r). A
+// full tile issues the loads of kModGrp samples (input and phasor reads) before it
+// uses any (a guarded load per sample waits for itself before the next is issued).
+constexpr int kModGrp = 4;
+template <class L, class F>
+__device__ __forceinline__ void mod_tiles(long long n, uint64_t k0, const OscDev& o, L ld, F f) {
   for (long long tile = static_cast<long long>(blockIdx.x) * kModTile; tile < n;
        tile += static_cast<long long>(gridDim.x) * kModTile) {
     const OscRun r = osc_run(o, k0 + static_cast<uint64_t>(tile), kModTile);
+    if (tile + kModTile <= n && r.kind != 2) {
+#pragma unroll
+      for (int g = 0; g < kModPer; g += kModGrp) {
+        decltype(ld(0LL)) v[kModGrp];
+        f2 p[kModGrp];
+#pragma unroll
+        for (int m = 0; m < kModGrp; ++m) {
+          const int off = static_cast<int>(threadIdx.x) + NT * (g + m);
+          v[m] = ld(tile + off);
+          p[m] = osc_ld(o, r, off);
+        }
+#pragma unroll
+        for (int m = 0; m < kModGrp; ++m) {
+          const int off = static_cast<int>(threadIdx.x) + NT * (g + m);
+          f(tile + off, v[m], osc_fin(o, r, off, p[m]));
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int m = 0; m < kModPer; ++m) {
       const int off = static_cast<int>(threadIdx.x) + NT * m;
       const long long i = tile + off;
-      if (i < n) f(i, osc_get(o, r, off));
+      if (i < n) f(i, ld(i), osc_get(o, r, off));
     }
   }
 }
@@ -47,8 +69,8 @@ __device__ __forceinline__ void mod_tiles(long long n, uint64_t k0, const OscDev
 // am.rs:87-89 (clamp: :56): m = (cl + mi x) [clamped to +-1] * g; out = m * r (Rotator rf).
 __global__ __launch_bounds__(NT) void k_am_mod(const float* __restrict__ x, f2* __restrict__ y, long long n,
                                                uint64_t k0, const OscDev o, float cl, float mi, float g, int clamp) {
-  mod_tiles(n, k0, o, [&](long long i, f2 r) {
-    float v = cl + mi * x[i];
+  mod_tiles(n, k0, o, [&](long long i) { return x[i]; }, [&](long long i, float xi, f2 r) {
+    float v = cl + mi * xi;
     if (clamp) v = fminf(fmaxf(v, -1.0f), 1.0f);
     const float m = v * g;
     y[i] = f2{m * r.x, m * r.y};
@@ -60,8 +82,8 @@ __global__ __launch_bounds__(NT) void k_am_mod(const float* __restrict__ x, f2* 
 // nco.rs:63-66).
 __global__ __launch_bounds__(NT) void k_pm_mod(const float* __restrict__ x, f2* __restrict__ y, long long n,
                                                uint64_t k0, const OscDev o, float kp, float g) {
-  mod_tiles(n, k0, o, [&](long long i, f2 r) {
-    const float phi = kp * x[i];
+  mod_tiles(n, k0, o, [&](long long i) { return x[i]; }, [&](long long i, float xi, f2 r) {
+    const float phi = kp * xi;
     float sn, cs;
     sincos_cr(phi, &sn, &cs);  // pm.rs:44 (phi.cos(), phi.sin())
     const float br = cs * g, bi = sn * g;
@@ -72,8 +94,7 @@ __global__ __launch_bounds__(NT) void k_pm_mod(const float* __restrict__ x, f2* 
 // ssb.rs:52-54: the two LpCascade inputs x p.re, x p.im (p = audio NCO), planar.
 __global__ __launch_bounds__(NT) void k_ssb_mod_front(const float* __restrict__ x, float* __restrict__ u,
                                                       long long n, uint64_t k0, const OscDev o) {
-  mod_tiles(n, k0, o, [&](long long i, f2 p) {
-    const float xi = x[i];
+  mod_tiles(n, k0, o, [&](long long i) { return x[i]; }, [&](long long i, float xi, f2 p) {
     u[i] = xi * p.x;
     u[n + i] = xi * p.y;
   });
@@ -82,8 +103,8 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_front(const float* __restrict__ 
 // ssb.rs:55-60: z = (I, side Q); out = z * r (rf NCO), FMA form of rotate_block.
 __global__ __launch_bounds__(NT) void k_ssb_mod_back(const float* __restrict__ v, f2* __restrict__ y, long long n,
                                                      uint64_t k0, const OscDev o, float side) {
-  mod_tiles(n, k0, o, [&](long long i, f2 r) {
-    const f2 z = f2{v[i], side * v[n + i]};
+  mod_tiles(n, k0, o, [&](long long i) { return f2{v[i], v[n + i]}; }, [&](long long i, f2 vi, f2 r) {
+    const f2 z = f2{vi.x, side * vi.y};
     y[i] = cmul_rot(z, r);
   });
 }
@@ -104,6 +125,19 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_back(const float* __restrict__ v
 //     16 pairs; base = z gain (fm.rs:66); mix_with_nco's non-FMA product with the
 //     RF Nco's phasor (nco.rs:62-66; the oscillator cursor of the chunk).
 // Against an f64 phase and a per-sample sincosf of it this is ~3x less VALU per sample.
+#ifndef ORION_FM_ABL
+#define ORION_FM_ABL 0  // experiment builds only (wrong output): 1 no look-back, 2 no RF phasor reads
+#endif
+#ifndef ORION_FM_LB
+#define ORION_FM_LB 1  // look-back records per lane and step (A/B at 2^26: 1 0.406 ms, 2 0.476, 4 0.581,
+                       // 8 0.729; no look-back at all 0.251: the wait for predecessors dominates)
+#endif
+#ifndef ORION_FM_G
+#define ORION_FM_G 8  // RF phasor reads per thread issued together
+#endif
+#ifndef ORION_FM_MINW
+#define ORION_FM_MINW 1  // waves per SIMD k_fm_mod_sp is compiled for (A/B: 5 = 96 VGPRs)
+#endif
 constexpr double kTurnsPerRad = 2.9358905032820014e18;  // 2^64 / (2 pi)
 
 struct FmPairs {
@@ -130,38 +164,44 @@ __device__ __forceinline__ uint64_t fm_pairs(float kf, const float* __restrict__
 }
 
 // Outputs of the chunk: thread t's samples i0 .. i0 + 15 (i0 = base + 16 t) from its
-// entering phase ph, stored coalesced through LDS in two passes of 8 per thread (each
-// thread owning 16 consecutive samples would store 64 lanes x 8 B at a 128-B stride per
-// instruction). ys: kFmYs f2 slots (pass h: thread t's 8 at 8 t + pad, one pad per 16:
-// conflict-free b64 stores), aliasing the input staging: every thread is past its
-// reads of it (the caller's barrier). Pass h covers the chunk's samples 16 t' + 8 h + j.
-constexpr int kFmYs = (kFmCH + kFmCH / 16) / 2;  // f2 slots (= the input staging's floats / 2)
+// entering phase ph. Each thread writes its 16 base values z gain to LDS (ys, one pad
+// slot per 16), then the chunk is mixed with the RF phasors and stored in sample order
+// (e = t + 256 m): the stores and the RF table reads are coalesced (a thread's own 16
+// consecutive samples would touch 64 cache lines per wave instruction). ys aliases
+// the input staging: every thread is past its reads of it (the caller's barrier).
+constexpr int kFmYs = kFmCH + kFmCH / 16;  // f2 slots
 __device__ __forceinline__ void fm_out(const FmPairs& p, uint64_t ph, float gain, const OscDev& o, uint64_t k0,
                                        f2* ys, f2* __restrict__ y, long long base, long long n) {
   const OscRun R = osc_run(o, k0 + static_cast<uint64_t>(base), kFmCH);  // RF Nco outputs of the chunk
-  f2 z = phasor_at(ph);
   const int t = threadIdx.x;
+  f2 z = phasor_at(ph);
+#pragma unroll
+  for (int k = 0; k < kFmC; ++k) {
+    // fm.rs:53-54: zr = z.re.mul_add(dc, -z.im*ds); zi = z.im.mul_add(dc, z.re*ds)
+    z = f2{__builtin_fmaf(z.x, p.c[k], -(z.y * p.s[k])), __builtin_fmaf(z.y, p.c[k], z.x * p.s[k])};
+    const int e = kFmC * t + k;
+    ys[e + (e >> 4)] = f2{z.x * gain, z.y * gain};  // fm.rs:66 base = z * gain
+  }
+  // the RF phasor reads in groups of G (the first group in flight across the barrier)
+  constexpr int G = ORION_FM_G;
   const bool full = base + kFmCH <= n;
+  f2 rp[G];
+  auto rd = [&](int g) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+    for (int m = 0; m < G; ++m) rp[m] = (ORION_FM_ABL & 2) ? f2{1.0f, 0.0f} : osc_ld(o, R, t + NT * (g + m));
+  };
+  rd(0);
+  __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 8 * h + j;
-      // fm.rs:53-54: zr = z.re.mul_add(dc, -z.im*ds); zi = z.im.mul_add(dc, z.re*ds)
-      z = f2{__builtin_fmaf(z.x, p.c[k], -(z.y * p.s[k])), __builtin_fmaf(z.y, p.c[k], z.x * p.s[k])};
-      const f2 bz = f2{z.x * gain, z.y * gain};  // fm.rs:66 base = z * gain
-      const f2 r = osc_get(o, R, kFmC * t + k);
-      const int e = 8 * t + j;
-      ys[e + (e >> 4)] = f2{bz.x * r.x - bz.y * r.y, bz.x * r.y + bz.y * r.x};  // nco.rs:65 (no FMA)
+  for (int g = 0; g < kFmC; g += G) {
+    if (g) rd(g);
+#pragma unroll
+    for (int m = 0; m < G; ++m) {
+      const int e = t + NT * (g + m);
+      const f2 bz = ys[e + (e >> 4)];
+      const f2 r = (ORION_FM_ABL & 2) ? rp[m] : osc_fin(o, R, e, rp[m]);
+      if (full || base + e < n) y[base + e] = f2{bz.x * r.x - bz.y * r.y, bz.x * r.y + bz.y * r.x};  // nco.rs:65
     }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const int e = t + NT * m;
-      const long long i = base + 16 * (e >> 3) + 8 * h + (e & 7);
-      if (full || i < n) y[i] = ys[e + (e >> 4)];
-    }
-    __syncthreads();
   }
 }
 
@@ -284,7 +324,7 @@ __device__ __forceinline__ uint64_t fm_ld64(const uint32_t* p) {
   return (static_cast<uint64_t>(fm_ld(p + 1)) << 32) | fm_ld(p);
 }
 
-__global__ __launch_bounds__(NT) void k_fm_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
+__global__ __launch_bounds__(NT, ORION_FM_MINW) void k_fm_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
                                                   float kf, float gain, uint32_t* __restrict__ rec, uint32_t epoch,
                                                   const uint64_t* __restrict__ carry_in, uint64_t* __restrict__ carry_out,
                                                   uint64_t k0, const OscDev o, int* __restrict__ err, uint32_t spin) {
@@ -312,26 +352,49 @@ __global__ __launch_bounds__(NT) void k_fm_mod_sp(const float* __restrict__ x, f
       if (lane == 0) fm_st(my + 6, epoch);
     }
     uint64_t excl = 0;
-    for (int b = c - 1;; b -= 64) {
-      const int k = b - lane;
-      uint64_t v = 0;
-      bool closes = true;
-      if (k >= 0) {
+    // lane l reads the records of chunks b - L l - j, j < L: 64 L predecessors per step,
+    // their flag loads all issued before any is tested
+    constexpr int L = ORION_FM_LB;
+    for (int b = c - 1; !(ORION_FM_ABL & 1); b -= 64 * L) {
+      uint32_t f7[L];
+      bool seen[L];
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const int k = b - L * lane - j;
         const uint32_t* pr = rec + static_cast<long long>(k) * 8;
-        bool seen = false;  // bounded wait (spin 0: time out at once, test-only)
-        for (uint32_t it = 0; it < spin && !seen; ++it) {
-          seen = fm_ld(pr + 6) == epoch || fm_ld(pr + 7) == epoch;
-          if (!seen) __builtin_amdgcn_s_sleep(2);
-        }
-        if (!seen) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        closes = fm_ld(pr + 7) == epoch;
-        v = closes ? fm_ld64(pr + 2) : fm_ld64(pr);
-      } else {
-        v = k == -1 ? carry_in[0] : 0;  // the carried phase before chunk 0
+        f7[j] = k >= 0 ? fm_ld(pr + 7) : epoch;
+        seen[j] = f7[j] == epoch || (k >= 0 && fm_ld(pr + 6) == epoch);
       }
-      const unsigned long long bal = __ballot(closes);
-      const int first = bal ? __builtin_ctzll(bal) : 64;
-      uint64_t term = lane <= first ? v : 0;
+      uint64_t all = 0, upto = 0;  // the lane's L terms; its terms up to its nearest closing one
+      int mine = L;                // the lane's nearest closing record (L: none)
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const int k = b - L * lane - j;
+        uint64_t v;
+        bool closes = true;
+        if (k >= 0) {
+          const uint32_t* pr = rec + static_cast<long long>(k) * 8;
+          // bounded wait (spin 0: time out at once, test-only)
+          for (uint32_t it = 0; it < spin && !seen[j]; ++it) {
+            __builtin_amdgcn_s_sleep(2);
+            f7[j] = fm_ld(pr + 7);
+            seen[j] = f7[j] == epoch || fm_ld(pr + 6) == epoch;
+          }
+          if (!seen[j]) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          closes = f7[j] == epoch;
+          v = closes ? fm_ld64(pr + 2) : fm_ld64(pr);
+        } else {
+          v = k == -1 ? carry_in[0] : 0;  // the carried phase before chunk 0
+        }
+        all += v;
+        if (mine == L) {
+          upto += v;
+          if (closes) mine = j;
+        }
+      }
+      const unsigned long long bal = __ballot(mine < L);
+      const int first = bal ? __builtin_ctzll(bal) : 64;  // the lane holding the nearest closing record
+      uint64_t term = lane < first ? all : (lane == first ? upto : 0);
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) {
         const uint32_t lo = __shfl_xor(static_cast<uint32_t>(term), off, 64);

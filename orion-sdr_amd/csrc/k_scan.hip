@@ -1099,13 +1099,17 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
   const OscRun Rr = osc_run(rf, k0 + static_cast<uint64_t>(base), cnt);
   {  // stage: x p.re, x p.im (ssb.rs:53-54), coalesced loads first (unconditional, clamped)
     float v[C];
+    f2 pa[C];  // the audio phasor reads (unconditional: the table is padded past a run)
 #pragma unroll
-    for (int k = 0; k < C; ++k) v[k] = x[min(base + t + k * NT, n - 1)];
+    for (int k = 0; k < C; ++k) {
+      v[k] = x[min(base + t + k * NT, n - 1)];
+      pa[k] = osc_ld(aud, Ra, t + k * NT);
+    }
 #pragma unroll
     for (int k = 0; k < C; ++k) {
       const int e = t + k * NT;
       const float xv = e < cnt ? v[k] : 0.0f;
-      const f2 p = e < cnt ? osc_get(aud, Ra, e) : f2{1.0f, 0.0f};
+      const f2 p = e < cnt ? osc_fin(aud, Ra, e, pa[k]) : f2{1.0f, 0.0f};
       sb[0][pos(e)] = xv * p.x;
       sb[1][pos(e)] = xv * p.y;
     }
@@ -1207,10 +1211,13 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
 #pragma unroll
   for (int i = 0; i < C; ++i) zs[17 * t + i] = f2{xs[0][i], side * xs[1][i]};
   __syncthreads();
+  f2 pr[C];  // the RF phasor reads, all issued before the first store
+#pragma unroll
+  for (int k = 0; k < C; ++k) pr[k] = osc_ld(rf, Rr, t + k * NT);
 #pragma unroll
   for (int k = 0; k < C; ++k) {  // ssb.rs:55-60
     const int e = t + k * NT;
-    if (e >= warm && e < cnt) y[base + e] = cmul_rot(zs[e + (e >> 4)], osc_get(rf, Rr, e));
+    if (e >= warm && e < cnt) y[base + e] = cmul_rot(zs[e + (e >> 4)], osc_fin(rf, Rr, e, pr[k]));
   }
 }
 

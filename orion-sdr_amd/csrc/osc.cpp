@@ -3,6 +3,7 @@
 
 #include <cmath>
 #include <stdexcept>
+#include <vector>
 
 namespace orion {
 
@@ -74,7 +75,18 @@ void RefOsc::build(const RecState& st, uint64_t closed_anchor_q64) {
   } else {
     tab_ = rec_table(osc_.w_re, osc_.w_im, st, budget_, kOscSpan, osc_.step_q64);
   }
-  if (tab_.n) dtab_.upload(tab_.z.data(), tab_.z.size() * sizeof(float));
+  if (tab_.n) {
+    // kOscSpan entries past the table (OscDev: a run reads tab[j + off] unwrapped): the
+    // cycle's continuation, or the last entry repeated (never a used value).
+    std::vector<float> z(tab_.z);
+    z.resize(2 * (tab_.n + kOscSpan));
+    for (uint64_t i = 0; i < static_cast<uint64_t>(kOscSpan); ++i) {
+      const uint64_t src = tab_.cyc_len ? tab_.cyc_start + i % tab_.cyc_len : tab_.n - 1;
+      z[2 * (tab_.n + i)] = tab_.z[2 * src];
+      z[2 * (tab_.n + i) + 1] = tab_.z[2 * src + 1];
+    }
+    dtab_.upload(z.data(), z.size() * sizeof(float));
+  }
   const double th = static_cast<double>(static_cast<long double>(tab_.mstep) / 18446744073709551616.0L * kTwoPiL);
   const auto mt = phasor_table(th, kOscSpan);
   dmtab_.upload(mt.data(), mt.size() * sizeof(float));

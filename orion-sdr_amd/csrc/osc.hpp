@@ -8,7 +8,7 @@
 // cycle the finite-state map falls into. The device reads the reference's own
 // phasors from that table — forever when the cycle closed within the budget
 // (bit-exact), else for the first `budget` outputs, then the drift model (the fitted
-// mean step and magnitude profile). budget 0: the closed form (the ideal phasor of
+// mean step and a linear magnitude over each renorm period). budget 0: the closed form (the ideal phasor of
 // the reference's f32 step w), which is what the engine computed before round 4.
 #pragma once
 #include <cstdint>

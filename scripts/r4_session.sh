@@ -7,7 +7,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-r4}; mkdir -p "$OUT"; export TMPDIR=/tmp
 if [ "${TESTS:-1}" = 1 ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -s -p no:cacheprovider --timeout 300 --timeout-method thread ${K:+-k "$K"} > "$OUT/tests.log" 2>&1
+  timeout -k 10 500 python -u -m pytest tests -m gpu -x -q -s -p no:cacheprovider --timeout 300 --timeout-method thread ${K:+-k "$K"} > "$OUT/tests.log" 2>&1
   rc=$?; grep -E "passed|failed|Error" "$OUT/tests.log" | tail -5; [ $rc -le 1 ] || exit $rc
 fi
 timeout -k 10 200 python bench.py --config c5 --steps 20 --warmup 5 > "$OUT/bench_c5.json" 2>&1 || { tail -5 "$OUT/bench_c5.json"; exit 1; }
