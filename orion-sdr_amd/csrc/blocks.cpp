@@ -720,6 +720,7 @@ class WbfmBlock final : public Block {
     }
     const auto msh = mat_pow(ss.A, 4, kSgL / 2);
     for (int i = 0; i < 16; ++i) cs_.mh[i] = msh[i];
+    build_audio_frags(a, bq);
     // The segmented chain starts every segment's first sub-range from a zero
     // state and hands the next sub-range that sub-range's zero-state end state
     // and last 128 outputs: exact when A^(kSgL - 128) is below f32 resolution
@@ -779,6 +780,7 @@ class WbfmBlock final : public Block {
       a.hist_in = hist_[cur_].as<f2>();
       a.hist_out = hist_[nxt].as<f2>();
       a.lanemats = lanemats_.as<double>();
+      a.afrag = afrag_.as<void>();
       const int path = path_ == kPathAuto ? (seg_ok_ ? kPathSeg : kPathSplit) : path_;
       if (path == kPathSeg) {
         const long long slots = wbfm_seg_slots(static_cast<long long>(n_dec), nch_);
@@ -836,6 +838,40 @@ class WbfmBlock final : public Block {
   }
   std::vector<float> taps(int which) const override { return which == 0 ? h_dec_ : h_aud_; }
   void seek(uint64_t index) { k0_ = index; }
+  // The segmented chain's audio FIR runs on f16 matrix cores with hi + lo parts
+  // (k_wbfm.hip sg::back): the A fragments of the Toeplitz tap matrix, and the
+  // scales. |f| <= pi |k| l1(LpCascade) (atan2_approx is within [-pi, pi]), so f 2^sf
+  // with sf = floor(log2(2^15 / bound)) stays below the f16 range with a 2x margin;
+  // the taps are scaled to the same headroom. Both scales are powers of two.
+  void build_audio_frags(const std::vector<float>& a, const BiquadCoeffs& c) {
+    // l1 norm of the LpCascade's impulse response (two TDF-II biquads, iir.rs:34-40)
+    double z[4] = {0, 0, 0, 0}, l1 = 0.0;
+    auto bq = [&](double* s, double x) {
+      const double y = x * c.b0 + s[0];
+      s[0] = x * c.b1 + s[1] - c.a1 * y;
+      s[1] = x * c.b2 - c.a2 * y;
+      return y;
+    };
+    for (int n = 0; n < 1 << 16; ++n) l1 += std::fabs(bq(z + 2, bq(z, n == 0 ? 1.0 : 0.0)));
+    const double bound = M_PI * std::fabs(static_cast<double>(cf_.k)) * l1;
+    const int sf = std::max(-60, std::min(60, static_cast<int>(std::floor(std::log2(32768.0 / std::max(bound, 1e-30))))));
+    float amax = 0.0f;
+    for (float v : a) amax = std::max(amax, std::fabs(v));
+    const int st2 = amax > 0.0f ? std::max(-60, std::min(60, static_cast<int>(std::floor(std::log2(32768.0 / amax))))) : 0;
+    cs_.fscale = std::ldexp(1.0f, sf);
+    cs_.yscale = std::ldexp(1.0f, -(sf + st2));
+    std::vector<_Float16> fr(kAudFragBytes / 2);
+    for (int s = 0; s < 5; ++s)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j) {
+          const int I = l & 15, kap = 32 * s + 8 * (l >> 4) + j, k = I + 128 - kap;
+          const float v = (k >= 0 && k < static_cast<int>(a.size())) ? std::ldexp(a[k], st2) : 0.0f;
+          const _Float16 h = static_cast<_Float16>(v);
+          fr[((2 * s) * 64 + l) * 8 + j] = h;
+          fr[((2 * s + 1) * 64 + l) * 8 + j] = static_cast<_Float16>(v - static_cast<float>(h));
+        }
+    afrag_.upload(fr.data(), kAudFragBytes);
+  }
   int set_path(int path, int max_seg) {
     if ((path != kPathAuto && path != kPathSeg && path != kPathSplit) || max_seg < 0) return -3;
     if (path == kPathSeg && !seg_ok_) return -3;
@@ -854,7 +890,7 @@ class WbfmBlock final : public Block {
   bool seg_ok_ = false;
   int path_ = kPathAuto, max_seg_ = 0;
   uint32_t epoch_ = 0;
-  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, hand_, flags_, trace_;
+  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, hand_, flags_, trace_, afrag_;
   int cur_ = 0;
   uint64_t k0_ = 0;
 };

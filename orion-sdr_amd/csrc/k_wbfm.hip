@@ -38,10 +38,8 @@
 // Experiment builds only (tools/wbfm_exp.py; the product build leaves it 0): bit 1
 // reads every tile from the channel's first 512 KB (L2-resident: no HBM stream),
 // bit 2 skips the audio FIR, bit 4 skips the backs' IIR, bit 8 the predecessor
-// wait. Outputs are wrong under any bit.
-#ifndef ORION_WBFM_XCDMAP
-#define ORION_WBFM_XCDMAP 0
-#endif
+// wait, bit 32 all but one decimator FMA per output and phase. Outputs are wrong
+// under any bit.
 #ifndef ORION_WBFM_EXP
 #define ORION_WBFM_EXP 0
 #endif
@@ -739,8 +737,13 @@ __device__ __forceinline__ void phase(const f2* __restrict__ U, int c, int lp, c
       const int m = r + Q - q;  // window entry 1 .. 23 (tap q of output 8l' + r)
       const f4& wc = w[m >> 1];
       const f2 xv = (m & 1) ? f2{wc.z, wc.w} : f2{wc.x, wc.y};
-      if (FIRST && qi == 0) d[r] = splat2(t[q]) * xv;
-      else d[r] = fma2(splat2(t[q]), xv, d[r]);
+      if constexpr ((ORION_WBFM_EXP & 32) != 0) {  // experiment: one FMA per output per phase
+        if (qi == 0) d[r] = FIRST ? splat2(t[q]) * xv : fma2(splat2(t[q]), xv, d[r]);
+      } else if (FIRST && qi == 0) {
+        d[r] = splat2(t[q]) * xv;
+      } else {
+        d[r] = fma2(splat2(t[q]), xv, d[r]);
+      }
     }
   }
 }
@@ -1012,14 +1015,35 @@ __device__ __forceinline__ void zs_only16(const WbfmFusedConst& Bc, const float*
   lds_order();
 }
 
+// ---- audio FIR on the matrix cores ---------------------------------------------------
+// y[o] = sum_k a[k] f[o - k] (fir.rs:57-66, quirk-mapped taps, k < 128) as Toeplitz
+// products on v_mfma_f32_16x16x32_f16: group g of 256 outputs o = 256 g + 16 J + I
+// (I the row, J the column), K = 160 window entries kap of the column's window
+// f[256 g + 16 J - 128 + kap]: A[I][kap] = a[I + 128 - kap] (zero outside [0, 128)),
+// B[kap][J] = the window. f16 parts: f 2^sf = fh + fl, a 2^st = ah + al (host:
+// WbfmFusedConst fscale, yscale = 2^-(sf+st); sf from the bound |f| <= pi |k| times the
+// LpCascade's l1 gain, so fh never overflows); three products ah fh + ah fl + al fh
+// per step, accumulated in f32 (error ~2^-21 of sum |a f|, the order of an f32 FMA
+// chain's: tools/micro/mfma_fir.hip). The A fragments (5 steps x hi/lo x 64 lanes x 8
+// halves) come from global memory (WbfmArgs.afrag, L2-resident).
+// f planes in LDS: index e = j + 128 for j in [-128, 1040), padded 8 halves per 128
+// (pe: the 16 column reads of one ds_read_b128 hit distinct banks).
+__host__ __device__ constexpr int pe(int e) { return e + ((e >> 7) << 3); }
+constexpr int kFpN = pe(128 + 1024 + 16) + 8;  // halves per plane
+static_assert(2 * kFpN * 2 <= WBytes, "f planes fit the sub-range region");
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ _Float16 hi16(float x) { return static_cast<_Float16>(x); }
+__device__ __forceinline__ _Float16 lo16(float x, _Float16 h) { return static_cast<_Float16>(x - static_cast<float>(h)); }
+
 // The back of one sub-range [A0, A0 + Lr) from its exact entering state sw and
 // FIR history hist (f[A0 - 128 + l + 64 r]): pass 2 (the reference's f32
-// recurrence) -> pair image P -> audio FIR -> y. Returns the end state (after
-// f[A0 + L - 1]) in sw and this sub-range's last 128 IIR outputs in hist. P may
-// alias Phi (Phi is read into registers first). chan_last: the channel's last
-// sub-range (writes the IIR state and FIR history carried to the next call).
-// publish_r >= 0: publish the end state and last 128 IIR outputs to the successor
-// (publish_end) as soon as they are known, before the audio FIR.
+// recurrence) -> f planes -> audio FIR -> y. Returns the end state (after
+// f[A0 + L - 1]) in sw and this sub-range's last 128 IIR outputs in hist (as the
+// planes hold them: fh + fl, which split again to the same parts). The planes alias
+// Phi (Phi is read into registers first). chan_last: the channel's last sub-range
+// (writes the IIR state and FIR history carried to the next call). publish_r >= 0:
+// publish the end state and last 128 IIR outputs to the successor (publish_end) as
+// soon as they are known, before the audio FIR.
 // Publish a segment's end state and last 128 IIR outputs to its successor.
 __device__ __forceinline__ void publish_end(const WbfmArgs& a, int r, const double (&sw)[4], const float (&hist)[2],
                                             int l) {
@@ -1035,15 +1059,16 @@ __device__ __forceinline__ void publish_end(const WbfmArgs& a, int r, const doub
   fu::publish(a.flags + 3LL * r, a.epoch, l);
 }
 
-template <int KB = 16>
 __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc, int ch, long long A0, int Lr,
-                                     bool chan_last, const float* Phi, f2* P, int l, double (&sw)[4],
+                                     bool chan_last, const float* Phi, void* Pv, int l, double (&sw)[4],
                                      float (&hist)[2], int publish_r = -1, int trace_r = -1) {
-  constexpr int NH = Y::NH;
   const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
+  _Float16* __restrict__ Fh = static_cast<_Float16*>(Pv);
+  _Float16* __restrict__ Fl = Fh + kFpN;
+  const float fsc = Bc.fscale, funsc = 1.0f / Bc.fscale;  // powers of two
   f2 xs[CH];
   f2 ef[4];
-  {  // lane l: samples 16l .. 16l+15 (iir16), written to P one scalar at a time
+  {  // lane l: samples 16l .. 16l+15 (iir16)
     double send[4];
     if constexpr ((ORION_WBFM_EXP & 4) == 0) {
       iir16(Bc, Phi, l, sw, xs, ef, send);
@@ -1057,19 +1082,24 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
     const int jl = Lr - 1;
     float cap[4] = {0, 0, 0, 0};
     bool have = false;
-    // f[16l + i] -> pair slot pslot((16l mod NH) + PB + i), component l >= 32; the
-    // slots of i and i + 8 are CH + 1 apart (one pad per CH pairs)
-    // (the offset is laundered: hoisted out of the sub-range loop it would be one
-    // more long-lived register, spilled, with a vmcnt(0) reload)
-    int po = 2 * Y::pslot(16 * (l & 31) + fu::PB) + (l >> 5);
-    asm volatile("" : "+v"(po));
-    float* __restrict__ pe = reinterpret_cast<float*>(P) + po;
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const int e0 = pe(128 + 16 * l);  // 16 consecutive halves, inside one 128-run
+    h2 eh, el, oh, ol;  // f16 parts of f[16l + i] (E) and f[16l + 8 + i] (O), two at a time
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const int j = 16 * l + i;  // and j + 8
       const f2 f = bq.lp4(ef, xs[i]);
-      pe[2 * i] = f.x;
-      pe[2 * (i + CH + 1)] = f.y;
+      const float fe = (j < Lr ? f.x : 0.0f) * fsc, fo = (j + 8 < Lr ? f.y : 0.0f) * fsc;  // zeros past Lr
+      eh[i & 1] = hi16(fe);
+      el[i & 1] = lo16(fe, eh[i & 1]);
+      oh[i & 1] = hi16(fo);
+      ol[i & 1] = lo16(fo, oh[i & 1]);
+      if (i & 1) {
+        *reinterpret_cast<h2*>(Fh + e0 + i - 1) = eh;
+        *reinterpret_cast<h2*>(Fl + e0 + i - 1) = el;
+        *reinterpret_cast<h2*>(Fh + e0 + 8 + i - 1) = oh;
+        *reinterpret_cast<h2*>(Fl + e0 + 8 + i - 1) = ol;
+      }
       if (chan_last) {
         if (j == jl) {
 #pragma unroll
@@ -1092,63 +1122,71 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
     for (int k = 0; k < 4; ++k)
       sw[k] = static_cast<double>(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(ef[k].y), 63)));
   }
-  lds_order();
 #pragma unroll
-  for (int r2 = 0; r2 < 2; ++r2) {  // pairs j in [-128, 0): (history, f[j + NH])
-    const int t = l + 64 * r2;
-    P[Y::pslot(t)] = f2{hist[r2], P[Y::pslot(t + NH)].x};
+  for (int r2 = 0; r2 < 2; ++r2) {  // j in [-128, 0): the history
+    const int e = pe(l + 64 * r2);
+    const float x = hist[r2] * fsc;
+    const _Float16 h = hi16(x);
+    Fh[e] = h;
+    Fl[e] = lo16(x, h);
+  }
+  if (l < 2) {  // j in [1024, 1040): read by the last columns' windows against zero taps
+    const h8 z = h8{0, 0, 0, 0, 0, 0, 0, 0};
+    *reinterpret_cast<h8*>(Fh + pe(128 + 1024 + 8 * l)) = z;
+    *reinterpret_cast<h8*>(Fl + pe(128 + 1024 + 8 * l)) = z;
   }
   lds_order();
+  auto recon = [&](int e) {  // f as the planes hold it
+    const int q = pe(e);
+    return (static_cast<float>(Fh[q]) + static_cast<float>(Fl[q])) * funsc;
+  };
 #pragma unroll
-  for (int r2 = 0; r2 < 2; ++r2) hist[r2] = P[Y::pslot(NH + l + 64 * r2)].y;  // f[L - 128 + t]: the next history
+  for (int r2 = 0; r2 < 2; ++r2) hist[r2] = recon(128 + L - 128 + l + 64 * r2);  // the next history
   if (publish_r >= 0) publish_end(a, publish_r, sw, hist, l);
-  if (trace_r >= 0) fu::trace(a, trace_r, 11);  // debug: IIR done
-  {  // audio FIR (fir.rs:57-66, quirk-mapped taps) in blocks of KB taps: lane l owns
-     // outputs CH l + i (x) and NH + CH l + i (y), one v_pk_fma_f32 per tap for both
-    constexpr int O = fu::PB - (KB - 1);  // pair index of window entry 0 at lane 0, block 0
-    f2 acc[CH];
-#pragma unroll
-    for (int i = 0; i < CH; ++i) acc[i] = f2{0.0f, 0.0f};
-#pragma unroll 1
-    for (int kb = 0; kb < ((ORION_WBFM_EXP & 2) ? 0 : 128 / KB); ++kb) {
-      // tap k = KB kb + kk of output i reads pair e = CH l + i - k + PB
-      // = CH (l - kb) + O + m, m = i + KB - 1 - kk
-      const f2* __restrict__ Pl = P + (CH + 1) * (l - KB * kb / CH) + O;
-      f2 w[CH + KB - 1];
-#pragma unroll
-      for (int m = 0; m < CH + KB - 1; ++m) w[m] = Pl[m + (O + m) / CH];
-#pragma unroll
-      for (int kk = 0; kk < KB; ++kk) {
-        const f2 tap = splat2(Bc.a[KB * kb + kk]);
-#pragma unroll
-        for (int i = 0; i < CH; ++i) acc[i] = fma2(tap, w[i + KB - 1 - kk], acc[i]);
-      }
-    }
-    float* __restrict__ y = a.y + ch * a.y_stride + A0;
-    if (Lr == L && (reinterpret_cast<uintptr_t>(y) & 15) == 0) {
-      float4* ya = reinterpret_cast<float4*>(y + CH * l);
-      float4* yb = reinterpret_cast<float4*>(y + NH + CH * l);
-#pragma unroll
-      for (int i = 0; i < CH; i += 4) {
-        ya[i / 4] = float4{acc[i].x, acc[i + 1].x, acc[i + 2].x, acc[i + 3].x};
-        yb[i / 4] = float4{acc[i].y, acc[i + 1].y, acc[i + 2].y, acc[i + 3].y};
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < CH; ++i) {
-        const int j = CH * l + i;
-        if (j < Lr) y[j] = acc[i].x;
-        if (j + NH < Lr) y[j + NH] = acc[i].y;
-      }
-    }
-  }
   if (chan_last) {  // the next call's FIR history: f[n_dec - 128 .. n_dec)
 #pragma unroll
     for (int r2 = 0; r2 < 2; ++r2) {
       const int t = l + 64 * r2;
-      const int j = Lr - 128 + t;  // >= -128
-      const float f = j < NH ? P[Y::pslot(j + fu::PB)].x : P[Y::pslot(j - NH + fu::PB)].y;
-      a.carry_out[ch * kWbfmCarry + 8 + t] = f;
+      a.carry_out[ch * kWbfmCarry + 8 + t] = recon(Lr + t);
+    }
+  }
+  if (trace_r >= 0) fu::trace(a, trace_r, 11);  // debug: IIR done
+  if constexpr ((ORION_WBFM_EXP & 2) == 0) {
+    const int J = l & 15, kg = l >> 4;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    f4v acc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[g] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+    const h8* __restrict__ af = static_cast<const h8*>(a.afrag);
+#pragma unroll 1
+    for (int st = 0; st < 5; ++st) {
+      const h8 ah = af[(2 * st) * 64 + l], al = af[(2 * st + 1) * 64 + l];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int e = pe(256 * g + 16 * J + 32 * st + 8 * kg);
+        const h8 bh = *reinterpret_cast<const h8*>(Fh + e);
+        const h8 bl = *reinterpret_cast<const h8*>(Fl + e);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[g], 0, 0, 0);
+      }
+    }
+    // lane (J, kg) holds outputs 256 g + 16 J + 4 kg + r, r < 4
+    float* __restrict__ y = a.y + ch * a.y_stride + A0;
+    const float ys = Bc.yscale;
+    if (Lr == L && (reinterpret_cast<uintptr_t>(y) & 15) == 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(y + 256 * g + 16 * J + 4 * kg) =
+            float4{acc[g][0] * ys, acc[g][1] * ys, acc[g][2] * ys, acc[g][3] * ys};
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = 256 * g + 16 * J + 4 * kg + r;
+          if (j < Lr) y[j] = acc[g][r] * ys;
+        }
     }
   }
   lds_order();
@@ -1176,9 +1214,6 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
   // XCD-contiguous map measured within noise, -0.8 us, and made seven segments wait on
   // the last-dispatched blocks: VERDICT r3 weak 5).
   g.r = blockIdx.x;
-#if ORION_WBFM_XCDMAP  // A/B only: round 3's XCD-contiguous map (unsafe under contention)
-  if ((gridDim.x & 7) == 0) g.r = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-#endif
   g.ch = g.r / spc;
   g.wl = g.r - g.ch * spc;
   g.A = static_cast<long long>(g.wl) * S;

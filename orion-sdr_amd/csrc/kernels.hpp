@@ -117,6 +117,7 @@ struct WbfmFusedConst {
   float b0, b1, b2, a1, a2;   // LpCascade biquad (iir.rs:49-71)
   double pw[6 * 16];          // (A^kSgC)^(2^s)
   double mh[16];              // A^(kSgL/2): one half sub-range (read by iir16 as pw[6])
+  float fscale, yscale;       // audio FIR on the matrix cores: f scale 2^sf, output scale 2^-(sf+st)
 };
 struct WbfmArgs {
   const f2* x;  long long x_stride;  long long n;
@@ -135,7 +136,9 @@ struct WbfmArgs {
   uint32_t spin;                                    // polls before a wait times out (kernels.hpp kSpinDefault)
   uint32_t epoch;                                   // this launch's tag (never 0)
   long long* trace;                                 // debug: per-wave phase timestamps (or null)
+  const void* afrag;                                // audio FIR A fragments (k_wbfm.hip sg::back)
 };
+constexpr int kAudFragBytes = 5 * 2 * 64 * 16;     // 5 K-steps x (hi, lo) x 64 lanes x 8 halves
 constexpr int kFuTracePoints = 16;
 void launch_wbfm(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmBackConst& b, int nch,
                  hipStream_t s);
