@@ -43,9 +43,6 @@
 #ifndef ORION_WBFM_EXP
 #define ORION_WBFM_EXP 0
 #endif
-#ifndef ORION_WBFM_STAGGER
-#define ORION_WBFM_STAGGER 0  // A/B: half-sub-range offset of a SIMD's second wave (k_wbfm_seg)
-#endif
 
 namespace orion {
 namespace {
@@ -1121,7 +1118,7 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
 #pragma unroll
       for (int k = 0; k < 4; ++k) co[k] = cap[k];
     }
-    // the state after f[Lr - 1] (Lr a multiple of 16 below L: a staggered sub-range)
+    // the state after f[Lr - 1] (Lr < L: a multiple of 16 unless it is the channel's end)
     const int lend = Lr >= L ? 63 : max(0, (Lr >> 4) - 1);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
@@ -1227,12 +1224,8 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
   g.first = g.wl == 0;
   g.last = g.B == a.n_dec;
   const bool late = blockIdx.x >= (gridDim.x >> 1);
-  // Sub-ranges of L outputs; ORION_WBFM_STAGGER: the later-dispatched half of the
-  // waves (a SIMD's second wave) makes its second sub-range L/2 long, so its later
-  // backs fall half a sub-range after its partner's.
-  const bool stag = ORION_WBFM_STAGGER && late && g.Lr > 2 * sg::L;
-  const int nsub = stag ? (g.Lr + sg::L / 2 + sg::L - 1) / sg::L : (g.Lr + sg::L - 1) / sg::L;
-  const int ntiles = stag ? (g.Lr + TW - 1) / TW : nsub * sg::NS;
+  const int nsub = (g.Lr + sg::L - 1) / sg::L;
+  const int ntiles = nsub * sg::NS;
   uint32_t* const myslot = a.hand + static_cast<long long>(g.r) * sg::kSegSlot;
   fu::trace(a, g.r, 0);
 
@@ -1291,11 +1284,10 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
         ph[k][1] = cmul(tb1, ek);
       }
     }
-    const long long A0 = g.A + static_cast<long long>(sub) * sg::L - (stag && sub >= 2 ? sg::L / 2 : 0);
-    const int Lr = static_cast<int>(min(static_cast<long long>(stag && sub == 1 ? sg::L / 2 : sg::L), g.B - A0));
-    const int ntl = stag ? (Lr + TW - 1) / TW : sg::NS;
+    const long long A0 = g.A + static_cast<long long>(sub) * sg::L;
+    const int Lr = static_cast<int>(min(static_cast<long long>(sg::L), g.B - A0));
 #pragma unroll 1
-    for (int tin = 0; tin < ntl; ++tin, ++n, porg += G::NEW) {
+    for (int tin = 0; tin < sg::NS; ++tin, ++n, porg += G::NEW) {
       if ((16 * n < kSegPrioQ16 * ntiles) == late) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
       if ((n & 63) == 0)  // lane l: the common phasor of tile n + l
