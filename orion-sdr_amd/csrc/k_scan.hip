@@ -12,12 +12,19 @@ constexpr int CH = kScanCH;
 constexpr int PADN = CH + CH / 16 + 16;
 #ifndef ORION_SP_ABL
 #define ORION_SP_ABL 0  // timing experiments only: 1 no phasor table, 2 no look-back, 4 no LP scan, 8 staging + stores only
+                        // (k_lpdc_sp); 16 no wait, 32 staging + stores only (k_scan_sp)
 #endif
 #ifndef ORION_SP_MINW
 #define ORION_SP_MINW 4  // waves per SIMD k_lpdc_sp is compiled for at kSpC samples per lane (<= 128 VGPRs)
 #endif
 #ifndef ORION_SP_MINW16
 #define ORION_SP_MINW16 6  // the same at 16 samples per lane (ORION_LPDC_SC=16 experiments)
+#endif
+#ifndef ORION_SP_BATCH
+#define ORION_SP_BATCH 8  // k_scan_sp staging: loads issued together per thread (complex input)
+#endif
+#ifndef ORION_SP_BATCH_REAL
+#define ORION_SP_BATCH_REAL 8  // (real input)
 #endif
 #ifndef ORION_SCAN_SP_MINW
 #define ORION_SCAN_SP_MINW 4  // waves per SIMD k_scan_sp is compiled for (4: <= 128 VGPRs, spills 52-132 B)
@@ -880,7 +887,6 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   constexpr int SC = kSpC, C = SC, CH = SC * NT, PADN = CH + CH / SC + SC;
   constexpr int kPw = ScanMatsLayout::kPwc + 1;    // (A^C)^(2^s), C = 2 kScanC
   constexpr int kWv = ScanMatsLayout::kM128;       // A^(64 C)
-  constexpr int KT = kScanCH / NT;                 // staging steps per oscillator-table span
   __shared__ float sb[PADN];
   __shared__ double tot[4][S];
   __shared__ double cin_sh[S];
@@ -900,16 +906,17 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   // (unconditional, index clamped into [0, n)), then the pre-map. (A guarded load per
   // sample compiles to a branch around each, which waits for its load before the LDS
   // store: one memory latency per sample.) FM / PM also load x[i - 1] (an L1/L2 hit).
-  static_assert(SC % 8 == 0 && KT % 8 == 0, "staging batches");
+  constexpr int BT = PR == Pre::Real ? ORION_SP_BATCH_REAL : PR == Pre::Pm ? 8 : ORION_SP_BATCH;  // loads per thread at once
+  static_assert(SC % BT == 0 && BT <= 64 && CH <= kOscSpan, "staging batches; one oscillator cursor per chunk");
   // FM: the previous sample from the neighbour lane (below); PM: its own load of x[i - 1]
   // (an L1/L2 hit; the neighbour form measured 6 % slower there: more spills)
   constexpr bool kPair = PR == Pre::Fm, kPrev = PR == Pre::Pm;
   const long long nl = a.n - 1;
 #pragma unroll 1
-  for (int k0 = 0; k0 < SC; k0 += 8) {
-    f2 z[8], zp[8], zq = f2{0.0f, 0.0f};
+  for (int k0 = 0; k0 < SC; k0 += BT) {
+    f2 z[BT], zp[BT], zq = f2{0.0f, 0.0f};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < BT; ++j) {
       const long long i = base + t + (k0 + j) * NT;
       if constexpr (PR == Pre::Real) {
         z[j] = f2{static_cast<const float*>(a.x)[ch * a.x_stride + min(i, nl)], 0.0f};
@@ -923,11 +930,11 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
       // FM: the previous sample of lane L is lane L - 1's (a DPP shift of the mapped
       // sample: no second load, no second translation); lane 0 of the wave needs the sample before the wave's run of
       // row k0 + j: lane j of the wave loads and maps it for all eight j in one load.
-      const long long iq = base + (t & ~63) + (k0 + (lane & 7)) * NT - 1;
+      const long long iq = base + (t & ~63) + (k0 + (lane % BT)) * NT - 1;
       zq = cin_v<PR>(a, (static_cast<const f2*>(a.x) + ch * a.x_stride)[max(min(iq, nl), 0LL)], iq, base, Ro);
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < BT; ++j) {
       const int e = t + (k0 + j) * NT;
       float o;
       if constexpr (kPair) {
@@ -946,6 +953,11 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
     }
   }
   __syncthreads();
+  if constexpr ((ORION_SP_ABL & 32) != 0) {  // timing floor: staging and stores only
+    float* y = static_cast<float*>(a.y) + ch * a.y_stride + base;
+    for (int e2 = t; e2 < cnt; e2 += NT) y[e2] = sb[posS<SC>(e2)];
+    return;
+  }
 
   float xs[C];
 #pragma unroll
@@ -1002,9 +1014,14 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
       for (int i = 0; i < S; ++i) cin_sh[i] = static_cast<double>(ci[i]);
     } else {
       const uint32_t* pr = rec + (static_cast<long long>(ch) * nchunk + c - 1) * 16;
+      if constexpr ((ORION_SP_ABL & 16) != 0) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) cin_sh[i] = 0.0;
+      } else {
       if (!sp_wait2(pr + 15, pr + 15, epoch, a.spin)) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #pragma unroll
       for (int i = 0; i < S; ++i) cin_sh[i] = sp_ld64(pr + 2 * i);
+      }
     }
   }
   __syncthreads();

@@ -36,6 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 26)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--only", default="", help="run only the cases whose name starts with this (no round trip)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
@@ -53,10 +54,14 @@ def main():
         ("SsbPhasingMod(48e3, 2800, 1500, 0, usb)", orion_sdr.SsbPhasingMod(48e3, 2800.0, 1500.0), aud48, iq, 12.0),
     ]
     for name, blk, x, y, bps in cases:
+        if args.only and not name.startswith(args.only):
+            continue
         ms = timed(lambda: blk.process_device(x, y, sh), args.steps, st)
         print(json.dumps({"case": name, "n": n, "ms_per_call": round(ms, 4), "Msamples_per_s": round(n / ms / 1e3, 1),
                           "achieved_GBs": round(n * bps / ms / 1e6, 1), "frac_of_8TBs": round(n * bps / ms / 1e6 / PEAK, 3),
                           "bytes_per_sample": bps}), flush=True)
+    if args.only:
+        return
     # round trip (the reference's published kind of metric): FM mod -> WBFM chain
     mod = orion_sdr.FmPhaseAccumMod(10e6, 75e3, 1.5e6)
     chain = orion_sdr.WbfmChain(f_off=1.5e6)
