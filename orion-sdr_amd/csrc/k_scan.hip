@@ -774,11 +774,19 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
     // the carried state before chunk 0) closes the walk:
     //   excl = sum_{i <= first} (prod_{j < i} r^len_j) v_i
     double excl = 0.0, mult = 1.0;
+    // The DC blocker forgets too, only slowly: r^len ~ 0.12 per 7936-sample chunk at
+    // 2 Hz / 48 kHz. Past K chunks, with r^(K len) < 1e-20, what entered them cannot reach
+    // this chunk's f32 outputs: the walk treats chunk c-1-K as a zero state (no wait on it
+    // or beyond), and ends at latest once the walked product of r^len is below 1e-20.
+    const float lr = static_cast<float>(CH - warm) * __logf(r);
+    const int K = !(r > 0.0f) ? 1 : (lr < 0.0f ? static_cast<int>(min(64.0f, ceilf(-46.06f / lr))) : 64);
     for (int base = c - 1; !(ORION_SP_ABL & 2); base -= 64) {
       const int k = base - lane;
       double v = 0.0, mk = 1.0;
       bool closes = true;
-      if (k >= 0) {
+      if (base == c - 1 && lane >= K) {
+        // past the horizon: a zero state closes the walk (v = 0)
+      } else if (k >= 0) {
         const uint32_t* pr = rec + (static_cast<long long>(ch) * nchunk + k) * 8;
         if (!sp_wait2(pr + 6, pr + 7, epoch, a.spin)) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         closes = sp_ld(pr + 7) == epoch;
@@ -804,6 +812,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
       excl = __builtin_fma(mult, term, excl);
       if (first < 64) break;
       mult *= __shfl(pm, 63, 64);
+      if (!(fabs(mult) >= 1e-20)) break;
     }
     if (!last && lane == 0) {
       sp_st64(my + 4, __builtin_fma(bm, excl, bd));

@@ -908,7 +908,10 @@ __device__ __forceinline__ FuPrefetch fu_origin(const WbfmArgs& a, const FuRange
 // Issue priority: a SIMD's arbiter favours the older of its two waves; the later-
 // dispatched wave takes s_setprio 1 for the first 9/16 of its tiles, the earlier
 // one for the rest, so both finish together.
-constexpr int kSegPrioQ16 = 9;
+#ifndef ORION_SEG_PRIO
+#define ORION_SEG_PRIO 9  // the later wave of a SIMD leads for ORION_SEG_PRIO/16 of its tiles (A/B)
+#endif
+constexpr int kSegPrioQ16 = ORION_SEG_PRIO;
 namespace sg {
 constexpr int NS = 8;          // front tiles per sub-range
 using Y = fu::Geo<NS>;         // L 1024, NH 512, CH 8
