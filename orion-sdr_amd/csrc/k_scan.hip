@@ -12,7 +12,8 @@ constexpr int CH = kScanCH;
 constexpr int PADN = CH + CH / 16 + 16;
 #ifndef ORION_SP_ABL
 #define ORION_SP_ABL 0  // timing experiments only: 1 no phasor table, 2 no look-back, 4 no LP scan, 8 staging + stores only
-                        // (k_lpdc_sp); 16 no wait, 32 staging + stores only (k_scan_sp)
+                        // (k_lpdc_sp); 16 no wait, 32 staging + stores only, 64 no zero-state pass,
+                        // 128 no re-run (k_scan_sp)
 #endif
 #ifndef ORION_SP_MINW
 #define ORION_SP_MINW 4  // waves per SIMD k_lpdc_sp is compiled for at kSpC samples per lane (<= 128 VGPRs)
@@ -976,7 +977,7 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   for (int i = 0; i < S; ++i) s0[i] = 0.0f;
 #pragma unroll
   for (int i = 0; i < C; ++i)
-    if (t * C + i < cnt) (void)rr.step(s0, xs[i]);
+    if (!(ORION_SP_ABL & 64) && t * C + i < cnt) (void)rr.step(s0, xs[i]);
   double q[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) q[i] = s0[i];
@@ -1075,7 +1076,7 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   }  // TR
 #pragma unroll
   for (int i = 0; i < C; ++i)
-    if (t * C + i < cnt) xs[i] = postmap<PO>(a, rr.step(ef, xs[i]));  // the reference's f32 update
+    if (!(ORION_SP_ABL & 128) && t * C + i < cnt) xs[i] = postmap<PO>(a, rr.step(ef, xs[i]));  // the reference's f32 update
   if (last && t * C <= cnt - 1 && cnt - 1 < t * C + C) {  // carried state of the next call
     float* co = a.carry_out + ch * kScanCarry;
 #pragma unroll
