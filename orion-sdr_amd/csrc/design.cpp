@@ -337,6 +337,13 @@ static std::vector<double> extract_A(int S, Step step) {
   }
   return A;
 }
+// B: one step from the zero state with x = 1.
+template <class Step>
+static std::vector<double> extract_B(int S, Step step) {
+  std::vector<double> s(S, 0.0);
+  step(s.data(), 1.0);
+  return s;
+}
 
 static double biquad_step(double* z, double x, const BiquadCoeffs& c) {  // iir.rs:34-40
   const double y = x * c.b0 + z[0];
@@ -350,10 +357,12 @@ static double biquad_step(double* z, double x, const BiquadCoeffs& c) {  // iir.
 StateSpace lp_cascade_ss(const BiquadCoeffs& c) {
   StateSpace ss;
   ss.S = 4;
-  ss.A = extract_A(4, [&](double* s, double x) {
+  const auto step = [&](double* s, double x) {
     const double y0 = biquad_step(s, x, c);
     biquad_step(s + 2, y0, c);
-  });
+  };
+  ss.A = extract_A(4, step);
+  ss.B = extract_B(4, step);
   ss.D = 0;
   return ss;
 }
@@ -361,7 +370,9 @@ StateSpace lp_cascade_ss(const BiquadCoeffs& c) {
 StateSpace biquad_ss(const BiquadCoeffs& c) {  // iir.rs:34-40, state (z1, z2)
   StateSpace ss;
   ss.S = 2;
-  ss.A = extract_A(2, [&](double* s, double x) { biquad_step(s, x, c); });
+  const auto step = [&](double* s, double x) { biquad_step(s, x, c); };
+  ss.A = extract_A(2, step);
+  ss.B = extract_B(2, step);
   ss.D = 0;
   return ss;
 }
@@ -369,13 +380,15 @@ StateSpace biquad_ss(const BiquadCoeffs& c) {  // iir.rs:34-40, state (z1, z2)
 StateSpace lpdc_ss(const LpDcCoeffs& c) {  // iir.rs:151-165, state (z0_1,z0_2,z1_1,z1_2,dc_x1,dc_y1)
   StateSpace ss;
   ss.S = 6;
-  ss.A = extract_A(6, [&](double* s, double x) {
+  const auto step = [&](double* s, double x) {
     const double y0 = biquad_step(s, x, c.bq);
     const double y1 = biquad_step(s + 2, y0, c.bq);
     const double y = y1 - s[4] + static_cast<double>(c.r) * s[5];
     s[4] = y1;
     s[5] = y;
-  });
+  };
+  ss.A = extract_A(6, step);
+  ss.B = extract_B(6, step);
   ss.D = 0;
   return ss;
 }
@@ -383,11 +396,13 @@ StateSpace lpdc_ss(const LpDcCoeffs& c) {  // iir.rs:151-165, state (z0_1,z0_2,z
 StateSpace dc_ss(float r) {  // dc.rs:47-51, state (x1, y1)
   StateSpace ss;
   ss.S = 2;
-  ss.A = extract_A(2, [&](double* s, double x) {
+  const auto step = [&](double* s, double x) {
     const double y = x - s[0] + static_cast<double>(r) * s[1];
     s[0] = x;
     s[1] = y;
-  });
+  };
+  ss.A = extract_A(2, step);
+  ss.B = extract_B(2, step);
   ss.D = 0;
   return ss;
 }
@@ -396,6 +411,7 @@ StateSpace onepole_ss(float a) {  // cw.rs:40, state y
   StateSpace ss;
   ss.S = 1;
   ss.A = {static_cast<double>(a)};
+  ss.B = {static_cast<double>(1.0f - a)};  // s = a s + (1 - a) x, (1 - a) in f32 as iir.hpp RecOnePole
   ss.D = 0;
   return ss;
 }

@@ -21,6 +21,9 @@ constexpr int PADN = CH + CH / 16 + 16;
 #ifndef ORION_SP_MINW16
 #define ORION_SP_MINW16 6  // the same at 16 samples per lane (ORION_LPDC_SC=16 experiments)
 #endif
+#ifndef ORION_SP_ZMAP
+#define ORION_SP_ZMAP 1  // k_scan_sp: zero-state pass as the linear map (0: the recurrence, A/B)
+#endif
 #ifndef ORION_SP_BATCH
 #define ORION_SP_BATCH 8  // k_scan_sp staging: loads issued together per thread (complex input)
 #endif
@@ -975,9 +978,24 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   float s0[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) s0[i] = 0.0f;
+  if constexpr ((ORION_SP_ABL & 64) != 0) {
+  } else if constexpr (ORION_SP_ZMAP != 0) {
+    // the lane run's zero-state end state as the linear map sum_i A^(C-1-i) B x_i
+    // (independent FMAs instead of the recurrence's dependent chain; samples past the
+    // chunk enter as zeros: only the last partial lane differs, whose state reaches no
+    // valid output)
+    const float* __restrict__ E = a.zmap;
 #pragma unroll
-  for (int i = 0; i < C; ++i)
-    if (!(ORION_SP_ABL & 64) && t * C + i < cnt) (void)rr.step(s0, xs[i]);
+    for (int i = 0; i < C; ++i) {
+      const float xv = t * C + i < cnt ? xs[i] : 0.0f;
+#pragma unroll
+      for (int k = 0; k < S; ++k) s0[k] = __builtin_fmaf(E[i * S + k], xv, s0[k]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < C; ++i)
+      if (t * C + i < cnt) (void)rr.step(s0, xs[i]);
+  }
   double q[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) q[i] = s0[i];

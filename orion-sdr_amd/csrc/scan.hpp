@@ -69,6 +69,7 @@ struct ScanArgs {
   int translate;                       // Pre::Fm: apply the fm.rs:48-58 translator
   OscDev osc;                          // the translator's / BFO's Rotator (hip_common.hpp)
   const double* mats;                  // ScanMatsLayout (f64: see iir.hpp matvec_acc)
+  const float* zmap;                   // k_scan_sp: [kSpC][S] A^(kSpC-1-i) B, a lane run's zero-state map
   double* aggs;                        // [ch][nblk][S]
   double* sin;                         // [ch][nblk][S] state entering each workgroup
   const float* carry_in;               // [ch][kScanCarry]

@@ -19,6 +19,19 @@ class ScanStage {
       : rec_(rec), pre_(pre), post_(post), c_(c), nch_(nch), S_(ss.S) {
     const auto mats = build_mats(ss);
     mats_.upload(mats.data(), mats.size() * sizeof(double));
+    {  // the zero-state end state of a kSpC-sample lane run, sum_i A^(kSpC-1-i) B x_i (k_scan_sp)
+      std::vector<float> z(static_cast<size_t>(kSpC) * S_);
+      std::vector<double> col = ss.B;  // A^j B, j = 0, 1, ...
+      if (col.size() != static_cast<size_t>(S_)) col.assign(S_, 0.0);
+      for (int i = kSpC - 1; i >= 0; --i) {
+        for (int k = 0; k < S_; ++k) z[static_cast<size_t>(i) * S_ + k] = static_cast<float>(col[k]);
+        std::vector<double> nx(S_, 0.0);
+        for (int r = 0; r < S_; ++r)
+          for (int k = 0; k < S_; ++k) nx[r] += ss.A[r * S_ + k] * col[k];
+        col = nx;
+      }
+      zmap_.upload(z.data(), z.size() * sizeof(float));
+    }
     for (auto& c0 : carry_) c0.resize(static_cast<size_t>(nch_) * kScanCarry * sizeof(float));
     // LpDcCascade after an SSB / AM-abs front end: single pass when the LP4
     // forgets its state within the kSpWarm-sample warm-up (SsbProductDemod at
@@ -112,6 +125,7 @@ class ScanStage {
     a.translate = translate_ ? 1 : 0;
     if (osc_) a.osc = osc_->dev();
     a.mats = mats_.as<double>();
+    a.zmap = zmap_.as<float>();
     a.aggs = ws_.as<double>();
     a.sin = ws_.as<double>() + nblk * nch_ * S_;
     a.carry_in = carry_[cur_].as<float>();
@@ -148,7 +162,7 @@ class ScanStage {
   int nch_, S_;
   bool translate_ = false;
   std::unique_ptr<RefOsc> osc_;
-  DevBuf mats_, carry_[2], ws_, mats_lp_, rec_buf_;
+  DevBuf mats_, carry_[2], ws_, mats_lp_, rec_buf_, zmap_;
   int cur_ = 0;
   bool sp_ok_ = false;   // k_lpdc_sp (LpDcCascade after SSB / AM-abs)
   bool sp1_ok_ = false;  // k_scan_sp (stages that forget within one chunk)
