@@ -27,6 +27,9 @@ enum : int { kRotate = 0, kUsb = 1, kNcoMix = 2, kNcoGen = 3 };
 #ifndef ORION_ROT_MINW
 #define ORION_ROT_MINW 6  // waves per SIMD k_rotator is compiled for (8: <= 64 VGPRs, 6 B of spills)
 #endif
+#ifndef ORION_FIR4_TILES_PER_CU
+#define ORION_FIR4_TILES_PER_CU 4  // k_fir_iq8 with 4 outputs per lane below this many 2048-output tiles per CU
+#endif
 #ifndef ORION_ROT_HP
 #define ORION_ROT_HP 2  // pairs per thread whose loads a full tile issues together
 #endif
@@ -505,6 +508,44 @@ __device__ __forceinline__ void fir8_blocks(const f2* __restrict__ L, const floa
   }
 }
 
+// Four outputs per lane (small calls: twice the waves of fir8_blocks). Image padded 2
+// f2 per 4 samples (pidx4), so lane t's window starts 6t f2 in: the 16 lanes of a
+// ds_read_b128 group start 12 banks apart, all distinct. Tap order per output as
+// fir8_blocks (bit-identical results).
+template <int KP>
+__device__ __forceinline__ void fir4_blocks(const f2* __restrict__ L, const float* __restrict__ Gt, int t,
+                                            f2 (&acc)[4]) {
+  const f2* __restrict__ Lt = L + 6 * t + 3 * (KP - 16) / 2;
+#pragma unroll 1
+  for (int kb = 0; kb < KP / 16; ++kb) {
+    const f2* __restrict__ Lb = Lt - 24 * kb;
+    const f4* __restrict__ tq = reinterpret_cast<const f4*>(Gt + 16 * kb);
+    float tp[16];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const f4 u = tq[q4];
+      tp[4 * q4] = u.x;
+      tp[4 * q4 + 1] = u.y;
+      tp[4 * q4 + 2] = u.z;
+      tp[4 * q4 + 3] = u.w;
+    }
+    f2 w[20];  // samples p0 .. p0 + 19 (group g of 4 at 6 g)
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const int h = i < 2 ? 8 + i : 9 - i;  // the last group first (the first FMAs' operands)
+      const f4 v = *reinterpret_cast<const f4*>(Lb + 6 * (h >> 1) + 2 * (h & 1));
+      w[2 * h] = f2{v.x, v.y};
+      w[2 * h + 1] = f2{v.z, v.w};
+    }
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      const f2 tap = splat2(tp[kk]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = fma2(tap, w[16 + r - kk], acc[r]);
+    }
+  }
+}
+
 // --------------------------------------------------------- real FIR -------
 // y[i] = sum_{k<KP} g[k] x[i-k], 512 outputs per sub-tile, 2 per lane.
 template <int KP>
@@ -594,20 +635,21 @@ __global__ __launch_bounds__(NT) void k_fir_real_generic(const float* __restrict
 // per lane; the tile plus its KP-sample halo is staged once in LDS (padded 2 per 8
 // against bank conflicts) behind one barrier. INPLACE (y == x): the halo comes from
 // boundary copies E taken before the launch, so no tile reads a neighbour's output.
-template <int KP, bool INPLACE = false>
+template <int KP, bool INPLACE = false, int R = 8>
 __global__ __launch_bounds__(NT) void k_fir_iq8(const f2* x, long long n,
                                                 const f2* __restrict__ hist, int hist_len,
                                                 f2* y, long long n_out, long long off,
                                                 const Taps256 g, const f2* __restrict__ E = nullptr,
                                                 f2* __restrict__ hist_out = nullptr) {
   if constexpr (!INPLACE) hist_next(x, n, hist, hist_out, hist_len);
-  constexpr int TT = 8 * NT;
+  static_assert(R == 8 || R == 4, "outputs per lane");
+  constexpr int TT = R * NT;
   constexpr int W = TT + KP + 2, PER = (W + NT - 1) / NT;
-  constexpr int WP = W + 2 * (W / 8) + 2;
+  constexpr int WP = R == 8 ? W + 2 * (W / 8) + 2 : W + 2 * (W / 4) + 2;
   static_assert(KP % 16 == 0, "taps padded to 16");
   __shared__ __attribute__((aligned(16))) f2 L[WP];
   __shared__ __attribute__((aligned(16))) float Gt[KP];  // the taps (read by the first barrier)
-  auto pidx = [](int p) { return p + 2 * (p >> 3); };
+  auto pidx = [](int p) { return R == 8 ? p + 2 * (p >> 3) : p + 2 * (p >> 2); };
   const int t = threadIdx.x;
   for (int k = t; k < KP; k += NT) Gt[k] = g.g[k];
   for (long long J = static_cast<long long>(blockIdx.x) * TT; J < n_out;
@@ -649,18 +691,19 @@ __global__ __launch_bounds__(NT) void k_fir_iq8(const f2* x, long long n,
       for (int p = t; p < W; p += NT) L[pidx(p)] = load_hist(x, n, hist, hist_len, org + p);
     }
     __syncthreads();
-    f2 acc[8];
+    f2 acc[R];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) acc[r] = f2{0.0f, 0.0f};
-    fir8_blocks<KP>(L, Gt, t, acc);
-    const long long j0 = J + 8 * t;
-    if (j0 + 8 <= n_out && (reinterpret_cast<uintptr_t>(y + j0) & 15) == 0) {
+    for (int r = 0; r < R; ++r) acc[r] = f2{0.0f, 0.0f};
+    if constexpr (R == 8) fir8_blocks<KP>(L, Gt, t, acc);
+    else fir4_blocks<KP>(L, Gt, t, acc);
+    const long long j0 = J + R * t;
+    if (j0 + R <= n_out && (reinterpret_cast<uintptr_t>(y + j0) & 15) == 0) {
       f4* yo = reinterpret_cast<f4*>(y + j0);
 #pragma unroll
-      for (int r = 0; r < 8; r += 2) yo[r / 2] = f4{acc[r].x, acc[r].y, acc[r + 1].x, acc[r + 1].y};
+      for (int r = 0; r < R; r += 2) yo[r / 2] = f4{acc[r].x, acc[r].y, acc[r + 1].x, acc[r + 1].y};
     } else {
 #pragma unroll
-      for (int r = 0; r < 8; ++r)
+      for (int r = 0; r < R; ++r)
         if (j0 + r < n_out) y[j0 + r] = acc[r];
     }
     __syncthreads();
@@ -827,10 +870,20 @@ void launch_fir_iq(const f2* x, long long n, const f2* hist, int hist_len, f2* y
                    long long off, int K, const Taps256& g, const float* g_dev, hipStream_t s, f2* hist_out) {
   if (n_out <= 0) return;
   if (K <= 256 && hist_len >= (K <= 64 ? 64 : K <= 128 ? 128 : 256)) {
-    const int g8 = grid_for(n_out, 8 * NT);
-    if (K <= 64) k_fir_iq8<64><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
-    else if (K <= 128) k_fir_iq8<128><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
-    else k_fir_iq8<256><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
+    // calls that fill fewer than ORION_FIR4_TILES_PER_CU tiles of 8 outputs per lane per CU
+    // take four outputs per lane (twice the waves; the FMA work is the same)
+    const bool four = n_out < static_cast<long long>(ORION_FIR4_TILES_PER_CU) * device_cus() * 8 * NT;
+    if (four) {
+      const int g4 = grid_for(n_out, 4 * NT);
+      if (K <= 64) k_fir_iq8<64, false, 4><<<g4, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
+      else if (K <= 128) k_fir_iq8<128, false, 4><<<g4, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
+      else k_fir_iq8<256, false, 4><<<g4, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
+    } else {
+      const int g8 = grid_for(n_out, 8 * NT);
+      if (K <= 64) k_fir_iq8<64><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
+      else if (K <= 128) k_fir_iq8<128><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
+      else k_fir_iq8<256><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
+    }
   } else {
     k_fir_iq_generic<<<grid_for(n_out, NT), NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, K, g_dev);
     if (hist_out) launch_hist_update_c(x, n, hist, hist_out, hist_len, s);
