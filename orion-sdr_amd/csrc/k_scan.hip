@@ -610,9 +610,21 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
   if constexpr (LP) {
   float s0[S] = {0, 0, 0, 0};
 #if !(ORION_SP_ABL & 4)
+#if ORION_SP_ZMAP
+  {  // the lane run's zero-state end state as the linear map (k_scan_sp)
+    const float* __restrict__ E = a.zmap;
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      const float xv = t * C + i < cnt ? xs[i] : 0.0f;
+#pragma unroll
+      for (int k = 0; k < S; ++k) s0[k] = __builtin_fmaf(E[i * S + k], xv, s0[k]);
+    }
+  }
+#else
 #pragma unroll
   for (int i = 0; i < C; ++i)
     if (t * C + i < cnt) (void)lp.step(s0, xs[i]);
+#endif
 #endif
   double q[S];
 #pragma unroll
@@ -1126,6 +1138,7 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
 __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
                                                    uint64_t k0, const OscDev aud, const OscDev rf, float side,
                                                    ScanCoef cf, const double* __restrict__ mlp,
+                                                   const float* __restrict__ zmap,
                                                    const float* __restrict__ carry_in, float* __restrict__ carry_out) {
   constexpr int S = 4;
   __shared__ float sb[2][PADN];
@@ -1173,9 +1186,18 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
     for (int i = 0; i < C; ++i) xs[b][i] = sb[b][pos(t * C + i)];
 #pragma unroll
     for (int k = 0; k < S; ++k) s0[b][k] = 0.0f;
+#if ORION_SP_ZMAP
+#pragma unroll
+    for (int i = 0; i < C; ++i) {  // the lane run's zero-state end state as the linear map (k_scan_sp)
+      const float xv = t * C + i < cnt ? xs[b][i] : 0.0f;
+#pragma unroll
+      for (int k = 0; k < S; ++k) s0[b][k] = __builtin_fmaf(zmap[i * S + k], xv, s0[b][k]);
+    }
+#else
 #pragma unroll
     for (int i = 0; i < C; ++i)
       if (t * C + i < cnt) (void)lp.step(s0[b], xs[b][i]);
+#endif
     double q[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) q[k] = s0[b][k];
@@ -1289,12 +1311,13 @@ int scan_state_dim(RecK rec) {
 }
 
 void launch_ssb_mod_sp(const float* x, f2* y, long long n, uint64_t k0, const OscDev& aud, const OscDev& rf,
-                       float side, const ScanCoef& c, const double* mats_lp, const float* carry_in, float* carry_out,
-                       hipStream_t s) {
+                       float side, const ScanCoef& c, const double* mats_lp, const float* zmap_lp,
+                       const float* carry_in, float* carry_out, hipStream_t s) {
   if (n <= 0) return;
   const long long grid = lpdc_sp_chunks(n);
   if (grid > (1LL << 31) - 1) throw HipError("single-pass SSB modulator grid too large");
-  k_ssb_mod_sp<<<static_cast<int>(grid), NT, 0, s>>>(x, y, n, k0, aud, rf, side, c, mats_lp, carry_in, carry_out);
+  k_ssb_mod_sp<<<static_cast<int>(grid), NT, 0, s>>>(x, y, n, k0, aud, rf, side, c, mats_lp, zmap_lp, carry_in,
+                                                       carry_out);
   ORION_LAUNCH_CHECK();
 }
 

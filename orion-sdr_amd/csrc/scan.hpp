@@ -100,8 +100,8 @@ long long lpdc_sp_demod_chunks(long long n, int sc, int warm);  // warm: kSpWarm
 // SsbPhasingMod in one pass (k_ssb_mod_sp): valid when ||A_lp^kSpWarm|| is
 // negligible; mats_lp = the LP4 scan matrices; carry = [I 4][Q 4] floats.
 void launch_ssb_mod_sp(const float* x, f2* y, long long n, uint64_t k0, const OscDev& aud, const OscDev& rf,
-                       float side, const ScanCoef& c, const double* mats_lp, const float* carry_in, float* carry_out,
-                       hipStream_t s);
+                       float side, const ScanCoef& c, const double* mats_lp, const float* zmap_lp,
+                       const float* carry_in, float* carry_out, hipStream_t s);
 void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, uint32_t* rec, uint32_t epoch,
                     hipStream_t s);
 int scan_state_dim(RecK rec);

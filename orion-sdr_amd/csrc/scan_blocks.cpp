@@ -19,17 +19,8 @@ class ScanStage {
       : rec_(rec), pre_(pre), post_(post), c_(c), nch_(nch), S_(ss.S) {
     const auto mats = build_mats(ss);
     mats_.upload(mats.data(), mats.size() * sizeof(double));
-    {  // the zero-state end state of a kSpC-sample lane run, sum_i A^(kSpC-1-i) B x_i (k_scan_sp)
-      std::vector<float> z(static_cast<size_t>(kSpC) * S_);
-      std::vector<double> col = ss.B;  // A^j B, j = 0, 1, ...
-      if (col.size() != static_cast<size_t>(S_)) col.assign(S_, 0.0);
-      for (int i = kSpC - 1; i >= 0; --i) {
-        for (int k = 0; k < S_; ++k) z[static_cast<size_t>(i) * S_ + k] = static_cast<float>(col[k]);
-        std::vector<double> nx(S_, 0.0);
-        for (int r = 0; r < S_; ++r)
-          for (int k = 0; k < S_; ++k) nx[r] += ss.A[r * S_ + k] * col[k];
-        col = nx;
-      }
+    {  // the zero-state end state of a kSpC-sample lane run (k_scan_sp)
+      const auto z = build_zmap(ss, kSpC);
       zmap_.upload(z.data(), z.size() * sizeof(float));
     }
     for (auto& c0 : carry_) c0.resize(static_cast<size_t>(nch_) * kScanCarry * sizeof(float));
@@ -68,8 +59,25 @@ class ScanStage {
       if (sp_ok_) {
         const auto ml = build_mats(lp);
         mats_lp_.upload(ml.data(), ml.size() * sizeof(double));
+        const auto zl = build_zmap(lp, kLpdcSC);  // k_lpdc_sp's LP4 lane runs
+        zmap_lp_.upload(zl.data(), zl.size() * sizeof(float));
       }
     }
+  }
+  // sum_i A^(C-1-i) B x_i, the zero-state end state of a C-sample lane run: [C][S] floats
+  static std::vector<float> build_zmap(const StateSpace& ss, int C) {
+    const int S = ss.S;
+    std::vector<float> z(static_cast<size_t>(C) * S, 0.0f);
+    std::vector<double> col = ss.B;  // A^j B, j = 0, 1, ...
+    if (col.size() != static_cast<size_t>(S)) col.assign(S, 0.0);
+    for (int i = C - 1; i >= 0; --i) {
+      for (int k = 0; k < S; ++k) z[static_cast<size_t>(i) * S + k] = static_cast<float>(col[k]);
+      std::vector<double> nx(S, 0.0);
+      for (int r = 0; r < S; ++r)
+        for (int k = 0; k < S; ++k) nx[r] += ss.A[r * S + k] * col[k];
+      col = nx;
+    }
+    return z;
   }
   static std::vector<double> build_mats(const StateSpace& ss) {
     const int S = ss.S;
@@ -125,7 +133,7 @@ class ScanStage {
     a.translate = translate_ ? 1 : 0;
     if (osc_) a.osc = osc_->dev();
     a.mats = mats_.as<double>();
-    a.zmap = zmap_.as<float>();
+    a.zmap = sp1_ok_ || !sp_ok_ ? zmap_.as<float>() : zmap_lp_.as<float>();  // k_lpdc_sp: its LP4's map
     a.aggs = ws_.as<double>();
     a.sin = ws_.as<double>() + nblk * nch_ * S_;
     a.carry_in = carry_[cur_].as<float>();
@@ -162,7 +170,7 @@ class ScanStage {
   int nch_, S_;
   bool translate_ = false;
   std::unique_ptr<RefOsc> osc_;
-  DevBuf mats_, carry_[2], ws_, mats_lp_, rec_buf_, zmap_;
+  DevBuf mats_, carry_[2], ws_, mats_lp_, rec_buf_, zmap_, zmap_lp_;
   int cur_ = 0;
   bool sp_ok_ = false;   // k_lpdc_sp (LpDcCascade after SSB / AM-abs)
   bool sp1_ok_ = false;  // k_scan_sp (stages that forget within one chunk)
@@ -388,6 +396,8 @@ class SsbModBlock final : public Block {
     if (sp_ok_) {
       const auto ml = ScanStage::build_mats(ss);
       mats_.upload(ml.data(), ml.size() * sizeof(double));
+      const auto zl = ScanStage::build_zmap(ss, kScanC);  // k_ssb_mod_sp's lane runs
+      zmap_.upload(zl.data(), zl.size() * sizeof(float));
       for (auto& c : carry_) c.resize(8 * sizeof(float));
     }
     reset_sp();
@@ -401,8 +411,8 @@ class SsbModBlock final : public Block {
     const long long nn = static_cast<long long>(n);
     if (sp_ok_ && mode_ == 0) {
       launch_ssb_mod_sp(static_cast<const float*>(in), static_cast<f2*>(out), nn, aud_.count(), aud_.dev(), rf_.dev(),
-                        side_, coef_lp(b_), mats_.as<double>(), carry_[cur_].as<float>(), carry_[cur_ ^ 1].as<float>(),
-                        s);
+                        side_, coef_lp(b_), mats_.as<double>(), zmap_.as<float>(), carry_[cur_].as<float>(),
+                        carry_[cur_ ^ 1].as<float>(), s);
       cur_ ^= 1;
     } else {
       u_.resize(2 * n * sizeof(float));
@@ -447,7 +457,7 @@ class SsbModBlock final : public Block {
   float side_;
   BiquadCoeffs b_;
   std::unique_ptr<ScanStage> st_;
-  DevBuf u_, v_, mats_, carry_[2];
+  DevBuf u_, v_, mats_, carry_[2], zmap_;
   bool sp_ok_ = false;
   int mode_ = 0, cur_ = 0;
 };
