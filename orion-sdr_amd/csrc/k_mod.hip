@@ -129,8 +129,7 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_back(const float* __restrict__ v
 #define ORION_FM_ABL 0  // experiment builds only (wrong output): 1 no look-back, 2 no RF phasor reads
 #endif
 #ifndef ORION_FM_LB
-#define ORION_FM_LB 1  // look-back records per lane and step (A/B at 2^26: 1 0.406 ms, 2 0.476, 4 0.581,
-                       // 8 0.729; no look-back at all 0.251: the wait for predecessors dominates)
+#define ORION_FM_LB 1  // look-back records per lane and step (64 ORION_FM_LB chunks per step)
 #endif
 #ifndef ORION_FM_G
 #define ORION_FM_G 8  // RF phasor reads per thread issued together
@@ -356,36 +355,43 @@ __global__ __launch_bounds__(NT, ORION_FM_MINW) void k_fm_mod_sp(const float* __
     // their flag loads all issued before any is tested
     constexpr int L = ORION_FM_LB;
     for (int b = c - 1; !(ORION_FM_ABL & 1); b -= 64 * L) {
-      uint32_t f7[L];
-      bool seen[L];
+      // every flag load of the step issued at once (clamped index; no short-circuit
+      // that would serialise them), then every value load
+      uint32_t f6[L], f7[L];
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const int k = max(b - L * lane - j, 0);
+        f6[j] = fm_ld(rec + static_cast<long long>(k) * 8 + 6);
+        f7[j] = fm_ld(rec + static_cast<long long>(k) * 8 + 7);
+      }
 #pragma unroll
       for (int j = 0; j < L; ++j) {
         const int k = b - L * lane - j;
-        const uint32_t* pr = rec + static_cast<long long>(k) * 8;
-        f7[j] = k >= 0 ? fm_ld(pr + 7) : epoch;
-        seen[j] = f7[j] == epoch || (k >= 0 && fm_ld(pr + 6) == epoch);
+        if (k >= 0 && f6[j] != epoch && f7[j] != epoch) {  // not yet published: bounded wait
+          const uint32_t* pr = rec + static_cast<long long>(k) * 8;
+          bool seen = false;  // (spin 0: time out at once, test-only)
+          for (uint32_t it = 0; it < spin && !seen; ++it) {
+            __builtin_amdgcn_s_sleep(2);
+            f7[j] = fm_ld(pr + 7);
+            f6[j] = fm_ld(pr + 6);
+            seen = f7[j] == epoch || f6[j] == epoch;
+          }
+          if (!seen) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      uint64_t vv[L];
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const int k = max(b - L * lane - j, 0);
+        vv[j] = fm_ld64(rec + static_cast<long long>(k) * 8 + (f7[j] == epoch ? 2 : 0));
       }
       uint64_t all = 0, upto = 0;  // the lane's L terms; its terms up to its nearest closing one
       int mine = L;                // the lane's nearest closing record (L: none)
 #pragma unroll
       for (int j = 0; j < L; ++j) {
         const int k = b - L * lane - j;
-        uint64_t v;
-        bool closes = true;
-        if (k >= 0) {
-          const uint32_t* pr = rec + static_cast<long long>(k) * 8;
-          // bounded wait (spin 0: time out at once, test-only)
-          for (uint32_t it = 0; it < spin && !seen[j]; ++it) {
-            __builtin_amdgcn_s_sleep(2);
-            f7[j] = fm_ld(pr + 7);
-            seen[j] = f7[j] == epoch || fm_ld(pr + 6) == epoch;
-          }
-          if (!seen[j]) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          closes = f7[j] == epoch;
-          v = closes ? fm_ld64(pr + 2) : fm_ld64(pr);
-        } else {
-          v = k == -1 ? carry_in[0] : 0;  // the carried phase before chunk 0
-        }
+        const bool closes = k < 0 || f7[j] == epoch;
+        const uint64_t v = k >= 0 ? vv[j] : (k == -1 ? carry_in[0] : 0);  // the carried phase before chunk 0
         all += v;
         if (mine == L) {
           upto += v;

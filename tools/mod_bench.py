@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 26)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--only", default="", help="run only the cases whose name starts with this (no round trip)")
+    ap.add_argument("--passes", type=int, default=0, help="orion_block_configure MOD_PASSES (0 single pass, 3)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
@@ -56,6 +57,8 @@ def main():
     for name, blk, x, y, bps in cases:
         if args.only and not name.startswith(args.only):
             continue
+        if args.passes and not name.startswith("Am"):
+            blk.configure_option("mod_passes", args.passes)
         ms = timed(lambda: blk.process_device(x, y, sh), args.steps, st)
         print(json.dumps({"case": name, "n": n, "ms_per_call": round(ms, 4), "Msamples_per_s": round(n / ms / 1e3, 1),
                           "achieved_GBs": round(n * bps / ms / 1e6, 1), "frac_of_8TBs": round(n * bps / ms / 1e6 / PEAK, 3),
