@@ -81,7 +81,7 @@ int orion_diag_stream_destroy(void* stream);
  * its phasors. The finite-state recurrence falls into a cycle; when the cycle closes
  * within the budget (-1.5 MHz / 10 MHz: after 21504 steps) every output is the
  * reference's, bit for bit, forever. Otherwise outputs past the budget follow a drift
- * model (the fitted mean step and renorm-period magnitude profile).
+ * model (the fitted mean step and a magnitude linear in the renorm position).
  * Construction fails (NULL, orion_last_error) if TAU * freq_hz / fs is not finite. */
 orion_block* orion_rotator_new(float freq_hz, float fs);
 /* dsp/rotator.rs:35-39 Rotator::set_freq(freq_hz, fs): a new step phasor; z and the

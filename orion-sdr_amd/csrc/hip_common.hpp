@@ -110,7 +110,7 @@ __device__ __forceinline__ float osc_mag(const OscDev& o, uint32_t pos) {
 // kind 0 every output from the table, 1 every output modelled, 2 mixed (the first
 // `rem` from the table); j = the table index of k, wrapped into the cycle (with
 // cyc_len >= kOscSpan a run wraps at most once; tables hold < 2^31 outputs, so table
-// indices are 32-bit); S = the model phasor of k; klo = k mod 2^32 (profile index).
+// indices are 32-bit); S = the model phasor of k; klo = k mod 2^32 (magnitude position).
 struct OscRun {
   uint32_t j, rem, klo;
   int kind;

@@ -494,7 +494,7 @@ __device__ __forceinline__ void dc_combine(double m1, double d1, double& m2, dou
 // the staging, the LP4 re-run's rewrite and the output staging from their readers (a
 // wave's LDS operations execute in order). The SSB mixing phasor of element e is the
 // BFO's output k0 + base + e: the reference's from its table, or in the drift model
-// (S mtab[64 SC w + l]) mtab[64 k] scaled by the magnitude profile.
+// (S mtab[64 SC w + l]) mtab[64 k] scaled by the linear magnitude model.
 template <int SC>
 __device__ __forceinline__ int posS(int e) { return e + e / SC; }
 __device__ __forceinline__ void wave_order() { asm volatile("" ::: "memory"); }

@@ -105,7 +105,7 @@ def test_osc_table_is_the_reference_recurrence(oracle, f, fs, cyc):
 @pytest.mark.parametrize("f,fs", [(1.234e6, 10e6), (1500.0, 48e3), (-5000.0, 48e3), (700.0, 48e3)])
 def test_osc_drift_model_past_the_budget(oracle, f, fs):
     """Without a cycle inside the budget the outputs past it follow the drift model
-    (the reference's last tabulated phasor, the fitted mean step, the magnitude profile
+    (the reference's last tabulated phasor, the fitted mean step, the linear magnitude
     by renorm position). Not the reference: its residual is measured and bounded here
     at 2^18 outputs past a 2^18 budget (DESIGN.md §3 lists it per configuration)."""
     import orion_sdr

@@ -97,7 +97,7 @@ def test_rotator_cycle_2_24(gpu_lib, oracle):
 @pytest.mark.parametrize("f,fs", [(1.234e6, 10e6), (1500.0, 48e3)])
 def test_rotator_past_the_table(gpu_lib, oracle, f, fs):
     """A recurrence that closes no cycle within the budget (2^20): bit-exact for the
-    tabulated outputs, then the drift model (fitted mean step, magnitude profile). The
+    tabulated outputs, then the drift model (fitted mean step, linear magnitude). The
     residual past the table is the reference's own random walk; measured and bounded
     (DESIGN.md §3 lists the values)."""
     n = (1 << 20) + (1 << 19)
