@@ -1,5 +1,6 @@
 // k_scan.hip — chunked state-carry scan kernels (see scan.hpp) for gfx950.
 #include <cstdlib>
+#include <type_traits>
 
 #include "scan.hpp"
 
@@ -32,6 +33,12 @@ constexpr int PADN = CH + CH / 16 + 16;
 #endif
 #ifndef ORION_SCAN_SP_MINW
 #define ORION_SCAN_SP_MINW 4  // waves per SIMD k_scan_sp is compiled for (4: <= 128 VGPRs, spills 52-132 B)
+#endif
+#ifndef ORION_SP_MPOW
+#define ORION_SP_MPOW 1  // k_lpdc_sp DC pass: lane-level warm-up test, r^v by squaring (0: per-sample guards and product, A/B)
+#endif
+#ifndef ORION_SP_FAST
+#define ORION_SP_FAST 1  // k_lpdc_sp: unguarded per-sample loops in full, non-final chunks (0: always guarded, A/B)
 #endif
 #ifndef ORION_SP_TRUNC
 #define ORION_SP_TRUNC 1  // k_lpdc_sp: the LP4 lane scan truncated to the forgetting horizon (0: full two-scan form)
@@ -496,7 +503,7 @@ __device__ __forceinline__ void dc_combine(double m1, double d1, double& m2, dou
 // BFO's output k0 + base + e: the reference's from its table, or in the drift model
 // (S mtab[64 SC w + l]) mtab[64 k] scaled by the linear magnitude model.
 template <int SC>
-__device__ __forceinline__ int posS(int e) { return e + e / SC; }
+__device__ __forceinline__ int posS(int e) { return e + static_cast<int>(static_cast<unsigned>(e) / SC); }
 __device__ __forceinline__ void wave_order() { asm volatile("" ::: "memory"); }
 template <Pre PR, int SC>
 __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long base, int cnt, float* sb) {
@@ -603,6 +610,12 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
   }
 
   // ---- LP4: zero-state lane aggregates, block scan, exact re-run ----
+  // Guards on the element range: the lane's valid samples are i < hi (the staged samples
+  // past cnt are zeros); `fast` (block-uniform: a full chunk that is not the call's last)
+  // selects unguarded copies of the per-sample loops — not for Ssb, whose kernel (three
+  // phasor forms in its staging) measured 5 % slower with the copies (r4_lpdc_guard_ab.txt).
+  const int hi = min(cnt - t * C, C);
+  const bool fast = ORION_SP_FAST && PR != Pre::Ssb && cnt == CH && !last;
   float xs[C];
 #pragma unroll
   for (int i = 0; i < C; ++i) xs[i] = sb[posS<SC>(t * C + i)];
@@ -614,11 +627,9 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
   {  // the lane run's zero-state end state as the linear map (k_scan_sp)
     const float* __restrict__ E = a.zmap;
 #pragma unroll
-    for (int i = 0; i < C; ++i) {
-      const float xv = t * C + i < cnt ? xs[i] : 0.0f;
+    for (int i = 0; i < C; ++i)
 #pragma unroll
-      for (int k = 0; k < S; ++k) s0[k] = __builtin_fmaf(E[i * S + k], xv, s0[k]);
-    }
+      for (int k = 0; k < S; ++k) s0[k] = __builtin_fmaf(E[i * S + k], xs[i], s0[k]);  // zeros past cnt (staging)
   }
 #else
 #pragma unroll
@@ -693,12 +704,16 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
 #endif
 #pragma unroll
   for (int i = 0; i < S; ++i) ef[i] = static_cast<float>(e[i]);
+  auto lp_rerun = [&](auto guarded) {
 #pragma unroll
-  for (int i = 0; i < C; ++i)
-    if (t * C + i < cnt) {
-      xs[i] = lp.step(ef, xs[i]);  // LP output x (f32, reference update)
-      if constexpr (PR == Pre::AmSqrt || PR == Pre::RealLpSqrt) xs[i] = sqrtf(xs[i]);  // process_mapped(.., f32::sqrt)
-    }
+    for (int i = 0; i < C; ++i)
+      if (!decltype(guarded)::value || i < hi) {
+        xs[i] = lp.step(ef, xs[i]);  // LP output x (f32, reference update)
+        if constexpr (PR == Pre::AmSqrt || PR == Pre::RealLpSqrt) xs[i] = sqrtf(xs[i]);  // process_mapped(.., f32::sqrt)
+      }
+  };
+  if (fast) lp_rerun(std::false_type{});
+  else lp_rerun(std::true_type{});
   wave_order();  // (the wave's own inputs: read before they are overwritten, in order)
 #pragma unroll
   for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
@@ -717,6 +732,33 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
   if constexpr (!LP)
     if (t == 0 && c > 0) xprev0 = static_cast<const float*>(a.x)[ch * a.x_stride + base - 1];
   double m = 1.0, d = 0.0;
+  // the warm-up is a whole number of lane runs: a lane is inside it or past it
+  const bool lane_on = t * C >= warm;
+#if ORION_SP_MPOW
+  {
+    float y = 0.0f;
+    auto dc_zero = [&](auto guarded) {
+      float xp = xprev0;
+#pragma unroll
+      for (int i = 0; i < C; ++i) {
+        if (!decltype(guarded)::value || i < hi) y = (xs[i] - xp) + r * y;
+        xp = xs[i];
+      }
+    };
+    if (fast) dc_zero(std::false_type{});
+    else dc_zero(std::true_type{});
+    d = lane_on ? static_cast<double>(y) : 0.0;
+    // r^v over the lane's v valid samples by squaring (equal to the running product to
+    // f64 rounding, ~1e-15 relative: far below the f32 outputs)
+    const int v = lane_on ? max(hi, 0) : 0;
+    double p = static_cast<double>(r);
+#pragma unroll
+    for (int b = 1; b <= C; b <<= 1) {
+      if (v & b) m *= p;
+      p *= p;
+    }
+  }
+#else
   {
     float xp = xprev0, y = 0.0f;
 #pragma unroll
@@ -730,6 +772,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
     }
     d = y;
   }
+#endif
   // inclusive scan of (m, d) over the wave, then over the waves
   double mi = m, di = d;
 #pragma unroll
@@ -846,20 +889,21 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
   }
   dc_combine(wm, wd, em, ed);  // waves before, then lanes before
   float y = static_cast<float>(__builtin_fma(em, excl_sh, ed));
-  {
+  auto dc_rerun = [&](auto guarded) {  // (warm-up lanes' outputs are not stored)
     float xp = xprev0;
 #pragma unroll
     for (int i = 0; i < C; ++i) {
-      const int ei = t * C + i;
       float out = 0.0f;
-      if (ei >= warm && ei < cnt) {
+      if (!decltype(guarded)::value || (ORION_SP_MPOW ? i < hi : (t * C + i >= warm && t * C + i < cnt))) {
         y = (xs[i] - xp) + r * y;  // dsp/iir.rs:161 (y1 - dc_x1) + r * dc_y1
         out = y;
       }
       xp = xs[i];
       xs[i] = out;
     }
-  }
+  };
+  if (fast) dc_rerun(std::false_type{});
+  else dc_rerun(std::true_type{});
   if (last && t * C <= cnt - 1 && cnt - 1 < t * C + C) {  // carried state of the next call
     float* co = a.carry_out + ch * kScanCarry;
     if constexpr (LP)
@@ -880,8 +924,13 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
   for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
   wave_order();
   float* yo = static_cast<float*>(a.y) + ch * a.y_stride + o0;
-  {
-    const int e0 = wave * (64 * SC) + lane;
+  const int e0 = wave * (64 * SC) + lane;
+  if (fast) {
+    const int kmin = (warm - wave * (64 * SC)) >> 6;  // wave-uniform: the warm-up is whole rows of 64
+#pragma unroll
+    for (int k = 0; k < SC; ++k)
+      if (k >= kmin) yo[e0 + 64 * k - warm] = sb[posS<SC>(e0 + 64 * k)];
+  } else {
 #pragma unroll
     for (int k = 0; k < SC; ++k) {
       const int e2 = e0 + 64 * k;
@@ -984,6 +1033,9 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
     return;
   }
 
+  // `fast` (block-uniform: a full chunk that is not the call's last) selects unguarded
+  // copies of the per-sample loops (as k_lpdc_sp)
+  const bool fast = ORION_SP_FAST && cnt == CH && !last;
   float xs[C];
 #pragma unroll
   for (int i = 0; i < C; ++i) xs[i] = sb[posS<SC>(t * C + i)];
@@ -997,12 +1049,16 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
     // chunk enter as zeros: only the last partial lane differs, whose state reaches no
     // valid output)
     const float* __restrict__ E = a.zmap;
+    auto zs = [&](auto guarded) {
 #pragma unroll
-    for (int i = 0; i < C; ++i) {
-      const float xv = t * C + i < cnt ? xs[i] : 0.0f;
+      for (int i = 0; i < C; ++i) {
+        const float xv = !decltype(guarded)::value || t * C + i < cnt ? xs[i] : 0.0f;
 #pragma unroll
-      for (int k = 0; k < S; ++k) s0[k] = __builtin_fmaf(E[i * S + k], xv, s0[k]);
-    }
+        for (int k = 0; k < S; ++k) s0[k] = __builtin_fmaf(E[i * S + k], xv, s0[k]);
+      }
+    };
+    if (fast) zs(std::false_type{});
+    else zs(std::true_type{});
   } else {
 #pragma unroll
     for (int i = 0; i < C; ++i)
@@ -1104,9 +1160,14 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
     ef[i] = static_cast<float>(lane == 0 ? cw[i] : o);
   }
   }  // TR
+  auto rerun = [&](auto guarded) {
 #pragma unroll
-  for (int i = 0; i < C; ++i)
-    if (!(ORION_SP_ABL & 128) && t * C + i < cnt) xs[i] = postmap<PO>(a, rr.step(ef, xs[i]));  // the reference's f32 update
+    for (int i = 0; i < C; ++i)
+      if (!(ORION_SP_ABL & 128) && (!decltype(guarded)::value || t * C + i < cnt))
+        xs[i] = postmap<PO>(a, rr.step(ef, xs[i]));  // the reference's f32 update
+  };
+  if (fast) rerun(std::false_type{});
+  else rerun(std::true_type{});
   if (last && t * C <= cnt - 1 && cnt - 1 < t * C + C) {  // carried state of the next call
     float* co = a.carry_out + ch * kScanCarry;
 #pragma unroll
@@ -1127,7 +1188,12 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
   __syncthreads();
   float* y = static_cast<float*>(a.y) + ch * a.y_stride + base;
-  for (int e2 = t; e2 < cnt; e2 += NT) y[e2] = sb[posS<SC>(e2)];
+  if (fast) {
+#pragma unroll
+    for (int k = 0; k < SC; ++k) y[t + k * NT] = sb[posS<SC>(t + k * NT)];
+  } else {
+    for (int e2 = t; e2 < cnt; e2 += NT) y[e2] = sb[posS<SC>(e2)];
+  }
 }
 
 // SsbPhasingMod in one pass (modulate/ssb.rs:43-114): per chunk, the audio-NCO
