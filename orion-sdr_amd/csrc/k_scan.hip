@@ -986,6 +986,10 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   // (an L1/L2 hit; the neighbour form measured 6 % slower there: more spills)
   constexpr bool kPair = PR == Pre::Fm, kPrev = PR == Pre::Pm;
   const long long nl = a.n - 1;
+  // a full chunk that is not the call's last: no index clamps, no store guards (below)
+  const bool fast = ORION_SP_FAST && cnt == CH && !last;
+  auto stage = [&](auto guarded) {
+  constexpr bool G = decltype(guarded)::value;
 #pragma unroll 1
   for (int k0 = 0; k0 < SC; k0 += BT) {
     f2 z[BT], zp[BT], zq = f2{0.0f, 0.0f};
@@ -993,11 +997,11 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
     for (int j = 0; j < BT; ++j) {
       const long long i = base + t + (k0 + j) * NT;
       if constexpr (PR == Pre::Real) {
-        z[j] = f2{static_cast<const float*>(a.x)[ch * a.x_stride + min(i, nl)], 0.0f};
+        z[j] = f2{static_cast<const float*>(a.x)[ch * a.x_stride + (G ? min(i, nl) : i)], 0.0f};
       } else {
         const f2* __restrict__ xc = static_cast<const f2*>(a.x) + ch * a.x_stride;
-        z[j] = xc[min(i, nl)];
-        zp[j] = kPrev ? xc[max(min(i - 1, nl), 0LL)] : z[j];
+        z[j] = xc[G ? min(i, nl) : i];
+        zp[j] = kPrev ? xc[G || c == 0 ? max(min(i - 1, nl), 0LL) : i - 1] : z[j];
       }
     }
     if constexpr (kPair) {
@@ -1023,9 +1027,12 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
       } else {
         o = premap_v<PR>(a, ch, base + e, base, Ro, z[j], zp[j]);
       }
-      if (e < cnt) sb[posS<SC>(e)] = o;
+      if (!G || e < cnt) sb[posS<SC>(e)] = o;
     }
   }
+  };
+  if (fast) stage(std::false_type{});
+  else stage(std::true_type{});
   __syncthreads();
   if constexpr ((ORION_SP_ABL & 32) != 0) {  // timing floor: staging and stores only
     float* y = static_cast<float*>(a.y) + ch * a.y_stride + base;
@@ -1035,7 +1042,6 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
 
   // `fast` (block-uniform: a full chunk that is not the call's last) selects unguarded
   // copies of the per-sample loops (as k_lpdc_sp)
-  const bool fast = ORION_SP_FAST && cnt == CH && !last;
   float xs[C];
 #pragma unroll
   for (int i = 0; i < C; ++i) xs[i] = sb[posS<SC>(t * C + i)];
