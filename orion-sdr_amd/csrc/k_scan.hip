@@ -1227,23 +1227,29 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
   // staging and of the stores): the audio and RF Rotators' cursors over the chunk.
   const OscRun Ra = osc_run(aud, k0 + static_cast<uint64_t>(base), cnt);
   const OscRun Rr = osc_run(rf, k0 + static_cast<uint64_t>(base), cnt);
-  {  // stage: x p.re, x p.im (ssb.rs:53-54), coalesced loads first (unconditional, clamped)
+  // `fast` (block-uniform: a full chunk that is not the call's last): unguarded copies of
+  // the per-sample loops (as k_lpdc_sp)
+  const bool fast = ORION_SP_FAST && cnt == CH && !last;
+  auto stage = [&](auto guarded) {  // x p.re, x p.im (ssb.rs:53-54), coalesced loads first
+    constexpr bool G = decltype(guarded)::value;
     float v[C];
     f2 pa[C];  // the audio phasor reads (unconditional: the table is padded past a run)
 #pragma unroll
     for (int k = 0; k < C; ++k) {
-      v[k] = x[min(base + t + k * NT, n - 1)];
+      v[k] = x[G ? min(base + t + k * NT, n - 1) : base + t + k * NT];
       pa[k] = osc_ld(aud, Ra, t + k * NT);
     }
 #pragma unroll
     for (int k = 0; k < C; ++k) {
       const int e = t + k * NT;
-      const float xv = e < cnt ? v[k] : 0.0f;
-      const f2 p = e < cnt ? osc_fin(aud, Ra, e, pa[k]) : f2{1.0f, 0.0f};
+      const float xv = !G || e < cnt ? v[k] : 0.0f;  // zeros past cnt (the zero-state map below)
+      const f2 p = !G || e < cnt ? osc_fin(aud, Ra, e, pa[k]) : f2{1.0f, 0.0f};
       sb[0][pos(e)] = xv * p.x;
       sb[1][pos(e)] = xv * p.y;
     }
-  }
+  };
+  if (fast) stage(std::false_type{});
+  else stage(std::true_type{});
   __syncthreads();
   float xs[2][C];
   float s0[2][S];
@@ -1260,11 +1266,9 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
     for (int k = 0; k < S; ++k) s0[b][k] = 0.0f;
 #if ORION_SP_ZMAP
 #pragma unroll
-    for (int i = 0; i < C; ++i) {  // the lane run's zero-state end state as the linear map (k_scan_sp)
-      const float xv = t * C + i < cnt ? xs[b][i] : 0.0f;
+    for (int i = 0; i < C; ++i)  // the lane run's zero-state end state as the linear map (k_scan_sp)
 #pragma unroll
-      for (int k = 0; k < S; ++k) s0[b][k] = __builtin_fmaf(zmap[i * S + k], xv, s0[b][k]);
-    }
+      for (int k = 0; k < S; ++k) s0[b][k] = __builtin_fmaf(zmap[i * S + k], xs[b][i], s0[b][k]);  // staged zeros past cnt
 #else
 #pragma unroll
     for (int i = 0; i < C; ++i)
@@ -1334,9 +1338,13 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
       ef[k] = static_cast<float>(lane == 0 ? cw[k] : o);
     }
 #endif
+    auto rerun = [&](auto guarded) {
 #pragma unroll
-    for (int i = 0; i < C; ++i)
-      if (t * C + i < cnt) xs[b][i] = lp.step(ef, xs[b][i]);  // ssb.rs:53-54 LpCascade outputs
+      for (int i = 0; i < C; ++i)
+        if (!decltype(guarded)::value || t * C + i < cnt) xs[b][i] = lp.step(ef, xs[b][i]);  // ssb.rs:53-54 LpCascade outputs
+    };
+    if (fast) rerun(std::false_type{});
+    else rerun(std::true_type{});
     if (last && t * C <= cnt - 1 && cnt - 1 < t * C + C)  // the next call's state
 #pragma unroll
       for (int k = 0; k < S; ++k) carry_out[4 * b + k] = ef[k];
@@ -1353,10 +1361,19 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
   f2 pr[C];  // the RF phasor reads, all issued before the first store
 #pragma unroll
   for (int k = 0; k < C; ++k) pr[k] = osc_ld(rf, Rr, t + k * NT);
+  static_assert(kSpWarm % NT == 0, "the warm-up is whole rows of the store order");
+  if (fast) {
 #pragma unroll
-  for (int k = 0; k < C; ++k) {  // ssb.rs:55-60
-    const int e = t + k * NT;
-    if (e >= warm && e < cnt) y[base + e] = cmul_rot(zs[e + (e >> 4)], osc_fin(rf, Rr, e, pr[k]));
+    for (int k = 0; k < C; ++k) {  // ssb.rs:55-60
+      const int e = t + k * NT;
+      if (k * NT >= warm) y[base + e] = cmul_rot(zs[e + (e >> 4)], osc_fin(rf, Rr, e, pr[k]));
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < C; ++k) {  // ssb.rs:55-60
+      const int e = t + k * NT;
+      if (e >= warm && e < cnt) y[base + e] = cmul_rot(zs[e + (e >> 4)], osc_fin(rf, Rr, e, pr[k]));
+    }
   }
 }
 
