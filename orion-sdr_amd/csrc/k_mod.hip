@@ -134,6 +134,9 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_back(const float* __restrict__ v
 #ifndef ORION_FM_G
 #define ORION_FM_G 8  // RF phasor reads per thread issued together
 #endif
+#ifndef ORION_FM_FAST
+#define ORION_FM_FAST 1  // k_fm_mod_sp: full chunks without per-sample tests (0: always tested, A/B)
+#endif
 #ifndef ORION_FM_MINW
 #define ORION_FM_MINW 1  // waves per SIMD k_fm_mod_sp is compiled for (A/B: 5 = 96 VGPRs)
 #endif
@@ -144,12 +147,14 @@ struct FmPairs {
 };
 // The thread's pairs (fm.rs:50-51) and the Q0.64 sum of their angles; samples past n
 // (valid < kFmC) are pairs (1, 0).
+// FULL: every thread's kFmC samples are valid (no per-sample test).
+template <bool FULL = false>
 __device__ __forceinline__ uint64_t fm_pairs(float kf, const float* __restrict__ xs, int valid, FmPairs& p) {
   double pr = 1.0, pi = 0.0;
 #pragma unroll
   for (int k = 0; k < kFmC; ++k) {
     float sn = 0.0f, cs = 1.0f;
-    if (k < valid) sincos_cr(kf * xs[k], &sn, &cs);  // fm.rs:50-51
+    if (FULL || k < valid) sincos_cr(kf * xs[k], &sn, &cs);  // fm.rs:50-51
     p.c[k] = cs;
     p.s[k] = sn;
     const double c = cs, s = sn;
@@ -169,6 +174,7 @@ __device__ __forceinline__ uint64_t fm_pairs(float kf, const float* __restrict__
 // consecutive samples would touch 64 cache lines per wave instruction). ys aliases
 // the input staging: every thread is past its reads of it (the caller's barrier).
 constexpr int kFmYs = kFmCH + kFmCH / 16;  // f2 slots
+template <bool FULL = false>
 __device__ __forceinline__ void fm_out(const FmPairs& p, uint64_t ph, float gain, const OscDev& o, uint64_t k0,
                                        f2* ys, f2* __restrict__ y, long long base, long long n) {
   const OscRun R = osc_run(o, k0 + static_cast<uint64_t>(base), kFmCH);  // RF Nco outputs of the chunk
@@ -199,7 +205,7 @@ __device__ __forceinline__ void fm_out(const FmPairs& p, uint64_t ph, float gain
       const int e = t + NT * (g + m);
       const f2 bz = ys[e + (e >> 4)];
       const f2 r = (ORION_FM_ABL & 2) ? rp[m] : osc_fin(o, R, e, rp[m]);
-      if (full || base + e < n) y[base + e] = f2{bz.x * r.x - bz.y * r.y, bz.x * r.y + bz.y * r.x};  // nco.rs:65
+      if (FULL || full || base + e < n) y[base + e] = f2{bz.x * r.x - bz.y * r.y, bz.x * r.y + bz.y * r.x};  // nco.rs:65
     }
   }
 }
@@ -233,14 +239,15 @@ __device__ __forceinline__ uint64_t wg_scan_u64(uint64_t v, uint64_t* tot, uint6
 // The loads are unconditional (index clamped to n - 1, n >= 1): all 16 in flight at
 // once. A guarded load per sample compiles to a branch around each, and each then
 // waits for its own load before the LDS store (16 serial memory latencies per chunk).
+template <bool FULL = false>
 __device__ __forceinline__ int fm_stage(const float* __restrict__ x, long long n, long long base, float* xs) {
   float v[kFmC];
 #pragma unroll
-  for (int k = 0; k < kFmC; ++k) v[k] = x[min(base + threadIdx.x + k * NT, n - 1)];
+  for (int k = 0; k < kFmC; ++k) v[k] = x[FULL ? base + threadIdx.x + k * NT : min(base + threadIdx.x + k * NT, n - 1)];
 #pragma unroll
   for (int k = 0; k < kFmC; ++k) {
     const int e = threadIdx.x + k * NT;
-    xs[e + (e >> 4)] = base + e < n ? v[k] : 0.0f;
+    xs[e + (e >> 4)] = FULL || base + e < n ? v[k] : 0.0f;
   }
   __syncthreads();
   const long long i0 = base + static_cast<long long>(threadIdx.x) * kFmC;
@@ -337,10 +344,18 @@ __global__ __launch_bounds__(NT, ORION_FM_MINW) void k_fm_mod_sp(const float* __
   const int nchunk = static_cast<int>((n + kFmCH - 1) / kFmCH);
   const bool last = c == nchunk - 1;
   const long long base = static_cast<long long>(c) * kFmCH;
-  const int valid = fm_stage(x, n, base, xs);
+  // a full chunk (not the call's last): the staging, pairs and stores without per-sample tests
+  const bool fast = ORION_FM_FAST && !last;
   FmPairs p;
   const int e = t * kFmC;
-  const uint64_t q = fm_pairs(kf, xs + e + (e >> 4), valid, p);
+  uint64_t q;
+  if (fast) {
+    (void)fm_stage<true>(x, n, base, xs);
+    q = fm_pairs<true>(kf, xs + e + (e >> 4), kFmC, p);
+  } else {
+    const int valid = fm_stage(x, n, base, xs);
+    q = fm_pairs(kf, xs + e + (e >> 4), valid, p);
+  }
   uint64_t agg;
   const uint64_t before = wg_scan_u64(q, tot, agg);
   if (w == 0) {
@@ -422,7 +437,8 @@ __global__ __launch_bounds__(NT, ORION_FM_MINW) void k_fm_mod_sp(const float* __
     }
   }
   __syncthreads();
-  fm_out(p, excl_sh + before, gain, o, k0, ys, y, base, n);
+  if (fast) fm_out<true>(p, excl_sh + before, gain, o, k0, ys, y, base, n);
+  else fm_out(p, excl_sh + before, gain, o, k0, ys, y, base, n);
 }
 
 }  // namespace
