@@ -40,6 +40,10 @@ constexpr int PADN = CH + CH / 16 + 16;
 #ifndef ORION_SP_FAST
 #define ORION_SP_FAST 1  // k_lpdc_sp: unguarded per-sample loops in full, non-final chunks (0: always guarded, A/B)
 #endif
+#ifndef ORION_SP_SSBMASK
+#define ORION_SP_SSBMASK 6  // k_lpdc_sp Ssb: which loops take the unguarded copies (1 LP re-run, 2 DC zero-state,
+                            // 4 DC re-run, 8 stores); 6 measured best (r4_lpdc_guard_ab.txt), 1 and 8 slower
+#endif
 #ifndef ORION_SP_TRUNC
 #define ORION_SP_TRUNC 1  // k_lpdc_sp: the LP4 lane scan truncated to the forgetting horizon (0: full two-scan form)
 #endif
@@ -612,10 +616,14 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
   // ---- LP4: zero-state lane aggregates, block scan, exact re-run ----
   // Guards on the element range: the lane's valid samples are i < hi (the staged samples
   // past cnt are zeros); `fast` (block-uniform: a full chunk that is not the call's last)
-  // selects unguarded copies of the per-sample loops — not for Ssb, whose kernel (three
-  // phasor forms in its staging) measured 5 % slower with the copies (r4_lpdc_guard_ab.txt).
+  // selects unguarded copies of the per-sample loops — for Ssb (three phasor forms in its
+  // staging) only the DC loops': its LP4 re-run and store copies measured slower
+  // (r4_lpdc_guard_ab.txt).
   const int hi = min(cnt - t * C, C);
-  const bool fast = ORION_SP_FAST && PR != Pre::Ssb && cnt == CH && !last;
+  const bool full_nl = ORION_SP_FAST && cnt == CH && !last;
+  const bool fast = PR != Pre::Ssb && full_nl;
+  // per loop for Ssb (A/B mask): 1 LP re-run, 2 DC zero-state, 4 DC re-run, 8 stores
+  auto fast_for = [&](int bit) { return PR == Pre::Ssb ? ((ORION_SP_SSBMASK & bit) != 0 && full_nl) : fast; };
   float xs[C];
 #pragma unroll
   for (int i = 0; i < C; ++i) xs[i] = sb[posS<SC>(t * C + i)];
@@ -712,7 +720,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
         if constexpr (PR == Pre::AmSqrt || PR == Pre::RealLpSqrt) xs[i] = sqrtf(xs[i]);  // process_mapped(.., f32::sqrt)
       }
   };
-  if (fast) lp_rerun(std::false_type{});
+  if (fast_for(1)) lp_rerun(std::false_type{});
   else lp_rerun(std::true_type{});
   wave_order();  // (the wave's own inputs: read before they are overwritten, in order)
 #pragma unroll
@@ -745,7 +753,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
         xp = xs[i];
       }
     };
-    if (fast) dc_zero(std::false_type{});
+    if (fast_for(2)) dc_zero(std::false_type{});
     else dc_zero(std::true_type{});
     d = lane_on ? static_cast<double>(y) : 0.0;
     // r^v over the lane's v valid samples by squaring (equal to the running product to
@@ -902,7 +910,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
       xs[i] = out;
     }
   };
-  if (fast) dc_rerun(std::false_type{});
+  if (fast_for(4)) dc_rerun(std::false_type{});
   else dc_rerun(std::true_type{});
   if (last && t * C <= cnt - 1 && cnt - 1 < t * C + C) {  // carried state of the next call
     float* co = a.carry_out + ch * kScanCarry;
@@ -925,7 +933,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
   wave_order();
   float* yo = static_cast<float*>(a.y) + ch * a.y_stride + o0;
   const int e0 = wave * (64 * SC) + lane;
-  if (fast) {
+  if (fast_for(8)) {
     const int kmin = (warm - wave * (64 * SC)) >> 6;  // wave-uniform: the warm-up is whole rows of 64
 #pragma unroll
     for (int k = 0; k < SC; ++k)
