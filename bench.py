@@ -58,23 +58,53 @@ def _sum_sin(w, k):
     return np.sin(w * (k - 1) / 2) * np.sin(w * k / 2) / np.sin(w / 2) if k > 0 else 0.0
 
 
+_M64 = (1 << 64) - 1
+
+
+def _s64(v):
+    """An unsigned 64-bit constant as the int64 with the same bits."""
+    v &= _M64
+    return v - (1 << 64) if v >> 63 else v
+
+
+def _srl(z, k):
+    """Logical right shift of an int64 tensor."""
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+def index_noise(idx, seed):
+    """Complex Gaussian noise (E|w|^2 = 1) as a pure function of the absolute sample
+    index: splitmix64 of (seed, index) -> two 24-bit uniforms -> Box-Muller. Any slice
+    of a stream gets the same samples whichever rank generates it, so the time shards
+    of --shard stream (halos included) are one stream's data."""
+    z = idx * _s64(0x9E3779B97F4A7C15) + _s64(seed * 0xD1B54A32D192ED03)
+    z = (z ^ _srl(z, 30)) * _s64(0xBF58476D1CE4E5B9)
+    z = (z ^ _srl(z, 27)) * _s64(0x94D049BB133111EB)
+    z = z ^ _srl(z, 31)
+    u1 = (_srl(z, 40) + 1).to(torch.float64) * 2.0 ** -24  # (0, 1]
+    u2 = (z & 0xFFFFFF).to(torch.float64) * 2.0 ** -24
+    del z
+    r = torch.sqrt(-torch.log(u1))  # sqrt(-2 ln u1) / sqrt(2): unit power over re + im
+    return torch.polar(r, 2 * np.pi * u2).to(torch.complex64)
+
+
 def wbfm_iq(n, f_off, dev, seed, fs=10e6, t0=0, noise=0.0025):
     """C2 synthetic IQ generated on the device: FM (dev 75 kHz) of
     0.5 sin(1 kHz) + 0.3 sin(7 kHz) at +f_off, plus complex AWGN (P = 0.0025).
     t0: index of the first sample within the stream (a time shard of it; the
-    FM phase accumulated before t0 is added in closed form)."""
-    t = (torch.arange(n, device=dev, dtype=torch.float64) + t0) / fs
+    FM phase accumulated before t0 is added in closed form, the noise is a function
+    of the absolute index)."""
+    idx = torch.arange(n, device=dev, dtype=torch.int64) + t0
+    t = idx.to(torch.float64) / fs
     aud = 0.5 * torch.sin(2 * np.pi * 1e3 * t) + 0.3 * torch.sin(2 * np.pi * 7e3 * t)
     k = 2 * np.pi * 75e3 / fs
     ph0 = k * (0.5 * _sum_sin(2 * np.pi * 1e3 / fs, t0) + 0.3 * _sum_sin(2 * np.pi * 7e3 / fs, t0))
     ph = torch.cumsum(k * aud, 0) + ph0 + 2 * np.pi * f_off * t
     del aud
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
     x = torch.polar(torch.ones_like(ph), ph).to(torch.complex64)
     del ph, t
     if noise > 0:
-        x += (torch.randn(n, dtype=torch.complex64, device=dev, generator=g) * np.sqrt(noise)).to(torch.complex64)
+        x += index_noise(idx, seed) * np.float32(np.sqrt(noise))
     return x
 
 
@@ -137,7 +167,7 @@ def make_workload(cfg, rank, dev, n_override=None, world=1, shard="stream"):
         n = n_override or (1 << 26)
         start, stop, h = orion_sdr.stream_shard(world * n, rank, world)
         blk = orion_sdr.WbfmChain(f_off=OFFSETS[0]).seek(h)
-        x = wbfm_iq(stop - h, OFFSETS[0], dev, 0x1234 + rank, t0=h)
+        x = wbfm_iq(stop - h, OFFSETS[0], dev, 0x1234, t0=h)  # one stream: the same seed on every rank
         desc = dict(workload="C2 WBFM chain on ONE stream cut in time: Rotator(-f_off) -> FirDecimator(10e6, 8, "
                     "200e3, 79e3; 127 taps) -> FmQuadratureDemod(1.25e6, 75e3, 15e3) -> FirLowpass(1.25e6, 15e3, "
                     "10e3; 125 taps)", fs_hz=10e6, stream_samples=world * n, samples_per_step_per_gpu=stop - start,
@@ -327,6 +357,9 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.gpus != world:  # one process per GPU: N > 1 needs the launcher (torch.distributed.run)
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N > 1 as "
+                         f"python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
@@ -378,6 +411,8 @@ def main():
         "metric": METRICS.get(args.config, METRIC), "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        **({"audio_fir": "f16 hi+lo MFMA (v_mfma_f32_16x16x32_f16, per-sub-range scale), f32 accumulate"}
+           if args.config in ("c2", "c4") else {}),
         "config": dict(desc, parallelism=(f"stream time-sharded x{world} (halo {orion_sdr.STREAM_HALO} samples), no "
                                           "data-path collective" if "halo_samples" in desc
                                           else f"channel-sharded x{world}, no data-path collective")),

@@ -4,13 +4,17 @@
 #include "osc.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <tuple>
+#include <vector>
 
 namespace orion {
 
@@ -93,19 +97,115 @@ int device_cus() {
 }
 
 // ---------------------------------------------------------- host path ----
-constexpr size_t kPinBytes = 8u << 20;        // one pinned staging buffer (two per direction)
+constexpr size_t kPinBytes = 8u << 20;        // one pinned staging buffer at most (two per direction)
 constexpr size_t kPipeSamples = 1u << 20;     // calls of >= 2 kPipeSamples take the chunked pipeline
+constexpr size_t kDirectBytes = 1u << 20;     // pageable copies up to this size go straight to hipMemcpy
 
+// Parallel memcpy for the pageable staging copies (pageable <-> pinned): one process-wide
+// pool of host threads; a copy is cut into >= 1 MiB pieces that the workers and the
+// caller take in turn. One thread copies ~20 GB/s, a third of the H2D link (VERDICT r4
+// weak 4); a few in parallel keep the copy ahead of the DMA.
+class CopyPool {
+ public:
+  static CopyPool& get() {
+    static CopyPool p;
+    return p;
+  }
+  void copy(void* dst, const void* src, size_t bytes) {
+    constexpr size_t kPiece = 1u << 20;
+    if (bytes < 2 * kPiece || th_.empty()) {
+      std::memcpy(dst, src, bytes);
+      return;
+    }
+    std::lock_guard<std::mutex> one(job_mu_);  // one job at a time
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      dst_ = static_cast<char*>(dst);
+      src_ = static_cast<const char*>(src);
+      bytes_ = bytes;
+      pieces_ = std::min<size_t>((bytes + kPiece - 1) / kPiece, 4 * (th_.size() + 1));
+      next_.store(0);
+      done_.store(0);
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [&] { return done_.load() == pieces_; });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+
+ private:
+  CopyPool() {
+    const unsigned hw = std::thread::hardware_concurrency();
+    const unsigned n = std::min(7u, hw > 2 ? hw / 2 - 1 : 0u);  // workers besides the caller
+    for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  void work() {  // take pieces until none is left
+    for (;;) {
+      const size_t i = next_.fetch_add(1);
+      if (i >= pieces_) return;
+      const size_t per = (bytes_ / pieces_ + 63) & ~size_t(63);
+      const size_t off = std::min(bytes_, i * per), len = std::min(per, bytes_ - off);
+      std::memcpy(dst_ + off, src_ + off, len);
+      if (done_.fetch_add(1) + 1 == pieces_) {
+        std::lock_guard<std::mutex> g(mu_);
+        done_cv_.notify_all();
+      }
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_, job_mu_;
+  std::condition_variable cv_, done_cv_;
+  char* dst_ = nullptr;
+  const char* src_ = nullptr;
+  size_t bytes_ = 0, pieces_ = 0;
+  std::atomic<size_t> next_{0}, done_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+void par_copy(void* dst, const void* src, size_t bytes) { CopyPool::get().copy(dst, src, bytes); }
+
+// Created on a handle's first call that needs it (pageable memory above kDirectBytes, or
+// the chunked pipeline); the pinned buffers are sized to the calls (kPinBytes at most).
 struct Block::HostPipe {
   hipStream_t s_in = nullptr, s_out = nullptr;
   void* pin_in[2] = {nullptr, nullptr};
   void* pin_out[2] = {nullptr, nullptr};
+  size_t pin_bytes = 0;
   hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr}, ev_k[2] = {nullptr, nullptr};
   DevBuf din[2], dout[2];
-  ~HostPipe() {
+  HostPipe() {
+    ORION_HIP(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking));
+    ORION_HIP(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking));
     for (int b = 0; b < 2; ++b) {
-      if (pin_in[b]) (void)hipHostFree(pin_in[b]);
-      if (pin_out[b]) (void)hipHostFree(pin_out[b]);
+      ORION_HIP(hipEventCreateWithFlags(&ev_in[b], hipEventDisableTiming));
+      ORION_HIP(hipEventCreateWithFlags(&ev_out[b], hipEventDisableTiming));
+      ORION_HIP(hipEventCreateWithFlags(&ev_k[b], hipEventDisableTiming));
+    }
+  }
+  ~HostPipe() {
+    free_pins();
+    for (int b = 0; b < 2; ++b) {
       if (ev_in[b]) (void)hipEventDestroy(ev_in[b]);
       if (ev_out[b]) (void)hipEventDestroy(ev_out[b]);
       if (ev_k[b]) (void)hipEventDestroy(ev_k[b]);
@@ -113,51 +213,58 @@ struct Block::HostPipe {
     if (s_in) (void)hipStreamDestroy(s_in);
     if (s_out) (void)hipStreamDestroy(s_out);
   }
-  // host -> device on stream s: DMA from pinned memory directly, else through the two
-  // pinned buffers (the CPU copy of chunk c + 1 overlaps the DMA of chunk c).
-  void h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
-    if (!bytes) return;
-    if (host_is_pinned(src)) {
-      ORION_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
-      return;
+  void free_pins() {
+    for (int b = 0; b < 2; ++b) {
+      if (pin_in[b]) (void)hipHostFree(pin_in[b]);
+      if (pin_out[b]) (void)hipHostFree(pin_out[b]);
+      pin_in[b] = pin_out[b] = nullptr;
     }
-    for (size_t off = 0, c = 0; off < bytes; off += kPinBytes, ++c) {
+    pin_bytes = 0;
+  }
+  // Called at the start of a host call (no copy of this pipe is in flight then).
+  void pins(size_t bytes) {
+    bytes = std::min(kPinBytes, (bytes + 4095) & ~size_t(4095));
+    if (bytes <= pin_bytes) return;
+    free_pins();
+    for (int b = 0; b < 2; ++b) {
+      ORION_HIP(hipHostMalloc(&pin_in[b], bytes, hipHostMallocDefault));
+      ORION_HIP(hipHostMalloc(&pin_out[b], bytes, hipHostMallocDefault));
+    }
+    pin_bytes = bytes;
+  }
+  // host -> device on stream s through the two pinned buffers: the CPU copy of piece
+  // c + 1 overlaps the DMA of piece c.
+  void h2d_staged(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    pins(bytes);
+    for (size_t off = 0, c = 0; off < bytes; off += pin_bytes, ++c) {
       const int b = static_cast<int>(c & 1);
-      const size_t len = std::min(kPinBytes, bytes - off);
-      ORION_HIP(hipEventSynchronize(ev_in[b]));  // the DMA of chunk c - 2 has read pin_in[b]
-      std::memcpy(pin_in[b], static_cast<const char*>(src) + off, len);
+      const size_t len = std::min(pin_bytes, bytes - off);
+      if (c >= 2) ORION_HIP(hipEventSynchronize(ev_in[b]));  // the DMA of piece c - 2 has read pin_in[b]
+      par_copy(pin_in[b], static_cast<const char*>(src) + off, len);
       ORION_HIP(hipMemcpyAsync(static_cast<char*>(dst) + off, pin_in[b], len, hipMemcpyHostToDevice, s));
       ORION_HIP(hipEventRecord(ev_in[b], s));
     }
   }
   // device -> host after everything enqueued on s; synchronous.
-  void d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
-    if (!bytes) {
-      ORION_HIP(hipStreamSynchronize(s));
-      return;
-    }
-    if (host_is_pinned(dst)) {
-      ORION_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
-      ORION_HIP(hipStreamSynchronize(s));
-      return;
-    }
+  void d2h_staged(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    pins(bytes);
     size_t prev_off = 0, prev_len = 0;
     int prev_b = -1;
-    for (size_t off = 0, c = 0; off < bytes; off += kPinBytes, ++c) {
+    for (size_t off = 0, c = 0; off < bytes; off += pin_bytes, ++c) {
       const int b = static_cast<int>(c & 1);
-      const size_t len = std::min(kPinBytes, bytes - off);
+      const size_t len = std::min(pin_bytes, bytes - off);
       ORION_HIP(hipMemcpyAsync(pin_out[b], static_cast<const char*>(src) + off, len, hipMemcpyDeviceToHost, s));
       ORION_HIP(hipEventRecord(ev_out[b], s));
-      if (prev_b >= 0) {  // the CPU copy of chunk c - 1 overlaps the DMA of chunk c
+      if (prev_b >= 0) {  // the CPU copy of piece c - 1 overlaps the DMA of piece c
         ORION_HIP(hipEventSynchronize(ev_out[prev_b]));
-        std::memcpy(static_cast<char*>(dst) + prev_off, pin_out[prev_b], prev_len);
+        par_copy(static_cast<char*>(dst) + prev_off, pin_out[prev_b], prev_len);
       }
       prev_b = b;
       prev_off = off;
       prev_len = len;
     }
     ORION_HIP(hipEventSynchronize(ev_out[prev_b]));
-    std::memcpy(static_cast<char*>(dst) + prev_off, pin_out[prev_b], prev_len);
+    par_copy(static_cast<char*>(dst) + prev_off, pin_out[prev_b], prev_len);
   }
 };
 
@@ -168,19 +275,7 @@ Block::~Block() {
 }
 
 Block::HostPipe& Block::pipe() {
-  if (!pipe_) {
-    auto p = std::make_unique<HostPipe>();
-    ORION_HIP(hipStreamCreateWithFlags(&p->s_in, hipStreamNonBlocking));
-    ORION_HIP(hipStreamCreateWithFlags(&p->s_out, hipStreamNonBlocking));
-    for (int b = 0; b < 2; ++b) {
-      ORION_HIP(hipHostMalloc(&p->pin_in[b], kPinBytes, hipHostMallocDefault));
-      ORION_HIP(hipHostMalloc(&p->pin_out[b], kPinBytes, hipHostMallocDefault));
-      ORION_HIP(hipEventCreateWithFlags(&p->ev_in[b], hipEventDisableTiming));
-      ORION_HIP(hipEventCreateWithFlags(&p->ev_out[b], hipEventDisableTiming));
-      ORION_HIP(hipEventCreateWithFlags(&p->ev_k[b], hipEventDisableTiming));
-    }
-    pipe_ = p.release();
-  }
+  if (!pipe_) pipe_ = new HostPipe();
   return *pipe_;
 }
 
@@ -201,19 +296,40 @@ bool host_is_pinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
+// host -> device / device -> host for process_host: pinned memory by DMA directly,
+// small pageable copies by hipMemcpy (HIP stages them), large ones through the pipe.
+void Block::h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (!bytes) return;
+  if (bytes > kDirectBytes && !host_is_pinned(src)) {
+    pipe().h2d_staged(dst, src, bytes, s);
+    return;
+  }
+  ORION_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+}
+void Block::d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes > kDirectBytes && !host_is_pinned(dst)) {
+    pipe().d2h_staged(dst, src, bytes, s);
+    return;
+  }
+  if (bytes) ORION_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+  ORION_HIP(hipStreamSynchronize(s));
+}
+
 WorkReport Block::process_host(const void* in, size_t n_in, void* out, size_t out_cap) {
   hipStream_t s = host_stream();
   const int nch = channels();
   const size_t q = chunk_quantum();
-  if (q && nch == 1 && n_in >= 2 * kPipeSamples) return host_chunked(in, n_in, out, out_cap, q);
-  HostPipe& P = pipe();
   const size_t ib = dt_size(in_type()), ob = dt_size(out_type());
+  // the chunked pipeline needs a quantum whose input and output fit one staging buffer
+  // (FirDecimator's 512 m quantum exceeds it for m > 2048)
+  if (q && nch == 1 && n_in >= 2 * kPipeSamples && q * std::max(ib, ob) <= kPinBytes)
+    return host_chunked(in, n_in, out, out_cap, q);
   stage_in_.resize(std::max<size_t>(1, n_in * nch * ib));
   stage_out_.resize(std::max<size_t>(1, out_cap * nch * ob));
-  P.h2d(stage_in_.as<void>(), in, n_in * nch * ib, s);
+  h2d(stage_in_.as<void>(), in, n_in * nch * ib, s);
   WorkReport w = process_device(stage_in_.as<void>(), n_in, stage_out_.as<void>(), out_cap, s);
   if (nch == 1) {
-    P.d2h(out, stage_out_.as<void>(), w.out_written * ob, s);
+    d2h(out, stage_out_.as<void>(), w.out_written * ob, s);
   } else {
     if (w.out_written)
       ORION_HIP(hipMemcpy2DAsync(out, out_cap * ob, stage_out_.as<void>(), out_cap * ob, w.out_written * ob, nch,
@@ -234,10 +350,11 @@ WorkReport Block::host_chunked(const void* in, size_t n_in, void* out, size_t ou
   HostPipe& P = pipe();
   hipStream_t sc = host_stream();
   const size_t ib = dt_size(in_type()), ob = dt_size(out_type());
-  const size_t Q = std::max<size_t>(q, kPinBytes / std::max(ib, ob) / q * q);
+  const size_t Q = std::max<size_t>(q, kPinBytes / std::max(ib, ob) / q * q);  // Q max(ib, ob) <= kPinBytes
   const size_t n = consumes_all() ? n_in : std::min(n_in, out_cap);  // decim.rs:72-75 / 1:1 min()
   const size_t n_out = std::min(out_len(n), out_cap);
   const bool pin_i = host_is_pinned(in), pin_o = host_is_pinned(out);
+  if (!pin_i || !pin_o) P.pins(Q * std::max(ib, ob));
   for (int b = 0; b < 2; ++b) {
     P.din[b].resize(Q * ib);
     P.dout[b].resize(std::max<size_t>(1, out_len(Q)) * ob);
@@ -247,7 +364,7 @@ WorkReport Block::host_chunked(const void* in, size_t n_in, void* out, size_t ou
   auto retire = [&](int b) {  // chunk c - 2's copy-out: its buffers of parity b are free after it
     if (!used[b]) return;
     ORION_HIP(hipEventSynchronize(P.ev_out[b]));
-    if (pend_len[b] && !pin_o) std::memcpy(static_cast<char*>(out) + pend_off[b] * ob, P.pin_out[b], pend_len[b] * ob);
+    if (pend_len[b] && !pin_o) par_copy(static_cast<char*>(out) + pend_off[b] * ob, P.pin_out[b], pend_len[b] * ob);
     used[b] = false;
   };
   size_t written = 0;
@@ -260,7 +377,7 @@ WorkReport Block::host_chunked(const void* in, size_t n_in, void* out, size_t ou
     if (pin_i) {
       ORION_HIP(hipMemcpyAsync(P.din[b].as<void>(), src, len * ib, hipMemcpyHostToDevice, P.s_in));
     } else {
-      std::memcpy(P.pin_in[b], src, len * ib);  // pin_in[b]'s previous DMA (chunk c - 2) is done: retire(b)
+      par_copy(P.pin_in[b], src, len * ib);  // pin_in[b]'s previous DMA (chunk c - 2) is done: retire(b)
       ORION_HIP(hipMemcpyAsync(P.din[b].as<void>(), P.pin_in[b], len * ib, hipMemcpyHostToDevice, P.s_in));
     }
     ORION_HIP(hipEventRecord(P.ev_in[b], P.s_in));
@@ -330,7 +447,7 @@ class OscBlock : public Block {
   }
   // One oscillator pass (launch_osc mode) over n samples, advancing the phase.
   void run(int mode, const void* in, void* out, size_t n, hipStream_t s) {
-    launch_osc(mode, static_cast<const f2*>(in), out, static_cast<long long>(n), osc_.count(), osc_.dev(), s);
+    launch_osc(mode, static_cast<const f2*>(in), out, static_cast<long long>(n), osc_.count(), osc_.dev(n, s), s);
     osc_.advance(n);
   }
 
@@ -389,7 +506,7 @@ class AmModBlock final : public Block {
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const size_t n = std::min(n_in, out_cap);  // am.rs:45
     launch_am_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), osc_.count(),
-                  osc_.dev(), cl_, mi_, g_, clamp_, s);
+                  osc_.dev(n, s), cl_, mi_, g_, clamp_, s);
     osc_.advance(n);
     return {n, n};
   }
@@ -416,7 +533,7 @@ class PmModBlock final : public Block {
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const size_t n = std::min(n_in, out_cap);  // pm.rs:37
     launch_pm_mod(static_cast<const float*>(in), static_cast<f2*>(out), static_cast<long long>(n), osc_.count(),
-                  osc_.dev(), kp_, g_, s);
+                  osc_.dev(n, s), kp_, g_, s);
     osc_.advance(n);
     return {n, n};
   }
@@ -461,12 +578,12 @@ class FmModBlock final : public Block {
         epoch_ = 1;
       }
       launch_fm_mod_sp(static_cast<const float*>(in), static_cast<f2*>(out), nn, kf, g_, rec_.as<uint32_t>(), epoch_,
-                       carry_[cur_].as<uint64_t>(), carry_[cur_ ^ 1].as<uint64_t>(), osc_.count(), osc_.dev(),
+                       carry_[cur_].as<uint64_t>(), carry_[cur_ ^ 1].as<uint64_t>(), osc_.count(), osc_.dev(n, s),
                        dev_err(), s);
     } else {
       sums_.resize(static_cast<size_t>(fm_mod_chunks(nn)) * sizeof(uint64_t));
       launch_fm_mod(static_cast<const float*>(in), static_cast<f2*>(out), nn, kf, g_, sums_.as<uint64_t>(),
-                    carry_[cur_].as<uint64_t>(), carry_[cur_ ^ 1].as<uint64_t>(), osc_.count(), osc_.dev(), s);
+                    carry_[cur_].as<uint64_t>(), carry_[cur_ ^ 1].as<uint64_t>(), osc_.count(), osc_.dev(n, s), s);
     }
     cur_ ^= 1;
     osc_.advance(n);
@@ -720,7 +837,7 @@ class WbfmBlock final : public Block {
     }
     const auto msh = mat_pow(ss.A, 4, kSgL / 2);
     for (int i = 0; i < 16; ++i) cs_.mh[i] = msh[i];
-    build_audio_frags(a, bq);
+    build_audio_frags(a);
     // The segmented chain starts every segment's first sub-range from a zero
     // state and hands the next sub-range that sub-range's zero-state end state
     // and last 128 outputs: exact when A^(kSgL - 128) is below f32 resolution
@@ -839,27 +956,16 @@ class WbfmBlock final : public Block {
   std::vector<float> taps(int which) const override { return which == 0 ? h_dec_ : h_aud_; }
   void seek(uint64_t index) { k0_ = index; }
   // The segmented chain's audio FIR runs on f16 matrix cores with hi + lo parts
-  // (k_wbfm.hip sg::back): the A fragments of the Toeplitz tap matrix, and the
-  // scales. |f| <= pi |k| l1(LpCascade) (atan2_approx is within [-pi, pi]), so f 2^sf
-  // with sf = floor(log2(2^15 / bound)) stays below the f16 range with a 2x margin;
-  // the taps are scaled to the same headroom. Both scales are powers of two.
-  void build_audio_frags(const std::vector<float>& a, const BiquadCoeffs& c) {
-    // l1 norm of the LpCascade's impulse response (two TDF-II biquads, iir.rs:34-40)
-    double z[4] = {0, 0, 0, 0}, l1 = 0.0;
-    auto bq = [&](double* s, double x) {
-      const double y = x * c.b0 + s[0];
-      s[0] = x * c.b1 + s[1] - c.a1 * y;
-      s[1] = x * c.b2 - c.a2 * y;
-      return y;
-    };
-    for (int n = 0; n < 1 << 16; ++n) l1 += std::fabs(bq(z + 2, bq(z, n == 0 ? 1.0 : 0.0)));
-    const double bound = M_PI * std::fabs(static_cast<double>(cf_.k)) * l1;
-    const int sf = std::max(-60, std::min(60, static_cast<int>(std::floor(std::log2(32768.0 / std::max(bound, 1e-30))))));
+  // (k_wbfm.hip sg::back): the A fragments of the Toeplitz tap matrix, the taps scaled
+  // by 2^st so that max |a| 2^st lies in [2^14, 2^15) (a power of two: exact). The f
+  // scale is the kernel's, per sub-range.
+  void build_audio_frags(const std::vector<float>& a) {
     float amax = 0.0f;
     for (float v : a) amax = std::max(amax, std::fabs(v));
-    const int st2 = amax > 0.0f ? std::max(-60, std::min(60, static_cast<int>(std::floor(std::log2(32768.0 / amax))))) : 0;
-    cs_.fscale = std::ldexp(1.0f, sf);
-    cs_.yscale = std::ldexp(1.0f, -(sf + st2));
+    int e = 0;
+    (void)std::frexp(amax, &e);  // amax < 2^e
+    const int st2 = amax > 0.0f ? std::max(-100, std::min(100, 15 - e)) : 0;
+    cs_.tscale = std::ldexp(1.0f, -st2);
     std::vector<_Float16> fr(kAudFragBytes / 2);
     for (int s = 0; s < 5; ++s)
       for (int l = 0; l < 64; ++l)

@@ -103,6 +103,8 @@ class Block {
  private:
   struct HostPipe;  // pinned staging, copy streams and events of process_host
   HostPipe& pipe();
+  void h2d(void* dst, const void* src, size_t bytes, hipStream_t s);
+  void d2h(void* dst, const void* src, size_t bytes, hipStream_t s);
   WorkReport host_chunked(const void* in, size_t n_in, void* out, size_t out_cap, size_t q);
   hipStream_t hs_ = nullptr;
   int* err_ = nullptr;

@@ -184,16 +184,13 @@ inline uint64_t state_key(const RecState& s) {
   std::memcpy(&b, &s.zi, 4);
   return (static_cast<uint64_t>(a) << 32) | b;
 }
-// The run: outputs into z until max_out or the first repeated renorm-point state.
-// Returns the step count of the earlier occurrence (cycle start) or UINT64_MAX.
+// The run from output k0 to k1 (z holds 2 k1 floats; s is the state after output
+// k0 - 1), stopping at the first repeated renorm-point state. Returns the step count
+// of the earlier occurrence (cycle start; z cut there) or UINT64_MAX.
 template <class Fma>
-uint64_t rec_run(float wr, float wi, RecState s, uint64_t max_out, std::vector<float>& z, Fma fma) {
-  std::unordered_map<uint64_t, uint64_t> seen;
-  seen.reserve(static_cast<size_t>(std::min<uint64_t>(max_out / 1024 + 2, 1u << 20)));
-  if ((s.ctr & 0x3FFu) == 0) seen.emplace(state_key(s), 0);
-  z.resize(static_cast<size_t>(2 * std::min<uint64_t>(max_out, 1u << 22)));
-  for (uint64_t k = 0; k < max_out; ++k) {
-    if (2 * k + 2 > z.size()) z.resize(std::min<size_t>(2 * z.size(), static_cast<size_t>(2 * max_out)));
+uint64_t rec_run(float wr, float wi, RecState& s, uint64_t k0, uint64_t k1, std::vector<float>& z,
+                 std::unordered_map<uint64_t, uint64_t>& seen, Fma fma) {
+  for (uint64_t k = k0; k < k1; ++k) {
     rec_step(s, wr, wi, fma);
     z[2 * k] = s.zr;
     z[2 * k + 1] = s.zi;
@@ -205,30 +202,51 @@ uint64_t rec_run(float wr, float wi, RecState s, uint64_t max_out, std::vector<f
       }
     }
   }
-  z.resize(static_cast<size_t>(2 * max_out));
   return UINT64_MAX;
 }
-__attribute__((target("fma"))) uint64_t rec_run_hw(float wr, float wi, RecState s, uint64_t max_out,
-                                                   std::vector<float>& z) {
-  return rec_run(wr, wi, s, max_out, z, [](float a, float b, float c) { return __builtin_fmaf(a, b, c); });
+__attribute__((target("fma"))) uint64_t rec_run_hw(float wr, float wi, RecState& s, uint64_t k0, uint64_t k1,
+                                                   std::vector<float>& z, std::unordered_map<uint64_t, uint64_t>& seen) {
+  return rec_run(wr, wi, s, k0, k1, z, seen, [](float a, float b, float c) { return __builtin_fmaf(a, b, c); });
 }
-uint64_t rec_run_sw(float wr, float wi, RecState s, uint64_t max_out, std::vector<float>& z) {
-  return rec_run(wr, wi, s, max_out, z, [](float a, float b, float c) { return std::fma(a, b, c); });
+uint64_t rec_run_sw(float wr, float wi, RecState& s, uint64_t k0, uint64_t k1, std::vector<float>& z,
+                    std::unordered_map<uint64_t, uint64_t>& seen) {
+  return rec_run(wr, wi, s, k0, k1, z, seen, [](float a, float b, float c) { return std::fma(a, b, c); });
 }
 }  // namespace
 
-RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t min_cycle, uint64_t step_q64) {
-  RecTable t;
-  t.ctr0 = s0.ctr;
-  t.mstep = step_q64;
-  const uint64_t c0 = __builtin_cpu_supports("fma") ? rec_run_hw(wr, wi, s0, max_out, t.z)
-                                                    : rec_run_sw(wr, wi, s0, max_out, t.z);
-  t.n = t.z.size() / 2;
+RecBuilder::RecBuilder(float wr, float wi, RecState s0, uint64_t budget, uint64_t min_cycle, uint64_t step_q64)
+    : wr_(wr), wi_(wi), s_(s0), s0_(s0), budget_(budget), min_cycle_(min_cycle) {
+  t_.ctr0 = s0.ctr;
+  t_.mstep = step_q64;
+  if ((s0.ctr & 0x3FFu) == 0) seen_.emplace(state_key(s0), 0);
+  if (budget_ == 0) finish(UINT64_MAX);
+}
+
+void RecBuilder::extend(uint64_t want) {
+  if (done_) return;
+  const uint64_t k1 = std::min(std::max(want, t_.n), budget_);
+  if (k1 > t_.n) {
+    t_.z.resize(static_cast<size_t>(2 * k1));
+    const uint64_t c0 = __builtin_cpu_supports("fma") ? rec_run_hw(wr_, wi_, s_, t_.n, k1, t_.z, seen_)
+                                                      : rec_run_sw(wr_, wi_, s_, t_.n, k1, t_.z, seen_);
+    t_.n = t_.z.size() / 2;
+    if (c0 != UINT64_MAX) {
+      finish(c0);
+      return;
+    }
+  }
+  if (t_.n >= budget_) finish(UINT64_MAX);
+}
+
+void RecBuilder::finish(uint64_t c0) {
+  done_ = true;
+  std::unordered_map<uint64_t, uint64_t>().swap(seen_);
+  RecTable& t = t_;
   if (c0 != UINT64_MAX) {  // outputs c0 .. n-1 repeat forever
     t.cyc_start = c0;
     t.cyc_len = t.n - c0;
     const uint64_t period = t.cyc_len;
-    while (t.cyc_len < min_cycle) {  // unroll
+    while (t.cyc_len < min_cycle_) {  // unroll
       for (uint64_t k = 0; k < period; ++k) {
         t.z.push_back(t.z[2 * (c0 + k)]);
         t.z.push_back(t.z[2 * (c0 + k) + 1]);
@@ -236,16 +254,18 @@ RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t m
       t.cyc_len += period;
     }
     t.n = t.z.size() / 2;
-    return t;
+    return;
   }
   // No cycle within the budget: outputs beyond n follow a model anchored at the last
   // exact output: its phase, plus the mean step fitted (least squares over the renorm
   // points of the run's last half) and the mean magnitude by renorm-counter position
   // (over its last quarter).
+  const RecState s0 = s0_;
   if (t.n == 0) {
     t.mbase = q64_of_angle(std::atan2(static_cast<long double>(s0.zi), static_cast<long double>(s0.zr)));
-    return t;
+    return;
   }
+  const float wr = wr_, wi = wi_;
   const long double th = std::atan2(static_cast<long double>(wi), static_cast<long double>(wr));
   const long double a0 = std::atan2(static_cast<long double>(s0.zi), static_cast<long double>(s0.zr));
   const uint64_t from = t.n / 2, from_mag = t.n - t.n / 4;
@@ -276,21 +296,21 @@ RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t m
     }
   }
   {  // least-squares line through the mean magnitude at each renorm position
-    double s0 = 0, s1 = 0, s2 = 0, t0 = 0, t1 = 0;
+    double s0m = 0, s1 = 0, s2 = 0, t0 = 0, t1 = 0;
     for (int j = 0; j < 1024; ++j) {
       if (!mcnt[j]) continue;
       const double m = msum[j] / static_cast<double>(mcnt[j]);
-      s0 += 1;
+      s0m += 1;
       s1 += j;
       s2 += static_cast<double>(j) * j;
       t0 += m;
       t1 += j * m;
     }
-    const double den = s0 * s2 - s1 * s1;
-    if (s0 >= 2 && den > 0) {
-      const double b = (s0 * t1 - s1 * t0) / den;
+    const double den = s0m * s2 - s1 * s1;
+    if (s0m >= 2 && den > 0) {
+      const double b = (s0m * t1 - s1 * t0) / den;
       t.mag1 = static_cast<float>(b);
-      t.mag0 = static_cast<float>((t0 - b * s1) / s0);
+      t.mag0 = static_cast<float>((t0 - b * s1) / s0m);
     }
   }
   long double slope = 0;
@@ -301,7 +321,12 @@ RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t m
   t.mstep = q64_of_angle(th + slope);
   const uint64_t l = t.n - 1;
   t.mbase = q64_of_angle(std::atan2(static_cast<long double>(t.z[2 * l + 1]), static_cast<long double>(t.z[2 * l])));
-  return t;
+}
+
+RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t min_cycle, uint64_t step_q64) {
+  RecBuilder b(wr, wi, s0, max_out, min_cycle, step_q64);
+  b.extend(max_out);
+  return b.table();
 }
 
 RecState rec_state_after(const RecTable& t, uint64_t k) {

@@ -7,6 +7,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <unordered_map>
 #include <vector>
 
 namespace orion {
@@ -73,6 +74,28 @@ struct RecTable {
 // unrolled (replicated) to at least min_cycle, so a kernel wraps a tile with one
 // subtraction. step_q64: the closed-form step (the model's starting estimate).
 RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t min_cycle, uint64_t step_q64);
+// The same table built incrementally (osc.hpp RefOsc: a retune tabulates only what the
+// next calls use): extend(want) runs the recurrence on to min(want, budget) outputs;
+// reaching the budget or closing the cycle finalises it (cycle unrolled / drift model
+// fitted), after which table() equals rec_table(..., budget, ...).
+class RecBuilder {
+ public:
+  RecBuilder() = default;
+  RecBuilder(float wr, float wi, RecState s0, uint64_t budget, uint64_t min_cycle, uint64_t step_q64);
+  void extend(uint64_t want);
+  bool done() const { return done_; }
+  const RecTable& table() const { return t_; }
+  RecTable& table() { return t_; }
+
+ private:
+  void finish(uint64_t cycle_start);
+  float wr_ = 1.0f, wi_ = 0.0f;
+  RecState s_, s0_;
+  uint64_t budget_ = 0, min_cycle_ = 0;
+  std::unordered_map<uint64_t, uint64_t> seen_;
+  RecTable t_;
+  bool done_ = false;
+};
 // The phasor of output k of a table (exact, or the model beyond it) and the state
 // after output k (for set_freq: the reference keeps z and renorm_ctr).
 RecState rec_state_after(const RecTable& t, uint64_t k);

@@ -416,7 +416,7 @@ class CwModBlock final : public Block {
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const long long n = static_cast<long long>(std::min(n_in, out_cap));  // cw.rs:47
     if (n == 0) return {0, 0};
-    runner_.run(in, out, n, CwPol{rise_, fall_, 1.0f - rise_, 1.0f - fall_, g_, osc_.count(), osc_.dev()}, s);
+    runner_.run(in, out, n, CwPol{rise_, fall_, 1.0f - rise_, 1.0f - fall_, g_, osc_.count(), osc_.dev(n, s)}, s);
     osc_.advance(static_cast<uint64_t>(n));
     return {static_cast<size_t>(n), static_cast<size_t>(n)};
   }

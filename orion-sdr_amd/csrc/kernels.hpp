@@ -117,7 +117,8 @@ struct WbfmFusedConst {
   float b0, b1, b2, a1, a2;   // LpCascade biquad (iir.rs:49-71)
   double pw[6 * 16];          // (A^kSgC)^(2^s)
   double mh[16];              // A^(kSgL/2): one half sub-range (read by iir16 as pw[6])
-  float fscale, yscale;       // audio FIR on the matrix cores: f scale 2^sf, output scale 2^-(sf+st)
+  float tscale;               // audio FIR on the matrix cores: 2^-st (taps scaled by 2^st; f per sub-range)
+  float pad_;
 };
 struct WbfmArgs {
   const f2* x;  long long x_stride;  long long n;

@@ -19,12 +19,20 @@ Oscillator checked_oscillator(float f, float fs) {
 }
 }  // namespace
 
+constexpr uint64_t kOscFirst = 16384;  // outputs tabulated at a (re)tune before any call asks
+
 RefOsc::RefOsc(float freq_hz, float fs, uint64_t budget)
     : fs_(fs), budget_(budget > kNcoTableMax ? kNcoTableMax : budget), osc_(checked_oscillator(freq_hz, fs)) {
+  for (auto& e : ev_) ORION_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   build(RecState{}, 0);
 }
 
-RecState RefOsc::state() const {
+RefOsc::~RefOsc() {
+  for (auto& e : ev_)
+    if (e) (void)hipEventDestroy(e);
+}
+
+RecState RefOsc::state() {
   if (k_ == 0) return org_;
   if (budget_ == 0) {  // closed form: the ideal phasor after k_ steps
     const uint64_t ph = closed_anchor();
@@ -35,11 +43,12 @@ RecState RefOsc::state() const {
     s.ctr = org_.ctr + static_cast<uint32_t>(k_);
     return s;
   }
-  return rec_state_after(tab_, k_ - 1);
+  rb_.extend(k_);  // no-op unless outputs were advanced past the table
+  return rec_state_after(tab(), k_ - 1);
 }
 
-uint64_t RefOsc::closed_anchor() const {
-  if (budget_ == 0) return tab_.mbase + k_ * tab_.mstep;  // phase(k) = mbase + (k + 1) mstep
+uint64_t RefOsc::closed_anchor() {
+  if (budget_ == 0) return tab().mbase + k_ * tab().mstep;  // phase(k) = mbase + (k + 1) mstep
   const RecState s = state();
   return q64_of_angle(std::atan2(static_cast<long double>(s.zi), static_cast<long double>(s.zr)));
 }
@@ -64,46 +73,88 @@ void RefOsc::set_budget(uint64_t budget) {
 }
 
 void RefOsc::build(const RecState& st, uint64_t closed_anchor_q64) {
-  ORION_HIP(hipDeviceSynchronize());  // kernels in flight may still read the old tables
+  // leave the current device tables to the kernels that may still read them
+  if (used_[cur_] && !multi_[cur_]) ORION_HIP(hipEventRecord(ev_[cur_], last_s_[cur_]));
+  cur_ ^= 1;
+  if (used_[cur_]) {  // used two tunes ago: wait until that work has drained
+    if (multi_[cur_]) ORION_HIP(hipDeviceSynchronize());
+    else ORION_HIP(hipEventSynchronize(ev_[cur_]));
+  }
+  used_[cur_] = multi_[cur_] = false;
+  last_s_[cur_] = nullptr;
+  up_ = 0;
+  mt_up_ = false;
   org_ = st;
   k_ = 0;
-  if (budget_ == 0) {
-    tab_ = RecTable{};
-    tab_.ctr0 = st.ctr;
-    tab_.mbase = closed_anchor_q64;
-    tab_.mstep = osc_.step_q64;
+  rb_ = RecBuilder(osc_.w_re, osc_.w_im, st, budget_, kOscSpan, osc_.step_q64);
+  if (budget_ == 0) {  // the closed form: no table, the model from this phase on
+    rb_.table().ctr0 = st.ctr;
+    rb_.table().mbase = closed_anchor_q64;
+    rb_.table().mstep = osc_.step_q64;
+    rb_.table().mag0 = 1.0f;
+    rb_.table().mag1 = 0.0f;
   } else {
-    tab_ = rec_table(osc_.w_re, osc_.w_im, st, budget_, kOscSpan, osc_.step_q64);
+    rb_.extend(std::min<uint64_t>(kOscFirst, budget_));
   }
-  if (tab_.n) {
-    // kOscSpan entries past the table (OscDev: a run reads tab[j + off] unwrapped): the
-    // cycle's continuation, or the last entry repeated (never a used value).
-    std::vector<float> z(tab_.z);
-    z.resize(2 * (tab_.n + kOscSpan));
-    for (uint64_t i = 0; i < static_cast<uint64_t>(kOscSpan); ++i) {
-      const uint64_t src = tab_.cyc_len ? tab_.cyc_start + i % tab_.cyc_len : tab_.n - 1;
-      z[2 * (tab_.n + i)] = tab_.z[2 * src];
-      z[2 * (tab_.n + i) + 1] = tab_.z[2 * src + 1];
-    }
-    dtab_.upload(z.data(), z.size() * sizeof(float));
-  }
-  const double th = static_cast<double>(static_cast<long double>(tab_.mstep) / 18446744073709551616.0L * kTwoPiL);
-  const auto mt = phasor_table(th, kOscSpan);
-  dmtab_.upload(mt.data(), mt.size() * sizeof(float));
 }
 
-OscDev RefOsc::dev() const {
+// New table entries [up_, n) and the kOscSpan entries past n (OscDev: a run reads
+// tab[j + off] unwrapped): the cycle's continuation, or the last entry repeated (never
+// a used value); once the table is final, the model's step table.
+void RefOsc::upload(hipStream_t s) {
+  const RecTable& t = tab();
+  if (t.n > up_ || (t.n && up_ == 0)) {
+    const uint64_t cap = budget_ + 3 * static_cast<uint64_t>(kOscSpan);
+    if (dtab_[cur_].size() < cap * sizeof(f2)) {  // first use of this buffer (or a larger budget)
+      if (dtab_[cur_].size()) ORION_HIP(hipDeviceSynchronize());
+      dtab_[cur_].resize(cap * sizeof(f2));
+    }
+    const uint64_t n0 = up_ ? up_ : 0;
+    std::vector<float> pad(2 * static_cast<size_t>(kOscSpan));
+    for (uint64_t i = 0; i < static_cast<uint64_t>(kOscSpan); ++i) {
+      const uint64_t src = t.cyc_len ? t.cyc_start + i % t.cyc_len : t.n - 1;
+      pad[2 * i] = t.z[2 * src];
+      pad[2 * i + 1] = t.z[2 * src + 1];
+    }
+    char* d = dtab_[cur_].as<char>();
+    // pageable sources: the copy has read them when hipMemcpyAsync returns
+    ORION_HIP(hipMemcpyAsync(d + n0 * sizeof(f2), t.z.data() + 2 * n0, (t.n - n0) * sizeof(f2),
+                             hipMemcpyHostToDevice, s));
+    ORION_HIP(hipMemcpyAsync(d + t.n * sizeof(f2), pad.data(), pad.size() * sizeof(float), hipMemcpyHostToDevice, s));
+    up_ = t.n;
+  }
+  if (!mt_up_ && rb_.done()) {
+    const double th = static_cast<double>(static_cast<long double>(t.mstep) / 18446744073709551616.0L * kTwoPiL);
+    const auto mt = phasor_table(th, kOscSpan);
+    dmtab_[cur_].resize(mt.size() * sizeof(float));
+    ORION_HIP(hipMemcpyAsync(dmtab_[cur_].as<void>(), mt.data(), mt.size() * sizeof(float), hipMemcpyHostToDevice, s));
+    mt_up_ = true;
+  }
+}
+
+OscDev RefOsc::dev(uint64_t n, hipStream_t s) {
+  // the launch's range plus one run past it (every run a kernel forms lies in the table)
+  if (!rb_.done()) rb_.extend(k_ + n + static_cast<uint64_t>(kOscSpan));
+  upload(s);
+  if (last_s_[cur_] && last_s_[cur_] != s) multi_[cur_] = true;
+  last_s_[cur_] = s;
+  used_[cur_] = true;
+  const RecTable& t = tab();
+  if (!dmtab_[cur_].size()) {  // never read before the table is final (runs lie in the table)
+    dmtab_[cur_].resize(2 * kOscSpan * sizeof(float));
+    dmtab_[cur_].zero(s);
+  }
   OscDev d{};
-  d.tab = tab_.n ? dtab_.as<f2>() : nullptr;
-  d.mtab = dmtab_.as<f2>();
-  d.n_tab = tab_.n;
-  d.cyc_start = tab_.cyc_start;
-  d.cyc_len = tab_.cyc_len;
-  d.mbase = tab_.mbase;
-  d.mstep = tab_.mstep;
-  d.ctr0 = tab_.ctr0;
-  d.mag0 = tab_.mag0;
-  d.mag1 = tab_.mag1;
+  d.tab = t.n ? dtab_[cur_].as<f2>() : nullptr;
+  d.mtab = dmtab_[cur_].as<f2>();
+  d.n_tab = t.n;
+  d.cyc_start = t.cyc_start;
+  d.cyc_len = t.cyc_len;
+  d.mbase = t.mbase;
+  d.mstep = t.mstep;
+  d.ctr0 = t.ctr0;
+  d.mag0 = t.mag0;
+  d.mag1 = t.mag1;
   return d;
 }
 

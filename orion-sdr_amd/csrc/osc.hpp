@@ -23,6 +23,9 @@ constexpr uint64_t kNcoTableMax = 1ull << 28;      // 2 GiB of device table
 class RefOsc {
  public:
   RefOsc(float freq_hz, float fs, uint64_t budget = kNcoTableDefault);
+  ~RefOsc();
+  RefOsc(const RefOsc&) = delete;
+  RefOsc& operator=(const RefOsc&) = delete;
   // set_freq (rotator.rs:35-39, nco.rs:33-38): a new step w; z and renorm_ctr carry on.
   void retune(float freq_hz, float fs);
   // reset_phase (rotator.rs:28-31): z = 1 + 0j, renorm_ctr = 0, the step stays.
@@ -30,27 +33,39 @@ class RefOsc {
   // Tabulation budget (orion_block_configure ORION_OPT_NCO_TABLE); the state carries on.
   void set_budget(uint64_t budget);
   uint64_t budget() const { return budget_; }
-  // The device view; the next call's output i is oscillator output count() + i.
-  OscDev dev() const;
+  // The device view for a launch on stream s whose outputs are count() .. count() + n - 1:
+  // tabulates on the host and uploads (stream-ordered on s) whatever of that range the
+  // table does not hold yet. A (re)tune itself only restarts the recurrence: the
+  // tabulation cost follows the samples actually produced (a retune used to
+  // run 2^20 steps, upload 8 MiB and synchronise the device).
+  OscDev dev(uint64_t n, hipStream_t s);
   uint64_t count() const { return k_; }
   void advance(uint64_t n) { k_ += n; }
   const Oscillator& osc() const { return osc_; }
   float fs() const { return fs_; }
-  // Every output is the reference's own (a cycle closed within the budget).
-  bool exact_forever() const { return tab_.cyc_len != 0; }
-  uint64_t exact_outputs() const { return tab_.cyc_len ? UINT64_MAX : tab_.n; }
 
  private:
   void build(const RecState& st, uint64_t closed_anchor_q64);
-  RecState state() const;        // the reference's (z, renorm_ctr) after count() outputs
-  uint64_t closed_anchor() const;  // closed form: the Q0.64 phase after count() outputs
+  void upload(hipStream_t s);
+  RecState state();                // the reference's (z, renorm_ctr) after count() outputs
+  uint64_t closed_anchor();        // closed form: the Q0.64 phase after count() outputs
+  const RecTable& tab() const { return rb_.table(); }
   float fs_;
   uint64_t budget_;
   Oscillator osc_{};
-  RecTable tab_;
-  RecState org_;  // start state of tab_
+  RecBuilder rb_;
+  RecState org_;  // start state of the table
   uint64_t k_ = 0;
-  DevBuf dtab_, dmtab_;
+  // Two device tables, alternating per (re)tune: kernels of the previous tune may still
+  // read theirs. A buffer is rewritten only after the work that used it has drained
+  // (an event on the stream it was used on; a device sync if several streams used it).
+  DevBuf dtab_[2], dmtab_[2];
+  hipEvent_t ev_[2] = {nullptr, nullptr};
+  bool used_[2] = {false, false}, multi_[2] = {false, false};
+  hipStream_t last_s_[2] = {nullptr, nullptr};
+  int cur_ = 0;
+  uint64_t up_ = 0;       // table entries uploaded to dtab_[cur_] (their padding included)
+  bool mt_up_ = false;    // dmtab_[cur_] holds this tune's model steps
 };
 
 }  // namespace orion

@@ -131,7 +131,7 @@ class ScanStage {
     a.n = n;
     a.k0 = osc_ ? static_cast<long long>(osc_->count()) : k0;
     a.translate = translate_ ? 1 : 0;
-    if (osc_) a.osc = osc_->dev();
+    if (osc_) a.osc = osc_->dev(static_cast<uint64_t>(n), s);
     a.mats = mats_.as<double>();
     a.zmap = sp1_ok_ || !sp_ok_ ? zmap_.as<float>() : zmap_lp_.as<float>();  // k_lpdc_sp: its LP4's map
     a.aggs = ws_.as<double>();
@@ -410,16 +410,16 @@ class SsbModBlock final : public Block {
     if (n == 0) return {0, 0};
     const long long nn = static_cast<long long>(n);
     if (sp_ok_ && mode_ == 0) {
-      launch_ssb_mod_sp(static_cast<const float*>(in), static_cast<f2*>(out), nn, aud_.count(), aud_.dev(), rf_.dev(),
+      launch_ssb_mod_sp(static_cast<const float*>(in), static_cast<f2*>(out), nn, aud_.count(), aud_.dev(n, s), rf_.dev(n, s),
                         side_, coef_lp(b_), mats_.as<double>(), zmap_.as<float>(), carry_[cur_].as<float>(),
                         carry_[cur_ ^ 1].as<float>(), s);
       cur_ ^= 1;
     } else {
       u_.resize(2 * n * sizeof(float));
       v_.resize(2 * n * sizeof(float));
-      launch_ssb_mod_front(static_cast<const float*>(in), u_.as<float>(), nn, aud_.count(), aud_.dev(), s);
+      launch_ssb_mod_front(static_cast<const float*>(in), u_.as<float>(), nn, aud_.count(), aud_.dev(n, s), s);
       st_->run(u_.as<void>(), nn, nn, v_.as<void>(), nn, 0, dev_err(), s);
-      launch_ssb_mod_back(v_.as<float>(), static_cast<f2*>(out), nn, rf_.count(), rf_.dev(), side_, s);
+      launch_ssb_mod_back(v_.as<float>(), static_cast<f2*>(out), nn, rf_.count(), rf_.dev(n, s), side_, s);
     }
     aud_.advance(n);
     rf_.advance(n);

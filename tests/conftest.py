@@ -66,14 +66,14 @@ def nrmse(got, ref):
     return float(np.sqrt(np.mean(np.abs(got - ref) ** 2)) / (den if den > 0 else 1.0))
 
 
-def wbfm_input(n, f_off=1.5e6, fs=10e6, noise=0.0025, seed=0x1234_5678_ABCD_EF00):
-    """C2 synthetic IQ: FM dev 75 kHz of 0.5 sin(1k) + 0.3 sin(7k),
+def wbfm_input(n, f_off=1.5e6, fs=10e6, noise=0.0025, seed=0x1234_5678_ABCD_EF00, amp=1.0, dev=75e3):
+    """C2 synthetic IQ: FM dev 75 kHz of amp (0.5 sin(1k) + 0.3 sin(7k)),
     up-converted to f_off by FmPhaseAccumMod's RF NCO, plus add_awgn."""
     import oracle as O
 
     t = np.arange(n) / fs
-    aud = (0.5 * np.sin(2 * np.pi * 1e3 * t) + 0.3 * np.sin(2 * np.pi * 7e3 * t)).astype(np.float32)
-    iq = O.fm_mod(aud, fs, 75e3, f_off)
+    aud = (amp * (0.5 * np.sin(2 * np.pi * 1e3 * t) + 0.3 * np.sin(2 * np.pi * 7e3 * t))).astype(np.float32)
+    iq = O.fm_mod(aud, fs, dev, f_off)
     if noise > 0:
         iq = O.add_awgn(iq, noise, seed)
     return iq
