@@ -53,11 +53,6 @@ KERNELS = {"c1": "k_fir_iq8", "c2": "k_wbfm_seg", "c3": "k_decim_w4q", "c4": "k_
 CHANNELS_PER_GPU = {"c3": 256, "c4": 8, "c5": 128}
 
 
-def _sum_sin(w, k):
-    """sum_{j < k} sin(w j), closed form (float64)."""
-    return np.sin(w * (k - 1) / 2) * np.sin(w * k / 2) / np.sin(w / 2) if k > 0 else 0.0
-
-
 _M64 = (1 << 64) - 1
 
 
@@ -91,18 +86,21 @@ def index_noise(idx, seed):
 def wbfm_iq(n, f_off, dev, seed, fs=10e6, t0=0, noise=0.0025):
     """C2 synthetic IQ generated on the device: FM (dev 75 kHz) of
     0.5 sin(1 kHz) + 0.3 sin(7 kHz) at +f_off, plus complex AWGN (P = 0.0025).
-    t0: index of the first sample within the stream (a time shard of it; the
-    FM phase accumulated before t0 is added in closed form, the noise is a function
-    of the absolute index)."""
+    t0: index of the first sample within the stream. Every sample is a function of its
+    absolute index alone (the FM phase sum_{j <= k} in closed form, the noise by
+    index_noise), so a time shard, halo included, is bit for bit the stream's slice."""
     idx = torch.arange(n, device=dev, dtype=torch.int64) + t0
-    t = idx.to(torch.float64) / fs
-    aud = 0.5 * torch.sin(2 * np.pi * 1e3 * t) + 0.3 * torch.sin(2 * np.pi * 7e3 * t)
-    k = 2 * np.pi * 75e3 / fs
-    ph0 = k * (0.5 * _sum_sin(2 * np.pi * 1e3 / fs, t0) + 0.3 * _sum_sin(2 * np.pi * 7e3 / fs, t0))
-    ph = torch.cumsum(k * aud, 0) + ph0 + 2 * np.pi * f_off * t
-    del aud
+    kk = (idx + 1).to(torch.float64)  # samples summed into the phase of sample idx
+
+    def sum_sin(w):  # sum_{j < K} sin(w j), closed form
+        return torch.sin(w * (kk - 1) / 2) * torch.sin(w * kk / 2) / np.sin(w / 2)
+
+    kdev = 2 * np.pi * 75e3 / fs
+    ph = kdev * (0.5 * sum_sin(2 * np.pi * 1e3 / fs) + 0.3 * sum_sin(2 * np.pi * 7e3 / fs))
+    del kk
+    ph += (2 * np.pi * f_off / fs) * idx.to(torch.float64)
     x = torch.polar(torch.ones_like(ph), ph).to(torch.complex64)
-    del ph, t
+    del ph
     if noise > 0:
         x += index_noise(idx, seed) * np.float32(np.sqrt(noise))
     return x

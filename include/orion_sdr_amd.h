@@ -206,9 +206,11 @@ orion_block* orion_ssb_phasing_mod_new(float fs, float audio_bw_hz, float audio_
 /* The WBFM chain composed per docs/demodulate.md:128-133 (no single reference
  * type): Rotator(-f_off, fs) -> FirDecimator(fs, m, dec_cutoff, dec_trans) ->
  * FmQuadratureDemod(fs/m, dev_hz, audio_bw) -> FirLowpass(fs/m, audio_pass,
- * audio_trans). cf32 -> f32 in one gfx950 kernel per call (m must be 8): NCO +
- * polyphase decimation + discriminator + LpCascade + audio FIR, intermediates on
- * chip (two kernels for IIR designs that decay too slowly; see configure). */
+ * audio_trans). Any design the reference's constructors accept. cf32 -> f32 in one
+ * gfx950 kernel per call for m = 8 with <= 128 decimator and audio taps and an
+ * LpCascade that forgets within 896 outputs (the WBFM defaults): NCO + polyphase
+ * decimation + discriminator + LpCascade + audio FIR, intermediates on chip; other
+ * designs run the four blocks stage by stage (see configure). */
 typedef struct {
   float fs, f_off, dec_cutoff, dec_trans, dev_hz, audio_bw, audio_pass, audio_trans;
   size_t m;
@@ -217,8 +219,9 @@ orion_block* orion_wbfm_chain_new(const orion_wbfm_params* p);
 /* nch channels sharing the design, each with its own tuning offset f_off[ch]. */
 orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float* f_off, size_t nch);
 /* Engine tuning and tests (no reference counterpart): the kernel path of a WBFM
- * chain handle. ORION_WBFM_AUTO picks the segmented single kernel when the
- * LpCascade decays fast enough for it (the WBFM defaults), else two kernels;
+ * chain handle, chosen before its first call. ORION_WBFM_AUTO picks the segmented
+ * single kernel when the design allows it, else the two-kernel path when its
+ * LpCascade warm-up suffices, else the four blocks (ORION_WBFM_GRAPH);
  * max_segments > 0 sets the segmented kernel's segments (waves; more than the
  * resident capacity runs several rounds), 0 = one round at the resident capacity.
  * ORION_E_TYPE if b is not a WBFM chain, ORION_E_ARG if the design cannot run on
@@ -231,7 +234,8 @@ orion_block* orion_wbfm_chain_batch_new(const orion_wbfm_params* p, const float*
  * orion_block_status) instead of returning the audio as valid. */
 #define ORION_WBFM_AUTO 0
 #define ORION_WBFM_SEGMENTED 1  /* one kernel, one round of segments (k_wbfm_seg) */
-#define ORION_WBFM_SPLIT 3      /* two kernels (front, back), any IIR design */
+#define ORION_WBFM_SPLIT 3      /* two kernels (front, back): m = 8, <= 128 taps, ||A^510|| < 1e-7 */
+#define ORION_WBFM_GRAPH 4      /* Rotator, FirDecimator, FmQuadratureDemod, FirLowpass blocks: any design */
 int orion_wbfm_chain_configure(orion_block* b, int path, int max_segments);
 /* Time-sharded streams (no reference counterpart): the absolute
  * index of the next input sample, i.e. the NCO phase origin (rotator.rs:44-62

@@ -2,6 +2,7 @@
 #include "blocks.hpp"
 
 #include "osc.hpp"
+#include "scan_blocks.hpp"
 
 #include <algorithm>
 #include <atomic>
@@ -437,6 +438,7 @@ class OscBlock : public Block {
   void reset() override { osc_.reset(); }  // phasor back to 1 + 0j (Rotator::reset_phase, rotator.rs:28-31)
   std::vector<float> taps(int) const override { return {osc_.osc().w_re, osc_.osc().w_im}; }
   void set_freq(float f, float fs) { osc_.retune(f, fs); }
+  void seek(uint64_t k) { osc_.seek(k); }  // the phase origin of a time shard (no reference counterpart)
   float fs() const { return osc_.fs(); }
   size_t chunk_quantum() const override { return kRotTile; }  // tiles keep their alignment
   int configure(int option, long long value) override {
@@ -793,72 +795,31 @@ class FirIqBlock final : public Block {
 };
 
 // ------------------------------------------------------------ WBFM chain ----
+// The reference composition (docs/demodulate.md:128-133) on three engines:
+//   kPathSeg   k_wbfm_seg, one kernel (m = 8, <= 128 decimator and audio taps, an
+//              LpCascade that forgets within a sub-range: the WBFM defaults);
+//   kPathSplit k_wbfm_front2 + k_wbfm_back (same designs, LpCascade warm-up of kBackW);
+//   kPathGraph the four blocks themselves, stage by stage through HBM: Rotator (the
+//              reference's own recurrence) -> FirDecimator (any m, any taps) ->
+//              FmQuadratureDemod (exact scan, any LpCascade) -> FirLowpass (any taps).
+//              Any design the reference's constructors accept (decim.rs:24-37,
+//              fir.rs:16-44, fm.rs:17-31).
+// The fused paths mix with the closed-form phasor of the recurrence's LONG-RUN step
+// (design.hpp rec_mean_step): the reference's f32 Rotator drifts from its nominal step
+// by ~1e-8 rad per sample (-1.5 MHz / 10 MHz: +1.15e-8), which the discriminator turns
+// into a DC offset of ~6e-7 of full-scale audio; the mean step reproduces it, the
+// per-step jitter is below the decimator's passband rounding.
 class WbfmBlock final : public Block {
  public:
-  WbfmBlock(const WbfmParams& p, const std::vector<float>& f_off) : p_(p), nch_(static_cast<int>(f_off.size())) {
-    if (p.m != 8) throw std::invalid_argument("fused WBFM chain requires m = 8");
+  WbfmBlock(const WbfmParams& p, const std::vector<float>& f_off)
+      : p_(p), nch_(static_cast<int>(f_off.size())), f_off_(f_off) {
+    if (p.m < 1) throw std::invalid_argument("WBFM chain: decimation m must be >= 1");
     if (nch_ < 1) throw std::invalid_argument("WBFM chain needs >= 1 channel");
     h_dec_ = fir_lowpass_taps(p.fs, p.dec_cutoff, p.dec_trans);
     const float fs2 = p.fs / static_cast<float>(p.m);
     h_aud_ = fir_lowpass_taps(fs2, p.audio_pass, p.audio_trans);
-    if (h_dec_.size() > 128 || h_aud_.size() > 128)
-      throw std::invalid_argument("fused WBFM chain supports <= 128 decimator and audio taps");
-    std::memset(&cf_, 0, sizeof(cf_));
-    std::memset(&cb_, 0, sizeof(cb_));
-    const auto g = fir_lowpass_as_standard(h_dec_);
-    for (size_t k = 0; k < g.size(); ++k) cf_.g[(k % 8) * kWbfmQ + k / 8] = g[k];
-    cf_.k = 1.0f / std::max(p.dev_hz, 1.0f);  // fm.rs:23
-    const auto a = fir_lowpass_as_standard(h_aud_);
-    for (size_t k = 0; k < a.size(); ++k) cb_.a[k] = a[k];
-    const BiquadCoeffs bq = lp_cascade_design(fs2, p.audio_bw * 0.9f);  // fm.rs:24
-    cb_.b0 = bq.b0; cb_.b1 = bq.b1; cb_.b2 = bq.b2; cb_.a1 = bq.a1; cb_.a2 = bq.a2;
-    const StateSpace ss = lp_cascade_ss(bq);
-    auto pwm = mat_pow(ss.A, 4, kBackC);
-    for (int s = 0; s < 6; ++s) {
-      for (int i = 0; i < 16; ++i) cb_.pw[s * 16 + i] = pwm[i];
-      pwm = mat_mul(pwm, pwm, 4);
-    }
-    const auto mw = mat_pow(ss.A, 4, 64ull * kBackC);
-    for (int i = 0; i < 16; ++i) cb_.mw[i] = mw[i];
-    std::vector<double> lm(64 * 16);
-    for (int L = 0; L < 64; ++L) {
-      const auto m = mat_pow(ss.A, 4, static_cast<uint64_t>(kBackC) * L);
-      std::copy(m.begin(), m.end(), lm.begin() + L * 16);
-    }
-    lanemats_.upload(lm.data(), lm.size() * sizeof(double));
-    // segmented chain constants: steps A^(kSgC 2^s), and A^(kSgL/2)
-    std::memset(&cs_, 0, sizeof(cs_));
-    for (size_t k = 0; k < a.size(); ++k) cs_.a[k] = a[k];
-    cs_.b0 = bq.b0; cs_.b1 = bq.b1; cs_.b2 = bq.b2; cs_.a1 = bq.a1; cs_.a2 = bq.a2;
-    auto ps = mat_pow(ss.A, 4, kSgC);
-    for (int s = 0; s < 6; ++s) {
-      for (int i = 0; i < 16; ++i) cs_.pw[s * 16 + i] = ps[i];
-      ps = mat_mul(ps, ps, 4);
-    }
-    const auto msh = mat_pow(ss.A, 4, kSgL / 2);
-    for (int i = 0; i < 16; ++i) cs_.mh[i] = msh[i];
-    build_audio_frags(a);
-    // The segmented chain starts every segment's first sub-range from a zero
-    // state and hands the next sub-range that sub-range's zero-state end state
-    // and last 128 outputs: exact when A^(kSgL - 128) is below f32 resolution
-    // relative to A^0 = I (~1e-16 for the WBFM defaults).
-    {
-      const auto m = mat_pow(ss.A, 4, kSgL - 128);
-      double fro = 0.0;
-      for (double v : m) fro += v * v;
-      seg_ok_ = std::sqrt(fro) < 1e-10;
-    }
-    std::vector<uint64_t> steps(nch_);
-    std::vector<float> tabs;
-    tabs.reserve(static_cast<size_t>(nch_) * kWbfmNS * 2);
-    for (int ch = 0; ch < nch_; ++ch) {
-      const Oscillator o = oscillator(-f_off[ch], p.fs);  // Rotator::new(-f_off, fs)
-      steps[ch] = o.step_q64;
-      const auto t = phasor_table(o.theta, kWbfmNS);
-      tabs.insert(tabs.end(), t.begin(), t.end());
-    }
-    step_.upload(steps.data(), steps.size() * sizeof(uint64_t));
-    tab_.upload(tabs.data(), tabs.size() * sizeof(float));
+    fused_ok_ = p.m == kWbfmM && h_dec_.size() <= 128 && h_aud_.size() <= 128;
+    if (fused_ok_) build_fused(f_off);
     for (int i = 0; i < 2; ++i) {
       carry_[i].resize(static_cast<size_t>(nch_) * kWbfmCarry * sizeof(float));
       hist_[i].resize(static_cast<size_t>(nch_) * kWbfmHist * sizeof(f2));
@@ -874,6 +835,12 @@ class WbfmBlock final : public Block {
   WorkReport process_device(const void* in, size_t n, void* out, size_t out_cap, hipStream_t s) override {
     if (n == 0) return {0, 0};
     const size_t n_dec = std::min(out_len(n), out_cap);
+    const int path = resolved_path();
+    if (path == kPathGraph) {
+      graph(static_cast<const f2*>(in), n, static_cast<float*>(out), out_cap, n_dec, s);
+      k0_ += n;
+      return {n, n_dec};
+    }
     const int nxt = cur_ ^ 1;
     if (n_dec == 0) {  // decimator consumed input, demod saw nothing (core.rs chain semantics)
       const f2* x = static_cast<const f2*>(in);
@@ -898,7 +865,6 @@ class WbfmBlock final : public Block {
       a.hist_out = hist_[nxt].as<f2>();
       a.lanemats = lanemats_.as<double>();
       a.afrag = afrag_.as<void>();
-      const int path = path_ == kPathAuto ? (seg_ok_ ? kPathSeg : kPathSplit) : path_;
       if (path == kPathSeg) {
         const long long slots = wbfm_seg_slots(static_cast<long long>(n_dec), nch_);
         if (static_cast<size_t>(slots) * kSeg4Slot * 4 > hand_.size()) hand_.resize(static_cast<size_t>(slots) * kSeg4Slot * 4);
@@ -952,9 +918,97 @@ class WbfmBlock final : public Block {
     ORION_HIP(hipDeviceSynchronize());
     cur_ = 0;
     k0_ = 0;
+    stages_.clear();  // the graph path's blocks restart from their constructors' state
   }
   std::vector<float> taps(int which) const override { return which == 0 ? h_dec_ : h_aud_; }
-  void seek(uint64_t index) { k0_ = index; }
+  void seek(uint64_t index) {
+    k0_ = index;
+    stages_.clear();
+    seek_ = index;
+  }
+  int set_path(int path, int max_seg) {
+    if ((path != kPathAuto && path != kPathSeg && path != kPathSplit && path != kPathGraph) || max_seg < 0) return -3;
+    if (path == kPathSeg && !seg_ok_) return -3;
+    if (path == kPathSplit && !split_ok_) return -3;
+    if (path != path_) {
+      if (k0_ != 0) return -3;  // the paths carry their state differently: choose before the first call
+      stages_.clear();
+    }
+    path_ = path;
+    max_seg_ = max_seg;
+    return 0;
+  }
+
+ private:
+  int resolved_path() const {
+    if (path_ != kPathAuto) return path_;
+    return seg_ok_ ? kPathSeg : split_ok_ ? kPathSplit : kPathGraph;
+  }
+  // ---- fused paths: constants ----
+  void build_fused(const std::vector<float>& f_off) {
+    const WbfmParams& p = p_;
+    const float fs2 = p.fs / static_cast<float>(p.m);
+    std::memset(&cf_, 0, sizeof(cf_));
+    std::memset(&cb_, 0, sizeof(cb_));
+    const auto g = fir_lowpass_as_standard(h_dec_);
+    for (size_t k = 0; k < g.size(); ++k) cf_.g[(k % 8) * kWbfmQ + k / 8] = g[k];
+    cf_.k = 1.0f / std::max(p.dev_hz, 1.0f);  // fm.rs:23
+    const auto a = fir_lowpass_as_standard(h_aud_);
+    for (size_t k = 0; k < a.size(); ++k) cb_.a[k] = a[k];
+    const BiquadCoeffs bq = lp_cascade_design(fs2, p.audio_bw * 0.9f);  // fm.rs:24
+    cb_.b0 = bq.b0; cb_.b1 = bq.b1; cb_.b2 = bq.b2; cb_.a1 = bq.a1; cb_.a2 = bq.a2;
+    const StateSpace ss = lp_cascade_ss(bq);
+    auto pwm = mat_pow(ss.A, 4, kBackC);
+    for (int s = 0; s < 6; ++s) {
+      for (int i = 0; i < 16; ++i) cb_.pw[s * 16 + i] = pwm[i];
+      pwm = mat_mul(pwm, pwm, 4);
+    }
+    const auto mw = mat_pow(ss.A, 4, 64ull * kBackC);
+    for (int i = 0; i < 16; ++i) cb_.mw[i] = mw[i];
+    std::vector<double> lm(64 * 16);
+    for (int L = 0; L < 64; ++L) {
+      const auto m = mat_pow(ss.A, 4, static_cast<uint64_t>(kBackC) * L);
+      std::copy(m.begin(), m.end(), lm.begin() + L * 16);
+    }
+    lanemats_.upload(lm.data(), lm.size() * sizeof(double));
+    // segmented chain constants: steps A^(kSgC 2^s), and A^(kSgL/2)
+    std::memset(&cs_, 0, sizeof(cs_));
+    for (size_t k = 0; k < a.size(); ++k) cs_.a[k] = a[k];
+    cs_.b0 = bq.b0; cs_.b1 = bq.b1; cs_.b2 = bq.b2; cs_.a1 = bq.a1; cs_.a2 = bq.a2;
+    auto ps = mat_pow(ss.A, 4, kSgC);
+    for (int s = 0; s < 6; ++s) {
+      for (int i = 0; i < 16; ++i) cs_.pw[s * 16 + i] = ps[i];
+      ps = mat_mul(ps, ps, 4);
+    }
+    const auto msh = mat_pow(ss.A, 4, kSgL / 2);
+    for (int i = 0; i < 16; ++i) cs_.mh[i] = msh[i];
+    build_audio_frags(a);
+    // The segmented chain starts every segment's first sub-range from a zero state and
+    // hands the next sub-range that sub-range's zero-state end state and last 128
+    // outputs: exact when A^(kSgL - 128) is below f32 resolution relative to A^0 = I
+    // (~1e-16 for the WBFM defaults). The split path's back starts each half from a
+    // kBackW-sample zero-state warm-up: the same test on A^kBackW.
+    auto fro = [&](uint64_t k) {
+      const auto m = mat_pow(ss.A, 4, k);
+      double f = 0.0;
+      for (double v : m) f += v * v;
+      return std::sqrt(f);
+    };
+    seg_ok_ = fro(kSgL - 128) < 1e-10;
+    split_ok_ = fro(kBackW) < 1e-7;  // the WBFM defaults: 2.0e-8
+    std::vector<uint64_t> steps(nch_);
+    std::vector<float> tabs;
+    tabs.reserve(static_cast<size_t>(nch_) * kWbfmNS * 2);
+    for (int ch = 0; ch < nch_; ++ch) {
+      const Oscillator o = oscillator(-f_off[ch], p.fs);  // Rotator::new(-f_off, fs)
+      const double th = rec_mean_step(o.w_re, o.w_im, o.step_q64);
+      steps[ch] = q64_of_angle(th);
+      const auto t = phasor_table(th, kWbfmNS);
+      tabs.insert(tabs.end(), t.begin(), t.end());
+    }
+    step_.upload(steps.data(), steps.size() * sizeof(uint64_t));
+    tab_.upload(tabs.data(), tabs.size() * sizeof(float));
+  }
   // The segmented chain's audio FIR runs on f16 matrix cores with hi + lo parts
   // (k_wbfm.hip sg::back): the A fragments of the Toeplitz tap matrix, the taps scaled
   // by 2^st so that max |a| 2^st lies in [2^14, 2^15) (a power of two: exact). The f
@@ -978,25 +1032,52 @@ class WbfmBlock final : public Block {
         }
     afrag_.upload(fr.data(), kAudFragBytes);
   }
-  int set_path(int path, int max_seg) {
-    if ((path != kPathAuto && path != kPathSeg && path != kPathSplit) || max_seg < 0) return -3;
-    if (path == kPathSeg && !seg_ok_) return -3;
-    path_ = path;
-    max_seg_ = max_seg;
-    return 0;
+  // ---- graph path: the reference's four blocks, per channel ----
+  struct Stages {
+    std::unique_ptr<Block> rot, dec, fm, aud;
+  };
+  void graph(const f2* x, size_t n, float* y, size_t out_cap, size_t n_dec, hipStream_t s) {
+    const WbfmParams& p = p_;
+    const float fs2 = p.fs / static_cast<float>(p.m);
+    if (stages_.empty()) {
+      for (int ch = 0; ch < nch_; ++ch) {
+        Stages st;
+        st.rot = make_rotator(-f_off_[ch], p.fs);
+        if (seek_) osc_seek(st.rot.get(), seek_);
+        st.dec = make_fir_decimator(p.fs, p.m, p.dec_cutoff, p.dec_trans, 1);
+        st.fm = make_fm_demod(fs2, p.dev_hz, p.audio_bw);
+        st.aud = make_fir_lowpass(fs2, p.audio_pass, p.audio_trans);
+        stages_.push_back(std::move(st));
+      }
+    }
+    const size_t nd_all = out_len(n);
+    mixed_.resize(n * sizeof(f2));
+    dec_.resize(std::max<size_t>(1, nd_all) * sizeof(f2));
+    phi_.resize(std::max<size_t>(1, nd_all) * sizeof(float));
+    for (int ch = 0; ch < nch_; ++ch) {
+      Stages& st = stages_[ch];
+      const f2* xc = x + static_cast<size_t>(ch) * n;
+      st.rot->process_device(xc, n, mixed_.as<void>(), n, s);
+      // decim.rs:44-76: all input consumed, min(ceil(n/m), cap) written
+      const WorkReport wd = st.dec->process_device(mixed_.as<void>(), n, dec_.as<void>(), n_dec, s);
+      st.fm->process_device(dec_.as<void>(), wd.out_written, phi_.as<void>(), wd.out_written, s);
+      st.aud->process_device(phi_.as<void>(), wd.out_written, y + static_cast<size_t>(ch) * out_cap, out_cap, s);
+    }
   }
 
- private:
   WbfmParams p_;
   int nch_;
+  std::vector<float> f_off_;
   std::vector<float> h_dec_, h_aud_;
-  WbfmFrontConst cf_;
-  WbfmBackConst cb_;
-  WbfmFusedConst cs_;
-  bool seg_ok_ = false;
+  WbfmFrontConst cf_{};
+  WbfmBackConst cb_{};
+  WbfmFusedConst cs_{};
+  bool fused_ok_ = false, seg_ok_ = false, split_ok_ = false;
   int path_ = kPathAuto, max_seg_ = 0;
   uint32_t epoch_ = 0;
-  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, hand_, flags_, trace_, afrag_;
+  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, hand_, flags_, trace_, afrag_, mixed_, dec_;
+  std::vector<Stages> stages_;
+  uint64_t seek_ = 0;
   int cur_ = 0;
   uint64_t k0_ = 0;
 };
@@ -1023,6 +1104,12 @@ int osc_mix_usb(Block* b, const void* in, size_t n, float* out, hipStream_t s) {
   auto* o = dynamic_cast<RotatorBlock*>(b);
   if (!o) return -4;
   o->run(1, in, out, n, s);
+  return 0;
+}
+int osc_seek(Block* b, uint64_t index) {
+  auto* o = dynamic_cast<OscBlock*>(b);
+  if (!o) return -4;
+  o->seek(index);
   return 0;
 }
 int osc_next_cs(Block* b, const char* kind, void* out, size_t n, hipStream_t s) {

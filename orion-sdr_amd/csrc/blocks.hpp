@@ -121,6 +121,8 @@ bool host_is_pinned(const void* p);
 std::unique_ptr<Block> make_rotator(float freq_hz, float fs);
 // dsp/nco.rs:11-66 (mix_with_nco per sample). C32 -> C32.
 std::unique_ptr<Block> make_nco(float freq_hz, float fs);
+// Oscillator output index of the next sample (a time shard's phase origin); -4 otherwise.
+int osc_seek(Block* b, uint64_t index);
 // Oscillator controls (-4 if b is not of that kind): set_freq (Rotator: rotator.rs:35-39,
 // kind "Rotator"; Nco: nco.rs:33-38, kind "Nco", the block's own fs), reset_phase
 // (rotator.rs:28-31), mix_usb_block (rotator.rs:88-94, C32 -> F32 on device buffers) and
@@ -156,8 +158,8 @@ int fm_mod_set_deviation(Block* b, float d);     // -4 if not an FmPhaseAccumMod
 std::unique_ptr<Block> make_agc(bool iq, float fs, float attack_ms, float release_ms, float target_rms);  // agc.rs
 
 // The WBFM chain (docs/demodulate.md:128-133): Rotator(-f_off) -> FirDecimator
-// (fs, m=8, dec_cutoff, dec_trans) -> FmQuadratureDemod(fs/8, dev, audio_bw) ->
-// FirLowpass(fs/8, audio_pass, audio_trans). C32 -> F32, out = ceil(n/8).
+// (fs, m, dec_cutoff, dec_trans) -> FmQuadratureDemod(fs/m, dev, audio_bw) ->
+// FirLowpass(fs/m, audio_pass, audio_trans). C32 -> F32, out = ceil(n/m).
 struct WbfmParams {
   float fs, dec_cutoff, dec_trans, dev_hz, audio_bw, audio_pass, audio_trans;
   size_t m;
@@ -167,7 +169,7 @@ std::unique_ptr<Block> make_wbfm_chain(const WbfmParams& p, const std::vector<fl
 // orion_wbfm_chain_configure). max_segments > 0 caps the segmented kernel's
 // waves (default: the resident capacity). Returns -4 if b is not a WBFM chain,
 // -3 if this design cannot run on that path.
-enum : int { kPathAuto = 0, kPathSeg = 1, kPathSplit = 3 };
+enum : int { kPathAuto = 0, kPathSeg = 1, kPathSplit = 3, kPathGraph = 4 };
 int wbfm_chain_configure(Block* b, int path, int max_segments);
 // Absolute index of the next input sample (the NCO phase origin) of a WBFM
 // chain: a time-sharded stream starts each shard's handle at its halo start

@@ -323,6 +323,23 @@ void RecBuilder::finish(uint64_t c0) {
   t.mbase = q64_of_angle(std::atan2(static_cast<long double>(t.z[2 * l + 1]), static_cast<long double>(t.z[2 * l])));
 }
 
+double rec_mean_step(float wr, float wi, uint64_t step_q64) {
+  const RecTable t = rec_table(wr, wi, RecState{}, 1ull << 18, 0, step_q64);
+  constexpr long double kTwoPi = 6.283185307179586476925286766559005768L;
+  if (t.cyc_len) {  // the advance around the cycle, increment by increment
+    long double sum = 0;
+    for (uint64_t i = 0; i < t.cyc_len; ++i) {
+      const uint64_t k = t.cyc_start + i, k1 = i + 1 < t.cyc_len ? k + 1 : t.cyc_start;
+      const long double ar = t.z[2 * k], ai = t.z[2 * k + 1], br = t.z[2 * k1], bi = t.z[2 * k1 + 1];
+      sum += std::atan2(bi * ar - br * ai, br * ar + bi * ai);  // arg(z[k1] conj z[k])
+    }
+    return static_cast<double>(sum / static_cast<long double>(t.cyc_len));
+  }
+  long double a = static_cast<long double>(t.mstep) / 18446744073709551616.0L * kTwoPi;
+  if (a > kTwoPi / 2) a -= kTwoPi;
+  return static_cast<double>(a);
+}
+
 RecTable rec_table(float wr, float wi, RecState s0, uint64_t max_out, uint64_t min_cycle, uint64_t step_q64) {
   RecBuilder b(wr, wi, s0, max_out, min_cycle, step_q64);
   b.extend(max_out);

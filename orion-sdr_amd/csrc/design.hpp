@@ -99,6 +99,10 @@ class RecBuilder {
 // The phasor of output k of a table (exact, or the model beyond it) and the state
 // after output k (for set_freq: the reference keeps z and renorm_ctr).
 RecState rec_state_after(const RecTable& t, uint64_t k);
+// The long-run phase step (radians) of the recurrence with step (wr, wi) from z = 1:
+// the exact mean over its cycle when it closes within 2^18 outputs, else the slope
+// fitted to its renorm points (RecTable mstep). step_q64: the closed-form step.
+double rec_mean_step(float wr, float wi, uint64_t step_q64);
 // Q0.64 fraction of a turn of an angle in radians.
 uint64_t q64_of_angle(long double rad);
 

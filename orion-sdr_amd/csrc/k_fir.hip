@@ -24,20 +24,14 @@ constexpr int kMaxGrid = 2048;  // memory-bound: cap and grid-stride (2048 = 8 W
 // rotator.rs:88-94), kNcoMix mix_with_nco (non-FMA product, nco.rs:63-66), kNcoGen
 // the phasors themselves (nco.rs:42-58 next_cs, no input).
 enum : int { kRotate = 0, kUsb = 1, kNcoMix = 2, kNcoGen = 3 };
-#ifndef ORION_ROT_MINW
-#define ORION_ROT_MINW 6  // waves per SIMD k_rotator is compiled for (8: <= 64 VGPRs, 6 B of spills)
-#endif
-#ifndef ORION_FIR4_TILES_PER_CU
-#define ORION_FIR4_TILES_PER_CU 4  // k_fir_iq8 with 4 outputs per lane below this many 2048-output tiles per CU
-#endif
-#ifndef ORION_ROT_HP
-#define ORION_ROT_HP 2  // pairs per thread whose loads a full tile issues together
-#endif
+constexpr int kRotMinW = 6;          // waves per SIMD k_rotator is compiled for (8: <= 64 VGPRs, 6 B of spills)
+constexpr int kFir4TilesPerCu = 4;   // k_fir_iq8 with 4 outputs per lane below this many 2048-output tiles per CU
+constexpr int kRotHp = 2;            // pairs per thread whose loads a full tile issues together
 template <bool A16, int MODE>
-__global__ __launch_bounds__(NT, ORION_ROT_MINW) void k_rotator(const f2* __restrict__ x, void* __restrict__ yv, long long n,
+__global__ __launch_bounds__(NT, kRotMinW) void k_rotator(const f2* __restrict__ x, void* __restrict__ yv, long long n,
                                                 uint64_t k0, const OscDev o) {
   constexpr int PER = kRotTile / (2 * NT);  // pairs per thread per tile (8)
-  constexpr int HP = ORION_ROT_HP;
+  constexpr int HP = kRotHp;
   const int t = threadIdx.x;
   // output pair P, P + 1 (only P when P + 1 == n) from inputs v0, v1 and phasors p0, p1
   auto emit = [&](long long P, bool full, f2 v0, f2 v1, f2 p0, f2 p1) {
@@ -233,9 +227,8 @@ __device__ __forceinline__ void dw_hist_next(const f2* __restrict__ xc, long lon
 // apart: conflict-free reads), pitch odd (the phase-scattered b64 staging stores
 // spread over banks). Per lane and tile (Q = 32): 64 ds_read_b128 against
 // k_decim_w's 136. Taps live in LDS (per-lane phases).
-#ifndef ORION_DW4_UNROLL
-#define ORION_DW4_UNROLL 4  // tap blocks unrolled: their LDS reads overlap the previous block's FMAs (1: 0.66 ms on C3, 4: 0.635)
-#endif
+// tap blocks unrolled 4 deep in k_decim_w4: their LDS reads overlap the previous block's FMAs
+// (1: 0.66 ms on C3, 4: 0.635)
 template <int Q>
 struct Dw4 {
   static constexpr int TW = 128;
@@ -302,7 +295,7 @@ __device__ __forceinline__ void dw4_tile(f2* __restrict__ U, const float* __rest
   f2 d[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) d[r] = f2{0.0f, 0.0f};
-#pragma unroll ORION_DW4_UNROLL
+#pragma unroll 4
   for (int b = 0; b < 2 * (Q / 16); ++b) {
     const int c = 2 * g + (b & 1), hq = b >> 1;
     // taps 16hq .. 16hq+15 of phase c read window entries from 2 cb, cb = Q/2 - 8 - 8hq chunks
@@ -394,7 +387,7 @@ __global__ __launch_bounds__(64, 2) void k_decim_w4(const f2* __restrict__ x, lo
 // k_decim_w4 with four waves per workgroup sharing one tap table (LDS per wave 12.9 KB
 // + 1 KB of taps per workgroup instead of per wave) and ONE tile of inputs in flight
 // per wave (<= 168 VGPRs): three waves per SIMD instead of two. Each wave still walks
-// its own range with no barrier after the tap load. ORION_DECIM_Q4=0 keeps k_decim_w4.
+// its own range with no barrier after the tap load. 
 template <int Q, bool A16, bool CLAMP>
 __global__ __launch_bounds__(256, 3) void k_decim_w4q(const f2* __restrict__ x, long long x_stride, long long n,
                                                      const f2* __restrict__ hist, int hist_len, f2* __restrict__ out,
@@ -870,9 +863,9 @@ void launch_fir_iq(const f2* x, long long n, const f2* hist, int hist_len, f2* y
                    long long off, int K, const Taps256& g, const float* g_dev, hipStream_t s, f2* hist_out) {
   if (n_out <= 0) return;
   if (K <= 256 && hist_len >= (K <= 64 ? 64 : K <= 128 ? 128 : 256)) {
-    // calls that fill fewer than ORION_FIR4_TILES_PER_CU tiles of 8 outputs per lane per CU
+    // calls that fill fewer than kFir4TilesPerCu tiles of 8 outputs per lane per CU
     // take four outputs per lane (twice the waves; the FMA work is the same)
-    const bool four = n_out < static_cast<long long>(ORION_FIR4_TILES_PER_CU) * device_cus() * 8 * NT;
+    const bool four = n_out < static_cast<long long>(kFir4TilesPerCu) * device_cus() * 8 * NT;
     if (four) {
       const int g4 = grid_for(n_out, 4 * NT);
       if (K <= 64) k_fir_iq8<64, false, 4><<<g4, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);

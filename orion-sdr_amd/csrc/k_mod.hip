@@ -125,21 +125,9 @@ __global__ __launch_bounds__(NT) void k_ssb_mod_back(const float* __restrict__ v
 //     16 pairs; base = z gain (fm.rs:66); mix_with_nco's non-FMA product with the
 //     RF Nco's phasor (nco.rs:62-66; the oscillator cursor of the chunk).
 // Against an f64 phase and a per-sample sincosf of it this is ~3x less VALU per sample.
-#ifndef ORION_FM_ABL
-#define ORION_FM_ABL 0  // experiment builds only (wrong output): 1 no look-back, 2 no RF phasor reads
-#endif
-#ifndef ORION_FM_LB
-#define ORION_FM_LB 1  // look-back records per lane and step (64 ORION_FM_LB chunks per step)
-#endif
-#ifndef ORION_FM_G
-#define ORION_FM_G 8  // RF phasor reads per thread issued together
-#endif
-#ifndef ORION_FM_FAST
-#define ORION_FM_FAST 1  // k_fm_mod_sp: full chunks without per-sample tests (0: always tested, A/B)
-#endif
-#ifndef ORION_FM_MINW
-#define ORION_FM_MINW 1  // waves per SIMD k_fm_mod_sp is compiled for (A/B: 5 = 96 VGPRs)
-#endif
+constexpr int kFmLb = 1;    // look-back records per lane and step (64 kFmLb chunks per step)
+constexpr int kFmG = 8;     // RF phasor reads per thread issued together
+constexpr int kFmMinW = 1;  // waves per SIMD k_fm_mod_sp is compiled for (A/B: 5 = 96 VGPRs was slower)
 constexpr double kTurnsPerRad = 2.9358905032820014e18;  // 2^64 / (2 pi)
 
 struct FmPairs {
@@ -188,12 +176,12 @@ __device__ __forceinline__ void fm_out(const FmPairs& p, uint64_t ph, float gain
     ys[e + (e >> 4)] = f2{z.x * gain, z.y * gain};  // fm.rs:66 base = z * gain
   }
   // the RF phasor reads in groups of G (the first group in flight across the barrier)
-  constexpr int G = ORION_FM_G;
+  constexpr int G = kFmG;
   const bool full = base + kFmCH <= n;
   f2 rp[G];
   auto rd = [&](int g) {
 #pragma unroll
-    for (int m = 0; m < G; ++m) rp[m] = (ORION_FM_ABL & 2) ? f2{1.0f, 0.0f} : osc_ld(o, R, t + NT * (g + m));
+    for (int m = 0; m < G; ++m) rp[m] = osc_ld(o, R, t + NT * (g + m));
   };
   rd(0);
   __syncthreads();
@@ -204,7 +192,7 @@ __device__ __forceinline__ void fm_out(const FmPairs& p, uint64_t ph, float gain
     for (int m = 0; m < G; ++m) {
       const int e = t + NT * (g + m);
       const f2 bz = ys[e + (e >> 4)];
-      const f2 r = (ORION_FM_ABL & 2) ? rp[m] : osc_fin(o, R, e, rp[m]);
+      const f2 r = osc_fin(o, R, e, rp[m]);
       if (FULL || full || base + e < n) y[base + e] = f2{bz.x * r.x - bz.y * r.y, bz.x * r.y + bz.y * r.x};  // nco.rs:65
     }
   }
@@ -330,7 +318,7 @@ __device__ __forceinline__ uint64_t fm_ld64(const uint32_t* p) {
   return (static_cast<uint64_t>(fm_ld(p + 1)) << 32) | fm_ld(p);
 }
 
-__global__ __launch_bounds__(NT, ORION_FM_MINW) void k_fm_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
+__global__ __launch_bounds__(NT, kFmMinW) void k_fm_mod_sp(const float* __restrict__ x, f2* __restrict__ y, long long n,
                                                   float kf, float gain, uint32_t* __restrict__ rec, uint32_t epoch,
                                                   const uint64_t* __restrict__ carry_in, uint64_t* __restrict__ carry_out,
                                                   uint64_t k0, const OscDev o, int* __restrict__ err, uint32_t spin) {
@@ -345,7 +333,7 @@ __global__ __launch_bounds__(NT, ORION_FM_MINW) void k_fm_mod_sp(const float* __
   const bool last = c == nchunk - 1;
   const long long base = static_cast<long long>(c) * kFmCH;
   // a full chunk (not the call's last): the staging, pairs and stores without per-sample tests
-  const bool fast = ORION_FM_FAST && !last;
+  const bool fast = !last;
   FmPairs p;
   const int e = t * kFmC;
   uint64_t q;
@@ -368,8 +356,8 @@ __global__ __launch_bounds__(NT, ORION_FM_MINW) void k_fm_mod_sp(const float* __
     uint64_t excl = 0;
     // lane l reads the records of chunks b - L l - j, j < L: 64 L predecessors per step,
     // their flag loads all issued before any is tested
-    constexpr int L = ORION_FM_LB;
-    for (int b = c - 1; !(ORION_FM_ABL & 1); b -= 64 * L) {
+    constexpr int L = kFmLb;
+    for (int b = c - 1;; b -= 64 * L) {
       // every flag load of the step issued at once (clamped index; no short-circuit
       // that would serialise them), then every value load
       uint32_t f6[L], f7[L];

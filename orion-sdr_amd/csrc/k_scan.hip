@@ -11,42 +11,14 @@ constexpr int C = kScanC;
 constexpr int NT = kScanNT;
 constexpr int CH = kScanCH;
 constexpr int PADN = CH + CH / 16 + 16;
-#ifndef ORION_SP_ABL
-#define ORION_SP_ABL 0  // timing experiments only: 1 no phasor table, 2 no look-back, 4 no LP scan, 8 staging + stores only
-                        // (k_lpdc_sp); 16 no wait, 32 staging + stores only, 64 no zero-state pass,
-                        // 128 no re-run (k_scan_sp)
-#endif
-#ifndef ORION_SP_MINW
-#define ORION_SP_MINW 4  // waves per SIMD k_lpdc_sp is compiled for at kSpC samples per lane (<= 128 VGPRs)
-#endif
-#ifndef ORION_SP_MINW16
-#define ORION_SP_MINW16 6  // the same at 16 samples per lane (ORION_LPDC_SC=16 experiments)
-#endif
-#ifndef ORION_SP_ZMAP
-#define ORION_SP_ZMAP 1  // k_scan_sp: zero-state pass as the linear map (0: the recurrence, A/B)
-#endif
-#ifndef ORION_SP_BATCH
-#define ORION_SP_BATCH 8  // k_scan_sp staging: loads issued together per thread (complex input)
-#endif
-#ifndef ORION_SP_BATCH_REAL
-#define ORION_SP_BATCH_REAL 8  // (real input)
-#endif
-#ifndef ORION_SCAN_SP_MINW
-#define ORION_SCAN_SP_MINW 4  // waves per SIMD k_scan_sp is compiled for (4: <= 128 VGPRs, spills 52-132 B)
-#endif
-#ifndef ORION_SP_MPOW
-#define ORION_SP_MPOW 1  // k_lpdc_sp DC pass: lane-level warm-up test, r^v by squaring (0: per-sample guards and product, A/B)
-#endif
-#ifndef ORION_SP_FAST
-#define ORION_SP_FAST 1  // k_lpdc_sp: unguarded per-sample loops in full, non-final chunks (0: always guarded, A/B)
-#endif
-#ifndef ORION_SP_SSBMASK
-#define ORION_SP_SSBMASK 6  // k_lpdc_sp Ssb: which loops take the unguarded copies (1 LP re-run, 2 DC zero-state,
-                            // 4 DC re-run, 8 stores); 6 measured best (r4_lpdc_guard_ab.txt), 1 and 8 slower
-#endif
-#ifndef ORION_SP_TRUNC
-#define ORION_SP_TRUNC 1  // k_lpdc_sp: the LP4 lane scan truncated to the forgetting horizon (0: full two-scan form)
-#endif
+// Tuning constants (each measured A/B; HISTORY.md):
+constexpr int kSpMinW = 4;       // waves per SIMD k_lpdc_sp is compiled for at kSpC samples per lane (<= 128 VGPRs)
+constexpr int kSpMinW16 = 6;     // the same at 16 samples per lane
+constexpr int kSpBatch = 8;      // k_scan_sp staging: loads issued together per thread (complex input)
+constexpr int kSpBatchReal = 8;  // (real input)
+constexpr int kScanSpMinW = 4;   // waves per SIMD k_scan_sp is compiled for (4: <= 128 VGPRs, spills 52-132 B)
+constexpr int kSpSsbMask = 6;    // k_lpdc_sp Ssb: which loops take the unguarded copies (1 LP re-run, 2 DC
+                                 // zero-state, 4 DC re-run, 8 stores); 6 measured best (r4_lpdc_guard_ab.txt)
 
 __device__ __forceinline__ int pos(int e) { return e + (e >> 4); }
 
@@ -570,7 +542,7 @@ __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long ba
 }
 
 template <Pre PR, int SC>
-__global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void k_lpdc_sp(const ScanArgs a, const double* __restrict__ mlp, int nch,
+__global__ __launch_bounds__(NT, SC > 16 ? kSpMinW : kSpMinW16) void k_lpdc_sp(const ScanArgs a, const double* __restrict__ mlp, int nch,
                                                uint32_t* __restrict__ rec, uint32_t epoch) {
   constexpr int S = 4;
   constexpr int C = SC, CH = SC * NT, PADN = CH + CH / SC + SC;
@@ -602,16 +574,6 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
   const float r = a.c.r;
   stage_sp<PR, SC>(a, ch, base, cnt, sb);
   wave_order();  // wave-local staging
-  if constexpr ((ORION_SP_ABL & 8) != 0) {  // timing floor: staging and stores only
-    float* yo = static_cast<float*>(a.y) + ch * a.y_stride + o0;
-    const int e0 = wave * (64 * SC) + lane;
-#pragma unroll
-    for (int k = 0; k < SC; ++k) {
-      const int e2 = e0 + 64 * k;
-      if (e2 >= warm && e2 < cnt) yo[e2 - warm] = sb[posS<SC>(e2)];
-    }
-    return;
-  }
 
   // ---- LP4: zero-state lane aggregates, block scan, exact re-run ----
   // Guards on the element range: the lane's valid samples are i < hi (the staged samples
@@ -620,18 +582,16 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
   // staging) only the DC loops': its LP4 re-run and store copies measured slower
   // (r4_lpdc_guard_ab.txt).
   const int hi = min(cnt - t * C, C);
-  const bool full_nl = ORION_SP_FAST && cnt == CH && !last;
+  const bool full_nl = cnt == CH && !last;
   const bool fast = PR != Pre::Ssb && full_nl;
   // per loop for Ssb (A/B mask): 1 LP re-run, 2 DC zero-state, 4 DC re-run, 8 stores
-  auto fast_for = [&](int bit) { return PR == Pre::Ssb ? ((ORION_SP_SSBMASK & bit) != 0 && full_nl) : fast; };
+  auto fast_for = [&](int bit) { return PR == Pre::Ssb ? ((kSpSsbMask & bit) != 0 && full_nl) : fast; };
   float xs[C];
 #pragma unroll
   for (int i = 0; i < C; ++i) xs[i] = sb[posS<SC>(t * C + i)];
   float ef[S] = {0, 0, 0, 0};
   if constexpr (LP) {
   float s0[S] = {0, 0, 0, 0};
-#if !(ORION_SP_ABL & 4)
-#if ORION_SP_ZMAP
   {  // the lane run's zero-state end state as the linear map (k_scan_sp)
     const float* __restrict__ E = a.zmap;
 #pragma unroll
@@ -639,17 +599,10 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
 #pragma unroll
       for (int k = 0; k < S; ++k) s0[k] = __builtin_fmaf(E[i * S + k], xs[i], s0[k]);  // zeros past cnt (staging)
   }
-#else
-#pragma unroll
-  for (int i = 0; i < C; ++i)
-    if (t * C + i < cnt) (void)lp.step(s0, xs[i]);
-#endif
-#endif
   double q[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) q[i] = s0[i];
   double e[S];
-#if ORION_SP_TRUNC
   // Truncated scan: the LP4 forgets its state within kSpWarm samples (the host checks
   // ||A^kSpWarm|| < 1e-10, the warm-up's own criterion), i.e. within NL lane runs, so
   // the state entering lane L is sum_{i = 1..NL} A^{C(i-1)} s0[L - i] to that bound:
@@ -681,35 +634,6 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
     for (int i = 0; i < S; ++i) v[i] = wave > 0 ? tot[wave - 1][i] : static_cast<double>(ci[i]);
     matvec_acc<S>(mlp + (ScanMatsLayout::kLane + lane * (SC / kScanC)) * S * S, v, e);
   }
-#else
-  wave_scan_inclusive<S>(q, mlp + kPw * S * S, lane);
-  if (lane == 63)
-#pragma unroll
-    for (int i = 0; i < S; ++i) tot[wave][i] = q[i];
-  __syncthreads();
-  double cw[S];
-#pragma unroll
-  for (int i = 0; i < S; ++i) cw[i] = c == 0 ? static_cast<double>(ci[i]) : 0.0;
-  for (int w = 0; w < wave; ++w) {
-    double v[S];
-#pragma unroll
-    for (int i = 0; i < S; ++i) v[i] = tot[w][i];
-    matvec_acc<S>(mlp + kWv * S * S, cw, v);
-#pragma unroll
-    for (int i = 0; i < S; ++i) cw[i] = v[i];
-  }
-  // the wave's entering state folded into lane 0 and the wave re-scanned (a
-  // per-lane transition matrix would be 128 B of global reads per lane)
-#pragma unroll
-  for (int i = 0; i < S; ++i) q[i] = s0[i];
-  if (lane == 0) matvec_acc<S>(mlp + kPw * S * S, cw, q);  // pw[0] = A^C
-  wave_scan_inclusive<S>(q, mlp + kPw * S * S, lane);
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    const double o = __shfl_up(q[i], 1, 64);
-    e[i] = lane == 0 ? cw[i] : o;
-  }
-#endif
 #pragma unroll
   for (int i = 0; i < S; ++i) ef[i] = static_cast<float>(e[i]);
   auto lp_rerun = [&](auto guarded) {
@@ -742,7 +666,6 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
   double m = 1.0, d = 0.0;
   // the warm-up is a whole number of lane runs: a lane is inside it or past it
   const bool lane_on = t * C >= warm;
-#if ORION_SP_MPOW
   {
     float y = 0.0f;
     auto dc_zero = [&](auto guarded) {
@@ -766,21 +689,6 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
       p *= p;
     }
   }
-#else
-  {
-    float xp = xprev0, y = 0.0f;
-#pragma unroll
-    for (int i = 0; i < C; ++i) {
-      const int ei = t * C + i;
-      if (ei >= warm && ei < cnt) {
-        y = (xs[i] - xp) + r * y;
-        m *= static_cast<double>(r);
-      }
-      xp = xs[i];
-    }
-    d = y;
-  }
-#endif
   // inclusive scan of (m, d) over the wave, then over the waves
   double mi = m, di = d;
 #pragma unroll
@@ -847,7 +755,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
     // or beyond), and ends at latest once the walked product of r^len is below 1e-20.
     const float lr = static_cast<float>(CH - warm) * __logf(r);
     const int K = !(r > 0.0f) ? 1 : (lr < 0.0f ? static_cast<int>(min(64.0f, ceilf(-46.06f / lr))) : 64);
-    for (int base = c - 1; !(ORION_SP_ABL & 2); base -= 64) {
+    for (int base = c - 1;; base -= 64) {
       const int k = base - lane;
       double v = 0.0, mk = 1.0;
       bool closes = true;
@@ -902,7 +810,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
 #pragma unroll
     for (int i = 0; i < C; ++i) {
       float out = 0.0f;
-      if (!decltype(guarded)::value || (ORION_SP_MPOW ? i < hi : (t * C + i >= warm && t * C + i < cnt))) {
+      if (!decltype(guarded)::value || i < hi) {
         y = (xs[i] - xp) + r * y;  // dsp/iir.rs:161 (y1 - dc_x1) + r * dc_y1
         out = y;
       }
@@ -962,7 +870,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? ORION_SP_MINW : ORION_SP_MINW16) void
 // picks the smallest H in {256, 512, 1024} samples with ||A^H|| < 1e-10): the lane scan
 // truncated to TRS steps, as in k_lpdc_sp. TRS = 0: the full scan and re-scan.
 template <RecK RK, Pre PR, Post PO, int TRS>
-__global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanArgs a, int nch, uint32_t* __restrict__ rec,
+__global__ __launch_bounds__(NT, kScanSpMinW) void k_scan_sp(const ScanArgs a, int nch, uint32_t* __restrict__ rec,
                                                    uint32_t epoch) {
   using R = typename RecSel<RK>::T;
   constexpr int S = R::S;
@@ -988,14 +896,14 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   // (unconditional, index clamped into [0, n)), then the pre-map. (A guarded load per
   // sample compiles to a branch around each, which waits for its load before the LDS
   // store: one memory latency per sample.) FM / PM also load x[i - 1] (an L1/L2 hit).
-  constexpr int BT = PR == Pre::Real ? ORION_SP_BATCH_REAL : PR == Pre::Pm ? 8 : ORION_SP_BATCH;  // loads per thread at once
+  constexpr int BT = PR == Pre::Real ? kSpBatchReal : PR == Pre::Pm ? 8 : kSpBatch;  // loads per thread at once
   static_assert(SC % BT == 0 && BT <= 64 && CH <= kOscSpan, "staging batches; one oscillator cursor per chunk");
   // FM: the previous sample from the neighbour lane (below); PM: its own load of x[i - 1]
   // (an L1/L2 hit; the neighbour form measured 6 % slower there: more spills)
   constexpr bool kPair = PR == Pre::Fm, kPrev = PR == Pre::Pm;
   const long long nl = a.n - 1;
   // a full chunk that is not the call's last: no index clamps, no store guards (below)
-  const bool fast = ORION_SP_FAST && cnt == CH && !last;
+  const bool fast = cnt == CH && !last;
   auto stage = [&](auto guarded) {
   constexpr bool G = decltype(guarded)::value;
 #pragma unroll 1
@@ -1042,11 +950,6 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   if (fast) stage(std::false_type{});
   else stage(std::true_type{});
   __syncthreads();
-  if constexpr ((ORION_SP_ABL & 32) != 0) {  // timing floor: staging and stores only
-    float* y = static_cast<float*>(a.y) + ch * a.y_stride + base;
-    for (int e2 = t; e2 < cnt; e2 += NT) y[e2] = sb[posS<SC>(e2)];
-    return;
-  }
 
   // `fast` (block-uniform: a full chunk that is not the call's last) selects unguarded
   // copies of the per-sample loops (as k_lpdc_sp)
@@ -1056,8 +959,7 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   float s0[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) s0[i] = 0.0f;
-  if constexpr ((ORION_SP_ABL & 64) != 0) {
-  } else if constexpr (ORION_SP_ZMAP != 0) {
+  {
     // the lane run's zero-state end state as the linear map sum_i A^(C-1-i) B x_i
     // (independent FMAs instead of the recurrence's dependent chain; samples past the
     // chunk enter as zeros: only the last partial lane differs, whose state reaches no
@@ -1073,10 +975,6 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
     };
     if (fast) zs(std::false_type{});
     else zs(std::true_type{});
-  } else {
-#pragma unroll
-    for (int i = 0; i < C; ++i)
-      if (t * C + i < cnt) (void)rr.step(s0, xs[i]);
   }
   double q[S];
 #pragma unroll
@@ -1124,14 +1022,9 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
       for (int i = 0; i < S; ++i) cin_sh[i] = static_cast<double>(ci[i]);
     } else {
       const uint32_t* pr = rec + (static_cast<long long>(ch) * nchunk + c - 1) * 16;
-      if constexpr ((ORION_SP_ABL & 16) != 0) {
-#pragma unroll
-        for (int i = 0; i < S; ++i) cin_sh[i] = 0.0;
-      } else {
       if (!sp_wait2(pr + 15, pr + 15, epoch, a.spin)) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #pragma unroll
       for (int i = 0; i < S; ++i) cin_sh[i] = sp_ld64(pr + 2 * i);
-      }
     }
   }
   __syncthreads();
@@ -1177,7 +1070,7 @@ __global__ __launch_bounds__(NT, ORION_SCAN_SP_MINW) void k_scan_sp(const ScanAr
   auto rerun = [&](auto guarded) {
 #pragma unroll
     for (int i = 0; i < C; ++i)
-      if (!(ORION_SP_ABL & 128) && (!decltype(guarded)::value || t * C + i < cnt))
+      if (!decltype(guarded)::value || t * C + i < cnt)
         xs[i] = postmap<PO>(a, rr.step(ef, xs[i]));  // the reference's f32 update
   };
   if (fast) rerun(std::false_type{});
@@ -1237,7 +1130,7 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
   const OscRun Rr = osc_run(rf, k0 + static_cast<uint64_t>(base), cnt);
   // `fast` (block-uniform: a full chunk that is not the call's last): unguarded copies of
   // the per-sample loops (as k_lpdc_sp)
-  const bool fast = ORION_SP_FAST && cnt == CH && !last;
+  const bool fast = cnt == CH && !last;
   auto stage = [&](auto guarded) {  // x p.re, x p.im (ssb.rs:53-54), coalesced loads first
     constexpr bool G = decltype(guarded)::value;
     float v[C];
@@ -1261,31 +1154,22 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
   __syncthreads();
   float xs[2][C];
   float s0[2][S];
-#if ORION_SP_TRUNC
   double qt[2][S];  // truncated scan (k_lpdc_sp): NL = kSpWarm / C lane runs span the horizon
   constexpr int NL = kSpWarm / C, STEPS = NL == 16 ? 4 : NL == 8 ? 3 : 5;
   static_assert(NL == (1 << STEPS) && NL * C / kScanC < 64, "truncated scan geometry");
-#endif
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
 #pragma unroll
     for (int i = 0; i < C; ++i) xs[b][i] = sb[b][pos(t * C + i)];
 #pragma unroll
     for (int k = 0; k < S; ++k) s0[b][k] = 0.0f;
-#if ORION_SP_ZMAP
 #pragma unroll
     for (int i = 0; i < C; ++i)  // the lane run's zero-state end state as the linear map (k_scan_sp)
 #pragma unroll
       for (int k = 0; k < S; ++k) s0[b][k] = __builtin_fmaf(zmap[i * S + k], xs[b][i], s0[b][k]);  // staged zeros past cnt
-#else
-#pragma unroll
-    for (int i = 0; i < C; ++i)
-      if (t * C + i < cnt) (void)lp.step(s0[b], xs[b][i]);
-#endif
     double q[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) q[k] = s0[b][k];
-#if ORION_SP_TRUNC
 #pragma unroll 1
     for (int st = 0; st < STEPS; ++st) {
       double o[S];
@@ -1295,9 +1179,6 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
     }
 #pragma unroll
     for (int k = 0; k < S; ++k) qt[b][k] = q[k];
-#else
-    wave_scan_inclusive<S>(q, mlp + ScanMatsLayout::kPwc * S * S, lane);
-#endif
     if (lane == 63)
 #pragma unroll
       for (int k = 0; k < S; ++k) tot[b][wave][k] = q[k];
@@ -1305,7 +1186,6 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
   __syncthreads();
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
-#if ORION_SP_TRUNC
     double e[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) {
@@ -1321,31 +1201,6 @@ __global__ __launch_bounds__(NT, 3) void k_ssb_mod_sp(const float* __restrict__ 
     float ef[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) ef[k] = static_cast<float>(e[k]);
-#else
-    double cw[S];
-#pragma unroll
-    for (int k = 0; k < S; ++k) cw[k] = c == 0 ? static_cast<double>(carry_in[4 * b + k]) : 0.0;
-    for (int w = 0; w < wave; ++w) {
-      double v[S];
-#pragma unroll
-      for (int k = 0; k < S; ++k) v[k] = tot[b][w][k];
-      matvec_acc<S>(mlp + ScanMatsLayout::kM64 * S * S, cw, v);
-#pragma unroll
-      for (int k = 0; k < S; ++k) cw[k] = v[k];
-    }
-    // the wave's entering state folded into lane 0, the wave re-scanned
-    double q[S];
-#pragma unroll
-    for (int k = 0; k < S; ++k) q[k] = s0[b][k];
-    if (lane == 0) matvec_acc<S>(mlp + ScanMatsLayout::kPwc * S * S, cw, q);
-    wave_scan_inclusive<S>(q, mlp + ScanMatsLayout::kPwc * S * S, lane);
-    float ef[S];
-#pragma unroll
-    for (int k = 0; k < S; ++k) {
-      const double o = __shfl_up(q[k], 1, 64);
-      ef[k] = static_cast<float>(lane == 0 ? cw[k] : o);
-    }
-#endif
     auto rerun = [&](auto guarded) {
 #pragma unroll
       for (int i = 0; i < C; ++i)

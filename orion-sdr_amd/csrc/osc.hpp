@@ -41,6 +41,7 @@ class RefOsc {
   OscDev dev(uint64_t n, hipStream_t s);
   uint64_t count() const { return k_; }
   void advance(uint64_t n) { k_ += n; }
+  void seek(uint64_t k) { k_ = k; }  // the next output index (tabulated on demand by dev())
   const Oscillator& osc() const { return osc_; }
   float fs() const { return fs_; }
 

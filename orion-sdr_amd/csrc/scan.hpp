@@ -91,11 +91,7 @@ long long lpdc_sp_chunks(long long n);
 // chunks of kSpCH samples.
 constexpr int kSpC = 2 * kScanC;
 constexpr int kSpCH = kSpC * kScanNT;
-// k_lpdc_sp's samples per lane (timing experiments: -DORION_LPDC_SC=16 halves its chunks)
-#ifndef ORION_LPDC_SC
-#define ORION_LPDC_SC 32
-#endif
-constexpr int kLpdcSC = ORION_LPDC_SC;
+constexpr int kLpdcSC = 32;  // k_lpdc_sp's samples per lane
 long long lpdc_sp_demod_chunks(long long n, int sc, int warm);  // warm: kSpWarm, or 0 for the DcBlocker alone
 // SsbPhasingMod in one pass (k_ssb_mod_sp): valid when ||A_lp^kSpWarm|| is
 // negligible; mats_lp = the LP4 scan matrices; carry = [I 4][Q 4] floats.

@@ -258,7 +258,7 @@ class _Block:
 
     def process_device(self, x, out=None, stream=None):
         """Device buffers (torch CUDA tensors). Asynchronous on `stream`
-        (default: torch's current stream). Returns (out, WorkReport)."""
+        (default: torch's current stream). Returns out (its first out_written samples)."""
         import torch
 
         if not x.is_cuda or not x.is_contiguous():
@@ -630,7 +630,7 @@ class WbfmChain(_Block):
         super().__init__(h)
         self.m = int(m)
 
-    _PATHS = {"auto": 0, "segmented": 1, "split": 3}
+    _PATHS = {"auto": 0, "segmented": 1, "split": 3, "graph": 4}
 
     def configure(self, path: str = "auto", max_segments: int = 0):
         """Engine tuning / tests (no reference counterpart): the kernel path and a

@@ -1,5 +1,5 @@
 """A/B of k_wbfm_seg build variants (orion-sdr_amd/exp/<name>/liborion_sdr_amd.so,
-built by scripts/build_exp.sh) on the C2 workload: each variant runs in its own
+built by scripts/build_variant.sh from a git revision) on the C2 workload: each variant runs in its own
 process (ORION_SDR_LIB), rounds interleaved so that clock drift hits every variant
 alike; per process W warm-up and K timed launches, HIP events around each launch
 on the launch stream. Prints per-variant medians over rounds.
