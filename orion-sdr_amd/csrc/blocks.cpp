@@ -973,15 +973,17 @@ class WbfmBlock final : public Block {
     lanemats_.upload(lm.data(), lm.size() * sizeof(double));
     // segmented chain constants: steps A^(kSgC 2^s), and A^(kSgL/2)
     std::memset(&cs_, 0, sizeof(cs_));
-    for (size_t k = 0; k < a.size(); ++k) cs_.a[k] = a[k];
     cs_.b0 = bq.b0; cs_.b1 = bq.b1; cs_.b2 = bq.b2; cs_.a1 = bq.a1; cs_.a2 = bq.a2;
+    std::vector<double> mats(kWbfmMats);
     auto ps = mat_pow(ss.A, 4, kSgC);
     for (int s = 0; s < 6; ++s) {
-      for (int i = 0; i < 16; ++i) cs_.pw[s * 16 + i] = ps[i];
+      for (int i = 0; i < 16; ++i) mats[s * 16 + i] = ps[i];
       ps = mat_mul(ps, ps, 4);
     }
     const auto msh = mat_pow(ss.A, 4, kSgL / 2);
-    for (int i = 0; i < 16; ++i) cs_.mh[i] = msh[i];
+    for (int i = 0; i < 16; ++i) mats[6 * 16 + i] = msh[i];
+    mats_.upload(mats.data(), mats.size() * sizeof(double));
+    cs_.mats = mats_.as<double>();
     build_audio_frags(a);
     // The segmented chain starts every segment's first sub-range from a zero state and
     // hands the next sub-range that sub-range's zero-state end state and last 128
@@ -1075,7 +1077,7 @@ class WbfmBlock final : public Block {
   bool fused_ok_ = false, seg_ok_ = false, split_ok_ = false;
   int path_ = kPathAuto, max_seg_ = 0;
   uint32_t epoch_ = 0;
-  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, hand_, flags_, trace_, afrag_, mixed_, dec_;
+  DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, hand_, flags_, trace_, afrag_, mixed_, dec_, mats_;
   std::vector<Stages> stages_;
   uint64_t seek_ = 0;
   int cur_ = 0;

@@ -22,7 +22,7 @@
 // chunk's recorded entry agrees again, then searches for the next disagreement.
 // Every output is therefore the reference's sequential f32 result. Typical
 // signals need no re-run; a long constant stretch (the ADVICE case) degrades to an
-// in-order walk of the stretch (agc_wave_walk, ~27 ns per sample), never to a
+// in-order walk of the stretch (agc_wave_walk), never to a
 // wrong answer.
 //
 // Per sample: the reference's f32 ops in its order, no FMA contraction
@@ -68,7 +68,11 @@ struct AgcPol {
   __device__ __forceinline__ bool up(float d, float env) const { return d > env; }
   __device__ __forceinline__ float seed(float env, float d0) const { return env == 0.0f ? fmaxf(d0, 1e-12f) : env; }
   __device__ __forceinline__ float warm_seed(float d) const { return fmaxf(d, 1e-12f); }
-  __device__ __forceinline__ Out out(In v, float env, long long) const {
+  static constexpr bool kBracket = false;  // the envelope (a power) has no a-priori bound
+  static constexpr float kLo = 0.0f, kHi = 0.0f;
+  struct Aux {};
+  __device__ __forceinline__ Aux aux(long long) const { return {}; }
+  __device__ __forceinline__ Out out(In v, float env, Aux) const {
     const float rms = fmaxf(sqrtf(env), 1e-6f);
     const float g = fminf(fmaxf(k.tgt / rms, k.gmin), k.gmax);
     if constexpr (IQ) return make_float2(g * v.x, g * v.y);
@@ -85,9 +89,16 @@ struct CwPol {
   __device__ __forceinline__ bool up(float d, float env) const { return d >= env; }
   __device__ __forceinline__ float seed(float env, float) const { return env; }
   __device__ __forceinline__ float warm_seed(float d) const { return d; }
-  __device__ __forceinline__ Out out(In, float env, long long i) const {
+  // env stays in [0, 1] (convex combinations of env_0 = 0 and clamped targets; in f32
+  // too: a + (1 - a) rounds to 1): a warm-up from both ends brackets the true envelope
+  static constexpr bool kBracket = true;
+  static constexpr float kLo = 0.0f, kHi = 1.0f;
+  // the tone Nco's phasor of sample i (a table read: the walks issue a batch's reads
+  // with its inputs, ahead of the envelope chain)
+  using Aux = f2;
+  __device__ __forceinline__ Aux aux(long long i) const { return osc_at(osc, k0 + static_cast<uint64_t>(i)); }
+  __device__ __forceinline__ Out out(In, float env, Aux p) const {
     const float m = env * gain;
-    const f2 p = osc_at(osc, k0 + static_cast<uint64_t>(i));
     return make_float2(m * p.x - 0.0f * p.y, m * p.y + 0.0f * p.x);
   }
 };
@@ -100,6 +111,49 @@ template <class Pol, bool OUT>
 __device__ __forceinline__ float agc_walk(const typename Pol::In* __restrict__ x, typename Pol::Out* __restrict__ y,
                                           long long s, long long e, float env, const Pol& P) {
   using T = typename Pol::In;
+  using A = typename Pol::Aux;
+  T cur[kB], nxt[kB];
+  A ca[kB], na[kB];
+#pragma unroll
+  for (int j = 0; j < kB; ++j) {
+    cur[j] = s + j < e ? x[s + j] : T{};
+    if constexpr (OUT) ca[j] = s + j < e ? P.aux(s + j) : A{};
+  }
+  for (long long base = s; base < e; base += kB) {
+    const long long nb = base + kB;
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      nxt[j] = nb + j < e ? x[nb + j] : T{};
+      if constexpr (OUT) na[j] = nb + j < e ? P.aux(nb + j) : A{};
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      const long long i = base + j;
+      const float d = P.drive(cur[j]);
+      const bool up = P.up(d, env);
+      const float ne = (up ? P.att : P.rel) * env + (up ? P.oma : P.omr) * d;  // agc.rs:40, cw.rs:58-62
+      if (i < e) {
+        env = ne;
+        if constexpr (OUT) y[i] = P.out(cur[j], env, ca[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kB; ++j) {
+      cur[j] = nxt[j];
+      if constexpr (OUT) ca[j] = na[j];
+    }
+  }
+  return env;
+}
+
+// Two trajectories over [s, e) (envelope only), from the bracket's ends: once they meet
+// they stay equal (the same map), and the maps are monotone in env, so the true envelope,
+// which starts between them, meets them too. Returns whether they met by e (the merged
+// envelope in lo); exactness is still checked bitwise (k_agc_check).
+template <class Pol>
+__device__ __forceinline__ bool agc_walk2(const typename Pol::In* __restrict__ x, long long s, long long e, float& lo,
+                                          float& hi, const Pol& P) {
+  using T = typename Pol::In;
   T cur[kB], nxt[kB];
 #pragma unroll
   for (int j = 0; j < kB; ++j) cur[j] = s + j < e ? x[s + j] : T{};
@@ -109,77 +163,111 @@ __device__ __forceinline__ float agc_walk(const typename Pol::In* __restrict__ x
     for (int j = 0; j < kB; ++j) nxt[j] = nb + j < e ? x[nb + j] : T{};
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
-      const long long i = base + j;
       const float d = P.drive(cur[j]);
-      const bool up = P.up(d, env);
-      const float ne = (up ? P.att : P.rel) * env + (up ? P.oma : P.omr) * d;  // agc.rs:40, cw.rs:58-62
-      if (i < e) {
-        env = ne;
-        if constexpr (OUT) y[i] = P.out(cur[j], env, i);
+      const bool ul = P.up(d, lo), uh = P.up(d, hi);
+      const float nl = (ul ? P.att : P.rel) * lo + (ul ? P.oma : P.omr) * d;
+      const float nh = (uh ? P.att : P.rel) * hi + (uh ? P.oma : P.omr) * d;
+      if (base + j < e) {
+        lo = nl;
+        hi = nh;
       }
     }
 #pragma unroll
     for (int j = 0; j < kB; ++j) cur[j] = nxt[j];
+    if (__float_as_uint(lo) == __float_as_uint(hi)) {  // met: one trajectory for the rest
+      lo = agc_walk<Pol, false>(x, nullptr, nb < e ? nb : e, e, lo, P);
+      hi = lo;
+      return true;
+    }
   }
-  return env;
+  return __float_as_uint(lo) == __float_as_uint(hi);
 }
+constexpr unsigned kNanEnt = 0x7FC00001u, kNanExt = 0x7FC00002u;  // unknown entry / exit: never equal
 
-// One wave walks samples [s, e) in order from env (the re-runs of k_agc_fix, the
-// sequential path and the long-warm-up chunks of k_agc_wave). The 64 lanes load 64
-// samples and form d and both candidate (1 - a) * d products; the envelope chain
-// itself is uniform across the wave (d and the products read lane by lane: compare,
-// two selects, one multiply, one add per sample), then every lane forms its
-// sample's output. Same f32 ops and roundings as the reference's per-sample
-// update. OUT = false: envelope only (a warm-up).
-template <class Pol, bool OUT = true>
-__device__ __forceinline__ float agc_wave_walk(const typename Pol::In* __restrict__ x,
-                                               typename Pol::Out* __restrict__ y, long long s, long long e, float env,
-                                               const Pol& P) {
+// One wave walks samples [s, e) in order (the re-runs of k_agc_fix and k_agc_fix_runs,
+// the sequential path and the wave-per-chunk pass 1). The 64 lanes load 64 samples
+// (coalesced, the next 64 in flight) and form d and both candidate (1 - a) * d products
+// into LDS (sm: 3 x 64 floats of this wave); then every lane runs the envelope chain over
+// the 64 values read back as broadcast b128 reads, 16 at a time (compare, two selects,
+// one multiply, one add per sample: the reference's f32 ops and order), and keeps its
+// own sample's envelope; then every lane forms its sample's output. NT trajectories
+// (1, or 2 for a bracketed warm-up: from env[0] and env[1]) share the broadcast values.
+// (The chain formerly read the values by v_readlane: ~27 ns per sample.)
+template <class Pol, bool OUT, int NT>
+__device__ __forceinline__ void agc_wave_walk_n(const typename Pol::In* __restrict__ x,
+                                                typename Pol::Out* __restrict__ y, long long s, long long e,
+                                                float (&env)[NT], const Pol& P, float* __restrict__ sm) {
   using T = typename Pol::In;
+  using A = typename Pol::Aux;
   const int lane = threadIdx.x & 63;
   T cur = s + lane < e ? x[s + lane] : T{};
+  A ca{};
+  if constexpr (OUT) ca = s + lane < e ? P.aux(s + lane) : A{};
   for (long long base = s; base < e; base += 64) {
     const long long i = base + lane;
     const T nxt = i + 64 < e ? x[i + 64] : T{};
+    A na{};
+    if constexpr (OUT) na = i + 64 < e ? P.aux(i + 64) : A{};
     const float d = P.drive(cur);
-    const float pa = P.oma * d, pr = P.omr * d;
+    asm volatile("" ::: "memory");  // the previous block's broadcast reads precede these writes (one wave: DS in order)
+    sm[lane] = d;
+    sm[64 + lane] = P.oma * d;
+    sm[128 + lane] = P.omr * d;
+    asm volatile("" ::: "memory");
     const int cnt = e - base < 64 ? static_cast<int>(e - base) : 64;
     float mine = 0.0f;
-    if (cnt == 64) {
+    auto chain = [&](auto full) {
 #pragma unroll
-      for (int j = 0; j < 64; ++j) {
-        const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), j));
-        const float aj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pa), j));
-        const float rj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pr), j));
-        const bool up = P.up(xj, env);
-        env = (up ? P.att : P.rel) * env + (up ? aj : rj);
-        if constexpr (OUT) mine = lane == j ? env : mine;
+      for (int q = 0; q < 64; q += 16) {
+        float dv[16], av[16], rv[16];
+#pragma unroll
+        for (int t = 0; t < 16; t += 4) {
+          const float4 u = *reinterpret_cast<const float4*>(sm + q + t);
+          const float4 v = *reinterpret_cast<const float4*>(sm + 64 + q + t);
+          const float4 w = *reinterpret_cast<const float4*>(sm + 128 + q + t);
+          dv[t] = u.x; dv[t + 1] = u.y; dv[t + 2] = u.z; dv[t + 3] = u.w;
+          av[t] = v.x; av[t + 1] = v.y; av[t + 2] = v.z; av[t + 3] = v.w;
+          rv[t] = w.x; rv[t + 1] = w.y; rv[t + 2] = w.z; rv[t + 3] = w.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (decltype(full)::value || q + j < cnt) {
+#pragma unroll
+            for (int k = 0; k < NT; ++k) {
+              const bool up = P.up(dv[j], env[k]);
+              env[k] = (up ? P.att : P.rel) * env[k] + (up ? av[j] : rv[j]);
+            }
+            if constexpr (OUT) mine = lane == q + j ? env[0] : mine;
+          }
+        }
       }
-    } else {
-      for (int j = 0; j < cnt; ++j) {
-        const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), j));
-        const float aj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pa), j));
-        const float rj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pr), j));
-        const bool up = P.up(xj, env);
-        env = (up ? P.att : P.rel) * env + (up ? aj : rj);
-        if constexpr (OUT) mine = lane == j ? env : mine;
-      }
-    }
+    };
+    if (cnt == 64) chain(std::true_type{});
+    else chain(std::false_type{});
     if constexpr (OUT) {
-      if (i < e) y[i] = P.out(cur, mine, i);
+      if (i < e) y[i] = P.out(cur, mine, ca);
+      ca = na;
     }
     cur = nxt;
   }
-  return env;
+}
+template <class Pol, bool OUT = true>
+__device__ __forceinline__ float agc_wave_walk(const typename Pol::In* __restrict__ x,
+                                               typename Pol::Out* __restrict__ y, long long s, long long e, float env,
+                                               const Pol& P, float* __restrict__ sm) {
+  float v[1] = {env};
+  agc_wave_walk_n<Pol, OUT, 1>(x, y, s, e, v, P, sm);
+  return v[0];
 }
 
 // The whole call in order by one wave (warm-ups as long as the call itself).
 template <class Pol>
 __global__ __launch_bounds__(64) void k_agc_seq(const void* __restrict__ in, void* __restrict__ out, long long n,
                                                 Pol P, const float* __restrict__ env_in, float* __restrict__ env_out) {
+  __shared__ __attribute__((aligned(16))) float sm[192];
   const auto* x = static_cast<const typename Pol::In*>(in);
   float env = P.seed(env_in[0], P.drive(x[0]));
-  env = agc_wave_walk<Pol>(x, static_cast<typename Pol::Out*>(out), 0, n, env, P);
+  env = agc_wave_walk<Pol>(x, static_cast<typename Pol::Out*>(out), 0, n, env, P, sm);
   if (threadIdx.x == 0) env_out[0] = env;
 }
 
@@ -199,23 +287,39 @@ __global__ __launch_bounds__(256) void k_agc(const void* __restrict__ in, void* 
   // A warm-up that would reach back past the call's first sample starts there, from
   // the carried envelope, exactly as chunk 0 does (such chunks are exact).
   const long long s0 = b - W > 0 ? b - W : 0;
-  float env = s0 == 0 ? P.seed(env_in[0], P.drive(x[0])) : P.warm_seed(P.drive(x[s0]));
-  env = agc_walk<Pol, false>(x, y, s0, b, env, P);
+  float env;
+  if constexpr (Pol::kBracket) {
+    if (s0 == 0) {
+      env = agc_walk<Pol, false>(x, y, 0, b, P.seed(env_in[0], P.drive(x[0])), P);
+    } else {
+      float lo = Pol::kLo, hi = Pol::kHi;
+      if (!agc_walk2<Pol>(x, s0, b, lo, hi, P)) {  // undetermined: the run fixer re-walks it
+        ent[c] = __uint_as_float(kNanEnt);
+        ext[c] = __uint_as_float(kNanExt);
+        return;
+      }
+      env = lo;
+    }
+  } else {
+    env = s0 == 0 ? P.seed(env_in[0], P.drive(x[0])) : P.warm_seed(P.drive(x[s0]));
+    env = agc_walk<Pol, false>(x, y, s0, b, env, P);
+  }
   ent[c] = env;
   env = agc_walk<Pol, true>(x, y, b, e, env, P);
   ext[c] = env;
   if (e == n) env_out[0] = env;
 }
 
-// Pass 1 for long warm-ups (few chunks: a lane per chunk would leave the chip
-// idle and walk W samples with its own strided loads, ~110 ns per sample): one
-// wave per chunk, warm-up and chunk by the wave walk (coalesced, ~27 ns per
-// sample). Same ent / ext records as k_agc.
+// Pass 1 for few chunks (a lane per chunk would leave the chip idle and walk W
+// samples with its own strided loads, ~110 ns per sample): one wave per chunk,
+// warm-up and chunk by the wave walk (coalesced, inputs in flight a block ahead).
+// Same ent / ext records as k_agc, bracketed warm-ups included.
 template <class Pol>
 __global__ __launch_bounds__(64) void k_agc_wave(const void* __restrict__ in, void* __restrict__ out, long long n,
                                                  long long L, long long W, Pol P, const float* __restrict__ env_in,
                                                  float* __restrict__ env_out, float* __restrict__ ent,
                                                  float* __restrict__ ext, long long* __restrict__ first_bad) {
+  __shared__ __attribute__((aligned(16))) float sm[192];
   const auto* x = static_cast<const typename Pol::In*>(in);
   auto* y = static_cast<typename Pol::Out*>(out);
   const long long c = blockIdx.x;
@@ -224,10 +328,24 @@ __global__ __launch_bounds__(64) void k_agc_wave(const void* __restrict__ in, vo
   if (c == 0 && lead) first_bad[0] = (n + L - 1) / L;
   const long long e = b + L < n ? b + L : n;
   const long long s0 = b - W > 0 ? b - W : 0;
-  float env = s0 == 0 ? P.seed(env_in[0], P.drive(x[0])) : P.warm_seed(P.drive(x[s0]));
-  env = agc_wave_walk<Pol, false>(x, y, s0, b, env, P);
+  float env;
+  if (Pol::kBracket && s0 > 0) {
+    float lh[2] = {Pol::kLo, Pol::kHi};
+    agc_wave_walk_n<Pol, false, 2>(x, y, s0, b, lh, P, sm);
+    if (__float_as_uint(lh[0]) != __float_as_uint(lh[1])) {  // undetermined: the run fixer re-walks it
+      if (lead) {
+        ent[c] = __uint_as_float(kNanEnt);
+        ext[c] = __uint_as_float(kNanExt);
+      }
+      return;
+    }
+    env = lh[0];
+  } else {
+    env = s0 == 0 ? P.seed(env_in[0], P.drive(x[0])) : P.warm_seed(P.drive(x[s0]));
+    env = agc_wave_walk<Pol, false>(x, y, s0, b, env, P, sm);
+  }
   if (lead) ent[c] = env;
-  env = agc_wave_walk<Pol, true>(x, y, b, e, env, P);
+  env = agc_wave_walk<Pol, true>(x, y, b, e, env, P, sm);
   if (lead) {
     ext[c] = env;
     if (e == n) env_out[0] = env;
@@ -235,13 +353,49 @@ __global__ __launch_bounds__(64) void k_agc_wave(const void* __restrict__ in, vo
 }
 
 // Pass 2: the first chunk whose entering envelope is not (bitwise) its
-// predecessor's exit.
+// predecessor's exit; bad (optional): every such chunk flagged.
 __global__ __launch_bounds__(256) void k_agc_check(const float* __restrict__ ent, const float* __restrict__ ext,
-                                                   long long chunks, long long* __restrict__ first_bad) {
+                                                   long long chunks, long long* __restrict__ first_bad,
+                                                   unsigned char* __restrict__ bad) {
   const long long c = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x + 1;
   if (c >= chunks) return;
-  if (__float_as_uint(ent[c]) != __float_as_uint(ext[c - 1]))
-    atomicMin(reinterpret_cast<unsigned long long*>(first_bad), static_cast<unsigned long long>(c));
+  const bool b = __float_as_uint(ent[c]) != __float_as_uint(ext[c - 1]);
+  if (bad) bad[c] = b ? 1 : 0;
+  if (b) atomicMin(reinterpret_cast<unsigned long long*>(first_bad), static_cast<unsigned long long>(c));
+}
+
+__global__ void k_agc_reset_first(long long* first_bad, long long chunks) { first_bad[0] = chunks; }
+
+// Pass 2b, the runs of flagged chunks in parallel (one wave per 64 chunks, each run
+// fixed by the wave its first chunk falls in): a run's predecessor is unflagged, so
+// its recorded exit is taken as true and the run is re-walked in order from it,
+// rewriting its chunks' outputs, ent and ext. A run whose predecessor was in fact
+// wrong (its predecessor's own predecessor was fixed to a different exit) is caught by
+// the second check, and the sequential pass 3 then re-walks from the first chunk
+// whose entry disagrees with its predecessor's true exit: every output is still the
+// reference's. (The CW keying of the reference's throughput harness: each key-up
+// stretch decays multiplicatively and never merges with a warm-up, so it is one run;
+// the single-wave pass 3 alone walked every one of them in order.)
+template <class Pol>
+__global__ __launch_bounds__(64) void k_agc_fix_runs(const void* __restrict__ in, void* __restrict__ out, long long n,
+                                                     long long L, Pol P, float* __restrict__ ent, float* __restrict__ ext,
+                                                     const unsigned char* __restrict__ bad, long long chunks,
+                                                     const long long* __restrict__ first_bad, float* __restrict__ env_out) {
+  __shared__ __attribute__((aligned(16))) float sm[192];
+  const long long s = blockIdx.x;  // a wave per candidate run start
+  if (first_bad[0] >= chunks || s < 1 || s >= chunks || !bad[s] || bad[s - 1]) return;
+  const auto* x = static_cast<const typename Pol::In*>(in);
+  auto* y = static_cast<typename Pol::Out*>(out);
+  const bool lead = threadIdx.x == 0;
+  float ex = ext[s - 1];  // unflagged: no fixer writes it
+  long long k = s;
+  for (; k < chunks && bad[k]; ++k) {
+    const long long b = k * L, e = b + L < n ? b + L : n;
+    if (lead) ent[k] = ex;
+    ex = agc_wave_walk<Pol>(x, y, b, e, ex, P, sm);
+    if (lead) ext[k] = ex;
+  }
+  if (k == chunks && lead) env_out[0] = ex;
 }
 
 // Pass 3 (one wave): re-run disagreeing chunks in order from the true exit of
@@ -251,6 +405,7 @@ __global__ __launch_bounds__(64) void k_agc_fix(const void* __restrict__ in, voi
                                                 long long L, Pol P, const float* __restrict__ ent,
                                                 const float* __restrict__ ext, const long long* __restrict__ first_bad,
                                                 float* __restrict__ env_out) {
+  __shared__ __attribute__((aligned(16))) float sm[192];
   const auto* x = static_cast<const typename Pol::In*>(in);
   auto* y = static_cast<typename Pol::Out*>(out);
   const long long chunks = (n + L - 1) / L;
@@ -261,7 +416,7 @@ __global__ __launch_bounds__(64) void k_agc_fix(const void* __restrict__ in, voi
   while (c < chunks) {
     // chunk c entered with the wrong envelope: re-run it from ex, in order
     const long long b = c * L, e = b + L < n ? b + L : n;
-    ex = agc_wave_walk<Pol>(x, y, b, e, ex, P);
+    ex = agc_wave_walk<Pol>(x, y, b, e, ex, P, sm);
     ++c;
     // the next chunk whose recorded entry is not the true exit of its predecessor
     long long nxt = chunks;
@@ -319,11 +474,12 @@ class EnvelopeRunner {
       ORION_HIP(hipGetLastError());
       return;
     }
-    const size_t need = static_cast<size_t>(chunks) * 2 * sizeof(float) + sizeof(long long);
+    const size_t need = static_cast<size_t>(chunks) * (2 * sizeof(float) + 1) + 2 * sizeof(long long);
     if (chunk_state_.size() < need) chunk_state_.resize(need);
     long long* first_bad = chunk_state_.as<long long>();
-    float* ent = reinterpret_cast<float*>(first_bad + 1);
+    float* ent = reinterpret_cast<float*>(first_bad + 2);
     float* ext = ent + chunks;
+    unsigned char* bad = reinterpret_cast<unsigned char*>(ext + chunks);
     const unsigned grid = static_cast<unsigned>((chunks + 255) / 256);
     const long long W = warm_ < 0 ? 0 : warm_;
     if (chunks <= kWaveChunks) {
@@ -333,8 +489,15 @@ class EnvelopeRunner {
       hipLaunchKernelGGL(k_agc<Pol>, dim3(grid), dim3(256), 0, s, in, out, n, L, W, P, ein, eout, ent, ext, first_bad);
     }
     ORION_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_agc_check, dim3(static_cast<unsigned>((chunks - 1 + 255) / 256)), dim3(256), 0, s, ent, ext,
-                       chunks, first_bad);
+    const dim3 cg(static_cast<unsigned>((chunks - 1 + 255) / 256));
+    ORION_HIP(hipMemsetAsync(bad, 0, 1, s));  // chunk 0 is never flagged (it starts from the carried state)
+    hipLaunchKernelGGL(k_agc_check, cg, dim3(256), 0, s, ent, ext, chunks, first_bad, bad);
+    ORION_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_agc_fix_runs<Pol>, dim3(static_cast<unsigned>(chunks)), dim3(64), 0, s, in, out, n, L, P, ent,
+                       ext, bad, chunks, first_bad, eout);
+    ORION_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_agc_reset_first, dim3(1), dim3(1), 0, s, first_bad, chunks);
+    hipLaunchKernelGGL(k_agc_check, cg, dim3(256), 0, s, ent, ext, chunks, first_bad, nullptr);
     ORION_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_agc_fix<Pol>, dim3(1), dim3(64), 0, s, in, out, n, L, P, ent, ext, first_bad, eout);
     ORION_HIP(hipGetLastError());

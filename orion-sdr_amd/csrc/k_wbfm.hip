@@ -916,8 +916,22 @@ __device__ __forceinline__ double uni(double v) {  // wave-uniform value -> SGPR
 // state directly: no per-lane transition matrices (lanemats) and half the f64 work
 // of zero_state + the A^{CH l} products. ef: the f32 entering states of E and O;
 // send: the f64 end state after sample L-1 (uniform).
-static_assert(offsetof(WbfmFusedConst, mh) == offsetof(WbfmFusedConst, pw) + 6 * 16 * sizeof(double),
-              "iir16 reads A^512 as pw[6]");
+// The step matrices, read with scalar loads (constant address space) at each use: held in
+// SGPRs across the segment loop they were spilled to VGPR lanes and re-read by v_readlane
+// (VALU work), ~200 per sub-range.
+typedef const __attribute__((address_space(4))) double* cmat_t;
+__device__ __forceinline__ cmat_t mats_of(const WbfmFusedConst& Bc) {
+  const double* p = Bc.mats;
+  asm volatile("" : "+s"(p));  // opaque per back: no hoisting of the loads out of the segment loop
+  return (cmat_t)(p);  // C-style: generic -> constant address space
+}
+template <int S>
+__device__ __forceinline__ void matvec_c(cmat_t M, const double (&x)[S], double (&y)[S]) {
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+#pragma unroll
+    for (int j = 0; j < S; ++j) y[i] = __builtin_fma(M[i * S + j], x[j], y[i]);
+}
 __device__ __forceinline__ void iir16(const WbfmFusedConst& Bc, const float* __restrict__ Phi, int l,
                                       const double (&sw)[4], f2 (&xs)[CH], f2 (&ef)[4], double (&send)[4]) {
 #pragma unroll
@@ -940,10 +954,11 @@ __device__ __forceinline__ void iir16(const WbfmFusedConst& Bc, const float* __r
     zE[k] = z[k].x;
     q[k] = z[k].y;
   }
-  matvec_acc<4>(Bc.pw, zE, q);  // A^8 zE + zO
+  const cmat_t pw = mats_of(Bc);
+  matvec_c<4>(pw, zE, q);  // A^8 zE + zO
   {
     double f[4] = {0, 0, 0, 0};
-    matvec_acc<4>(Bc.pw + 16, sw, f);  // A^16 sw
+    matvec_c<4>(pw + 16, sw, f);  // A^16 sw
 #pragma unroll
     for (int k = 0; k < 4; ++k) q[k] += l == 0 ? f[k] : 0.0;
   }
@@ -953,7 +968,7 @@ __device__ __forceinline__ void iir16(const WbfmFusedConst& Bc, const float* __r
     double o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) o[k] = __shfl_up(q[k], dd, 64);
-    if (l >= dd) matvec_acc<4>(Bc.pw + (st + 1) * 16, o, q);
+    if (l >= dd) matvec_c<4>(pw + (st + 1) * 16, o, q);
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -969,7 +984,7 @@ __device__ __forceinline__ void iir16(const WbfmFusedConst& Bc, const float* __r
     eE[k] = l == 0 ? sw[k] : o;
     eO[k] = zE[k];
   }
-  matvec_acc<4>(Bc.pw, eE, eO);  // entering O = A^8 (entering E) + zE
+  matvec_c<4>(pw, eE, eO);  // entering O = A^8 (entering E) + zE
 #pragma unroll
   for (int k = 0; k < 4; ++k) ef[k] = f2{static_cast<float>(eE[k]), static_cast<float>(eO[k])};
 }

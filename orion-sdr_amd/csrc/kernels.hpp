@@ -113,13 +113,13 @@ constexpr int kFuSlot = 144;                         // u32 words of a segment's
 // record layout (u32 words): [2,10) end state of the IIR (4 f64), [16,144) last
 // 128 IIR outputs. Flags: 3 u32 per segment (the epoch of the last publish).
 struct WbfmFusedConst {
-  float a[128];               // audio taps, quirk-mapped, zero padded
   float b0, b1, b2, a1, a2;   // LpCascade biquad (iir.rs:49-71)
-  double pw[6 * 16];          // (A^kSgC)^(2^s)
-  double mh[16];              // A^(kSgL/2): one half sub-range (read by iir16 as pw[6])
   float tscale;               // audio FIR on the matrix cores: 2^-st (taps scaled by 2^st; f per sub-range)
-  float pad_;
+  // device memory, read with scalar loads where used (kWbfmMats doubles): (A^kSgC)^(2^s)
+  // for s = 0..5, then A^(kSgL/2) (one half sub-range, read by iir16 as step 6)
+  const double* mats;
 };
+constexpr int kWbfmMats = 7 * 16;
 struct WbfmArgs {
   const f2* x;  long long x_stride;  long long n;
   float* phi;   long long phi_stride;               // workspace [nch][>= n_dec]

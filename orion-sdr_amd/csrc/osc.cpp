@@ -24,7 +24,7 @@ constexpr uint64_t kOscFirst = 16384;  // outputs tabulated at a (re)tune before
 RefOsc::RefOsc(float freq_hz, float fs, uint64_t budget)
     : fs_(fs), budget_(budget > kNcoTableMax ? kNcoTableMax : budget), osc_(checked_oscillator(freq_hz, fs)) {
   for (auto& e : ev_) ORION_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  build(RecState{}, 0);
+  reset();
 }
 
 RefOsc::~RefOsc() {
@@ -62,7 +62,12 @@ void RefOsc::retune(float freq_hz, float fs) {
   build(st, anchor);
 }
 
-void RefOsc::reset() { build(RecState{}, 0); }
+// Construction and reset_phase tabulate the whole budget at once (a block's setup, outside
+// its streaming calls); retune and set_budget tabulate on demand (dev()).
+void RefOsc::reset() {
+  build(RecState{}, 0);
+  rb_.extend(budget_);
+}
 
 void RefOsc::set_budget(uint64_t budget) {
   if (budget > kNcoTableMax) throw std::invalid_argument("NCO table budget above 2^28 outputs");

@@ -35,9 +35,10 @@ class RefOsc {
   uint64_t budget() const { return budget_; }
   // The device view for a launch on stream s whose outputs are count() .. count() + n - 1:
   // tabulates on the host and uploads (stream-ordered on s) whatever of that range the
-  // table does not hold yet. A (re)tune itself only restarts the recurrence: the
-  // tabulation cost follows the samples actually produced (a retune used to
-  // run 2^20 steps, upload 8 MiB and synchronise the device).
+  // table does not hold yet. Construction and reset tabulate the whole budget up front;
+  // a retune only restarts the recurrence, so its tabulation cost follows the samples
+  // actually produced after it (a retune used to run 2^20 steps, upload
+  // 8 MiB and synchronise the device).
   OscDev dev(uint64_t n, hipStream_t s);
   uint64_t count() const { return k_; }
   void advance(uint64_t n) { k_ += n; }
