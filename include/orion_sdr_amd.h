@@ -184,8 +184,10 @@ orion_block* orion_agc_rms_iq_new(float fs, float attack_ms, float release_ms, f
 int orion_am_dsb_mod_set_gain(orion_block* b, float g);
 int orion_am_dsb_mod_set_clamp(orion_block* b, int on);
 /* modulate/fm.rs:21-32 FmPhaseAccumMod::new(sample_rate, deviation_hz, rf_hz);
- * set_deviation :33-35, set_gain :36-38. The phase is summed in f64 on the
- * device (the reference multiplies f32 phasors, renormalised every 1024). */
+ * set_deviation :33-35, set_gain :36-38. The running phase is summed on the device as
+ * exact Q0.64 turn counts of the reference's own f32 step pairs (associative: any
+ * summation order gives the same bits), then the reference's f32 recurrence is re-run
+ * over each thread's 16 samples; the RF Nco is the reference's recurrence (tabulated). */
 orion_block* orion_fm_phase_accum_mod_new(float fs, float deviation_hz, float rf_hz);
 int orion_fm_phase_accum_mod_set_deviation(orion_block* b, float deviation_hz);
 int orion_fm_phase_accum_mod_set_gain(orion_block* b, float g);

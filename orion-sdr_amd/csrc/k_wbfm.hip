@@ -1086,11 +1086,20 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
   _Float16* __restrict__ Fh = static_cast<_Float16*>(Pv);
   _Float16* __restrict__ Fl = Fh + kFpN;
   float* __restrict__ Tx = reinterpret_cast<float*>(static_cast<unsigned char*>(Pv) + kTxOff);
+  h8 afr[2];  // the audio FIR's A fragments of one K-step (hi, lo)
   f2 xs[CH];
   {  // lane l: samples 16l .. 16l+15 (iir16); f replaces x in xs (zeros past Lr)
     f2 ef[4];
     double send[4];
     iir16(Bc, Phi, l, sw, xs, ef, send);
+    // the audio FIR's first A fragments (L2-resident), requested now: their latency hides
+    // behind the recurrence and the plane writes; later steps' one step ahead (loaded at
+    // their own step they cost ~5 L2 round trips per back)
+    {
+      const h8* __restrict__ af = static_cast<const h8*>(a.afrag);
+      afr[0] = af[l];
+      afr[1] = af[64 + l];
+    }
     if (trace_r >= 0) fu::trace(a, trace_r, 10);
     const int jl = Lr - 1;
     float cap[4] = {0, 0, 0, 0};
@@ -1188,19 +1197,31 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
     f4v acc[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) acc[g] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+    // per K-step: the eight plane reads issued together, then the four groups' MFMAs
+    // interleaved (independent accumulators back to back)
     const h8* __restrict__ af = static_cast<const h8*>(a.afrag);
 #pragma unroll 1
     for (int st = 0; st < 5; ++st) {
-      const h8 ah = af[(2 * st) * 64 + l], al = af[(2 * st + 1) * 64 + l];
+      const h8 ah = afr[0], al = afr[1];
+      {  // the next step's fragments, one step ahead (step 5 reads step 0's again: unused)
+        const int sn = st < 4 ? st + 1 : 0;
+        afr[0] = af[(2 * sn) * 64 + l];
+        afr[1] = af[(2 * sn + 1) * 64 + l];
+      }
+      h8 bh[4], bl[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int e = pe(256 * g + 16 * J + 32 * st + 8 * kg);
-        const h8 bh = *reinterpret_cast<const h8*>(Fh + e);
-        const h8 bl = *reinterpret_cast<const h8*>(Fl + e);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[g], 0, 0, 0);
+        bh[g] = *reinterpret_cast<const h8*>(Fh + e);
+        bl[g] = *reinterpret_cast<const h8*>(Fl + e);
       }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[g], acc[g], 0, 0, 0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[g], acc[g], 0, 0, 0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[g], acc[g], 0, 0, 0);
+      asm volatile("" ::: "memory");  // the next step's plane reads stay behind these MFMAs (registers)
     }
     // lane (J, kg) holds outputs 256 g + 16 J + 4 kg + r, r < 4
     float* __restrict__ y = a.y + ch * a.y_stride + A0;
