@@ -48,6 +48,14 @@ def main():
         ("kernel span (first start -> last end)", np.array([t[:, 3].max() - t0])),
     ]
     print(f"segments {len(t)}; n {a.n}")
+    end = t[:, 3] - t0
+    seg = np.arange(len(t))
+    print("end time by XCD (blockIdx mod 8):", " ".join(f"{np.median(end[seg % 8 == x]):.1f}" for x in range(8)))
+    print("end time by blockIdx decile:     ", " ".join(f"{np.median(end[(seg * 10) // len(t) == d]):.1f}"
+                                                        for d in range(10)))
+    print("segment total by decile:         ", " ".join(f"{np.median((t[:, 3] - t[:, 0])[(seg * 10) // len(t) == d]):.1f}"
+                                                        for d in range(10)))
+    print("end-time percentiles 50/90/99/max:", " ".join(f"{np.percentile(end, q):.1f}" for q in (50, 90, 99, 100)))
     for name, v in rows:
         print(f"{name:48s} median {med(v):8.2f} us  p10 {np.percentile(v, 10):8.2f}  p90 {np.percentile(v, 90):8.2f}")
     os.remove(path)
