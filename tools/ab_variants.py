@@ -3,8 +3,8 @@
 = lib/) is loaded as its own module, launches are interleaved A B C, B C A, ... so the
 chip's clock state hits every variant alike, one HIP event pair per launch.
   python tools/ab_variants.py --case c5 --rounds 4 --k 10 base v1 v2
-Cases: c2 (WBFM 2^26), c4 (WBFM 8 x 2^24), c5 (SSB 128 x 2^20), a10 (SSB 2^24),
-a6 (LpCascade 2^24), a9 (FM demod 2^24)."""
+Cases: c2 (WBFM 2^26), c4 (WBFM 8 x 2^24), c5 (SSB 128 x 2^20), a10 (SSB 2^24), a11 / a11abs (AM PowerSqrt / AbsApprox 2^24), a7 (DcBlocker
+2^24), a6 (LpCascade 2^24), a9 (FM demod 2^24)."""
 import argparse
 import importlib.util
 import os
@@ -36,6 +36,13 @@ def case(m, name, dev):
                 torch.randn(128, 1 << 20, dtype=torch.complex64, device=dev, generator=g))
     if name == "a10":
         return m.SsbProductDemod(48e3, 1500.0, 2800.0), torch.randn(1 << 24, dtype=torch.complex64, device=dev, generator=g)
+    if name == "a11":
+        return m.AmEnvelopeDemod(48e3, 5e3), torch.randn(1 << 24, dtype=torch.complex64, device=dev, generator=g)
+    if name == "a11abs":
+        return (m.AmEnvelopeDemod(48e3, 5e3, abs_approx=True),
+                torch.randn(1 << 24, dtype=torch.complex64, device=dev, generator=g))
+    if name == "a7":
+        return m.DcBlocker(48e3, 2.0), torch.randn(1 << 24, dtype=torch.float32, device=dev, generator=g)
     if name == "a6":
         return m.LpCascade(1.25e6, 13.5e3), torch.randn(1 << 24, dtype=torch.float32, device=dev, generator=g)
     if name == "a9":
