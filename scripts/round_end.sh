@@ -14,5 +14,5 @@ TAG=${TAG:-end} bash scripts/blocks_session.sh || exit $?
 timeout -k 10 300 python tools/mod_bench.py > "gpurun_out/${TAG:-end}/mod.jsonl" 2>&1 || { tail -3 "gpurun_out/${TAG:-end}/mod.jsonl"; exit 1; }
 grep -h case "gpurun_out/${TAG:-end}/mod.jsonl" | cut -c1-150
 if [ "${TRAFFIC:-0}" = 1 ]; then
-  TAG=${TAG:-end}_traffic CFGS="c2 c5" bash scripts/traffic_session.sh || exit $?
+  TAG=${TAG:-end}_traffic CFGS="${TCFGS:-c2 c5}" bash scripts/traffic_session.sh || exit $?
 fi
