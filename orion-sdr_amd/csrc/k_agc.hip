@@ -119,30 +119,39 @@ __device__ __forceinline__ float agc_walk(const typename Pol::In* __restrict__ x
     cur[j] = s + j < e ? x[s + j] : T{};
     if constexpr (OUT) ca[j] = s + j < e ? P.aux(s + j) : A{};
   }
-  for (long long base = s; base < e; base += kB) {
-    const long long nb = base + kB;
+  auto walk = [&](auto same) {
+    for (long long base = s; base < e; base += kB) {
+      const long long nb = base + kB;
 #pragma unroll
-    for (int j = 0; j < kB; ++j) {
-      nxt[j] = nb + j < e ? x[nb + j] : T{};
-      if constexpr (OUT) na[j] = nb + j < e ? P.aux(nb + j) : A{};
-    }
+      for (int j = 0; j < kB; ++j) {
+        nxt[j] = nb + j < e ? x[nb + j] : T{};
+        if constexpr (OUT) na[j] = nb + j < e ? P.aux(nb + j) : A{};
+      }
 #pragma unroll
-    for (int j = 0; j < kB; ++j) {
-      const long long i = base + j;
-      const float d = P.drive(cur[j]);
-      const bool up = P.up(d, env);
-      const float ne = (up ? P.att : P.rel) * env + (up ? P.oma : P.omr) * d;  // agc.rs:40, cw.rs:58-62
-      if (i < e) {
-        env = ne;
-        if constexpr (OUT) y[i] = P.out(cur[j], env, ca[j]);
+      for (int j = 0; j < kB; ++j) {
+        const long long i = base + j;
+        const float d = P.drive(cur[j]);
+        float ne;
+        if constexpr (decltype(same)::value) {
+          ne = P.att * env + P.oma * d;  // one coefficient pair (agc_wave_walk_n)
+        } else {
+          const bool up = P.up(d, env);
+          ne = (up ? P.att : P.rel) * env + (up ? P.oma : P.omr) * d;  // agc.rs:40, cw.rs:58-62
+        }
+        if (i < e) {
+          env = ne;
+          if constexpr (OUT) y[i] = P.out(cur[j], env, ca[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kB; ++j) {
+        cur[j] = nxt[j];
+        if constexpr (OUT) ca[j] = na[j];
       }
     }
-#pragma unroll
-    for (int j = 0; j < kB; ++j) {
-      cur[j] = nxt[j];
-      if constexpr (OUT) ca[j] = na[j];
-    }
-  }
+  };
+  if (P.att == P.rel && P.oma == P.omr) walk(std::true_type{});
+  else walk(std::false_type{});
   return env;
 }
 
@@ -161,10 +170,11 @@ __device__ __forceinline__ bool agc_walk2(const typename Pol::In* __restrict__ x
     const long long nb = base + kB;
 #pragma unroll
     for (int j = 0; j < kB; ++j) nxt[j] = nb + j < e ? x[nb + j] : T{};
+    const bool same = P.att == P.rel && P.oma == P.omr;
 #pragma unroll
     for (int j = 0; j < kB; ++j) {
       const float d = P.drive(cur[j]);
-      const bool ul = P.up(d, lo), uh = P.up(d, hi);
+      const bool ul = same || P.up(d, lo), uh = same || P.up(d, hi);
       const float nl = (ul ? P.att : P.rel) * lo + (ul ? P.oma : P.omr) * d;
       const float nh = (uh ? P.att : P.rel) * hi + (uh ? P.oma : P.omr) * d;
       if (base + j < e) {
@@ -187,12 +197,15 @@ constexpr unsigned kNanEnt = 0x7FC00001u, kNanExt = 0x7FC00002u;  // unknown ent
 // One wave walks samples [s, e) in order (the re-runs of k_agc_fix and k_agc_fix_runs,
 // the sequential path and the wave-per-chunk pass 1). The 64 lanes load 64 samples
 // (coalesced, the next 64 in flight) and form d and both candidate (1 - a) * d products
-// into LDS (sm: 3 x 64 floats of this wave); then every lane runs the envelope chain over
+// into LDS (sm: 4 x 64 floats of this wave); then every lane runs the envelope chain over
 // the 64 values read back as broadcast b128 reads, 16 at a time (compare, two selects,
-// one multiply, one add per sample: the reference's f32 ops and order), and keeps its
-// own sample's envelope; then every lane forms its sample's output. NT trajectories
-// (1, or 2 for a bracketed warm-up: from env[0] and env[1]) share the broadcast values.
-// (The chain formerly read the values by v_readlane: ~27 ns per sample.)
+// one multiply, one add per sample: the reference's f32 ops and order), lane 0 records
+// every step's envelope in LDS (four b128 writes per 16 steps), and each lane then reads
+// its own sample's envelope back and forms its output. NT trajectories (1, or 2 for a
+// bracketed warm-up: from env[0] and env[1]) share the broadcast values. When both
+// branches use the same coefficients (att == rel and oma == omr: CwKeyedMod with rise ==
+// fall) the compare and selects cannot change a bit and the chain is the multiply and
+// the add alone. (~27 ns per sample when the chain read its values by v_readlane.)
 template <class Pol, bool OUT, int NT>
 __device__ __forceinline__ void agc_wave_walk_n(const typename Pol::In* __restrict__ x,
                                                 typename Pol::Out* __restrict__ y, long long s, long long e,
@@ -200,14 +213,35 @@ __device__ __forceinline__ void agc_wave_walk_n(const typename Pol::In* __restri
   using T = typename Pol::In;
   using A = typename Pol::Aux;
   const int lane = threadIdx.x & 63;
-  T cur = s + lane < e ? x[s + lane] : T{};
-  A ca{};
-  if constexpr (OUT) ca = s + lane < e ? P.aux(s + lane) : A{};
+  const bool uni = P.att == P.rel && P.oma == P.omr;  // kernel-argument uniform
+  // inputs (and output phasors) of the next kAhead blocks in flight: a block's chain
+  // (~64 x 10 cycles) is shorter than a load's latency
+  constexpr int kAhead = 4;
+  T q[kAhead];
+  A qa[kAhead];
+  // (unconditional loads at a clamped index: a conditional one makes the compiler's wait
+  // counting drain every load in flight at its first use)
+#pragma unroll
+  for (int u = 0; u < kAhead; ++u) {
+    const long long i = s + 64 * u + lane;
+    q[u] = x[i < e ? i : e - 1];
+    if constexpr (OUT) qa[u] = P.aux(i < e ? i : e - 1);
+  }
   for (long long base = s; base < e; base += 64) {
     const long long i = base + lane;
-    const T nxt = i + 64 < e ? x[i + 64] : T{};
-    A na{};
-    if constexpr (OUT) na = i + 64 < e ? P.aux(i + 64) : A{};
+    const T cur = q[0];
+    A ca{};
+    if constexpr (OUT) ca = qa[0];
+#pragma unroll
+    for (int u = 0; u + 1 < kAhead; ++u) {
+      q[u] = q[u + 1];
+      if constexpr (OUT) qa[u] = qa[u + 1];
+    }
+    {
+      const long long ip = i + 64 * kAhead;
+      q[kAhead - 1] = x[ip < e ? ip : e - 1];
+      if constexpr (OUT) qa[kAhead - 1] = P.aux(ip < e ? ip : e - 1);
+    }
     const float d = P.drive(cur);
     asm volatile("" ::: "memory");  // the previous block's broadcast reads precede these writes (one wave: DS in order)
     sm[lane] = d;
@@ -215,40 +249,69 @@ __device__ __forceinline__ void agc_wave_walk_n(const typename Pol::In* __restri
     sm[128 + lane] = P.omr * d;
     asm volatile("" ::: "memory");
     const int cnt = e - base < 64 ? static_cast<int>(e - base) : 64;
-    float mine = 0.0f;
-    auto chain = [&](auto full) {
+    auto chain = [&](auto full, auto same) {
+      constexpr bool kSame = decltype(same)::value;
+      float a64[64];  // one coefficient pair: the block's 64 (1 - a) d values read at once
+      if constexpr (kSame) {
 #pragma unroll
-      for (int q = 0; q < 64; q += 16) {
-        float dv[16], av[16], rv[16];
+        for (int t = 0; t < 64; t += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(sm + 64 + t);
+          a64[t] = v.x; a64[t + 1] = v.y; a64[t + 2] = v.z; a64[t + 3] = v.w;
+        }
+      }
 #pragma unroll
-        for (int t = 0; t < 16; t += 4) {
-          const float4 u = *reinterpret_cast<const float4*>(sm + q + t);
-          const float4 v = *reinterpret_cast<const float4*>(sm + 64 + q + t);
-          const float4 w = *reinterpret_cast<const float4*>(sm + 128 + q + t);
-          dv[t] = u.x; dv[t + 1] = u.y; dv[t + 2] = u.z; dv[t + 3] = u.w;
-          av[t] = v.x; av[t + 1] = v.y; av[t + 2] = v.z; av[t + 3] = v.w;
-          rv[t] = w.x; rv[t + 1] = w.y; rv[t + 2] = w.z; rv[t + 3] = w.w;
+      for (int g = 0; g < 64; g += 16) {
+        float dv[16], av[16], rv[16], rec[16];
+        if constexpr (kSame) {
+#pragma unroll
+          for (int t = 0; t < 16; ++t) av[t] = a64[g + t];
+        } else {
+#pragma unroll
+          for (int t = 0; t < 16; t += 4) {
+            const float4 u = *reinterpret_cast<const float4*>(sm + g + t);
+            const float4 v = *reinterpret_cast<const float4*>(sm + 64 + g + t);
+            const float4 w = *reinterpret_cast<const float4*>(sm + 128 + g + t);
+            dv[t] = u.x; dv[t + 1] = u.y; dv[t + 2] = u.z; dv[t + 3] = u.w;
+            av[t] = v.x; av[t + 1] = v.y; av[t + 2] = v.z; av[t + 3] = v.w;
+            rv[t] = w.x; rv[t + 1] = w.y; rv[t + 2] = w.z; rv[t + 3] = w.w;
+          }
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          if (decltype(full)::value || q + j < cnt) {
+          if (decltype(full)::value || g + j < cnt) {
 #pragma unroll
             for (int k = 0; k < NT; ++k) {
-              const bool up = P.up(dv[j], env[k]);
-              env[k] = (up ? P.att : P.rel) * env[k] + (up ? av[j] : rv[j]);
+              if constexpr (kSame) {
+                env[k] = P.att * env[k] + av[j];  // agc.rs:40 / cw.rs:58-62 with one coefficient pair
+              } else {
+                const bool up = P.up(dv[j], env[k]);
+                env[k] = (up ? P.att : P.rel) * env[k] + (up ? av[j] : rv[j]);
+              }
             }
-            if constexpr (OUT) mine = lane == q + j ? env[0] : mine;
+          }
+          rec[j] = env[0];
+        }
+        if constexpr (OUT) {
+          if (lane == 0) {
+#pragma unroll
+            for (int t = 0; t < 16; t += 4)
+              *reinterpret_cast<float4*>(sm + 192 + g + t) = make_float4(rec[t], rec[t + 1], rec[t + 2], rec[t + 3]);
           }
         }
       }
     };
-    if (cnt == 64) chain(std::true_type{});
-    else chain(std::false_type{});
-    if constexpr (OUT) {
-      if (i < e) y[i] = P.out(cur, mine, ca);
-      ca = na;
+    if (uni) {
+      if (cnt == 64) chain(std::true_type{}, std::true_type{});
+      else chain(std::false_type{}, std::true_type{});
+    } else {
+      if (cnt == 64) chain(std::true_type{}, std::false_type{});
+      else chain(std::false_type{}, std::false_type{});
     }
-    cur = nxt;
+    if constexpr (OUT) {
+      asm volatile("" ::: "memory");  // lane 0's records precede the reads (one wave: DS in order)
+      const float mine = sm[192 + lane];
+      if (i < e) y[i] = P.out(cur, mine, ca);
+    }
   }
 }
 template <class Pol, bool OUT = true>
@@ -264,7 +327,7 @@ __device__ __forceinline__ float agc_wave_walk(const typename Pol::In* __restric
 template <class Pol>
 __global__ __launch_bounds__(64) void k_agc_seq(const void* __restrict__ in, void* __restrict__ out, long long n,
                                                 Pol P, const float* __restrict__ env_in, float* __restrict__ env_out) {
-  __shared__ __attribute__((aligned(16))) float sm[192];
+  __shared__ __attribute__((aligned(16))) float sm[256];
   const auto* x = static_cast<const typename Pol::In*>(in);
   float env = P.seed(env_in[0], P.drive(x[0]));
   env = agc_wave_walk<Pol>(x, static_cast<typename Pol::Out*>(out), 0, n, env, P, sm);
@@ -319,7 +382,7 @@ __global__ __launch_bounds__(64) void k_agc_wave(const void* __restrict__ in, vo
                                                  long long L, long long W, Pol P, const float* __restrict__ env_in,
                                                  float* __restrict__ env_out, float* __restrict__ ent,
                                                  float* __restrict__ ext, long long* __restrict__ first_bad) {
-  __shared__ __attribute__((aligned(16))) float sm[192];
+  __shared__ __attribute__((aligned(16))) float sm[256];
   const auto* x = static_cast<const typename Pol::In*>(in);
   auto* y = static_cast<typename Pol::Out*>(out);
   const long long c = blockIdx.x;
@@ -331,7 +394,11 @@ __global__ __launch_bounds__(64) void k_agc_wave(const void* __restrict__ in, vo
   float env;
   if (Pol::kBracket && s0 > 0) {
     float lh[2] = {Pol::kLo, Pol::kHi};
-    agc_wave_walk_n<Pol, false, 2>(x, y, s0, b, lh, P, sm);
+    // both ends in pieces of 256 samples; once they meet, one trajectory for the rest
+    long long p = s0;
+    for (; p < b && __float_as_uint(lh[0]) != __float_as_uint(lh[1]); p += 256)
+      agc_wave_walk_n<Pol, false, 2>(x, y, p, p + 256 < b ? p + 256 : b, lh, P, sm);
+    if (p < b) lh[0] = lh[1] = agc_wave_walk<Pol, false>(x, y, p, b, lh[0], P, sm);
     if (__float_as_uint(lh[0]) != __float_as_uint(lh[1])) {  // undetermined: the run fixer re-walks it
       if (lead) {
         ent[c] = __uint_as_float(kNanEnt);
@@ -381,7 +448,7 @@ __global__ __launch_bounds__(64) void k_agc_fix_runs(const void* __restrict__ in
                                                      long long L, Pol P, float* __restrict__ ent, float* __restrict__ ext,
                                                      const unsigned char* __restrict__ bad, long long chunks,
                                                      const long long* __restrict__ first_bad, float* __restrict__ env_out) {
-  __shared__ __attribute__((aligned(16))) float sm[192];
+  __shared__ __attribute__((aligned(16))) float sm[256];
   const long long s = blockIdx.x;  // a wave per candidate run start
   if (first_bad[0] >= chunks || s < 1 || s >= chunks || !bad[s] || bad[s - 1]) return;
   const auto* x = static_cast<const typename Pol::In*>(in);
@@ -405,7 +472,7 @@ __global__ __launch_bounds__(64) void k_agc_fix(const void* __restrict__ in, voi
                                                 long long L, Pol P, const float* __restrict__ ent,
                                                 const float* __restrict__ ext, const long long* __restrict__ first_bad,
                                                 float* __restrict__ env_out) {
-  __shared__ __attribute__((aligned(16))) float sm[192];
+  __shared__ __attribute__((aligned(16))) float sm[256];
   const auto* x = static_cast<const typename Pol::In*>(in);
   auto* y = static_cast<typename Pol::Out*>(out);
   const long long chunks = (n + L - 1) / L;
