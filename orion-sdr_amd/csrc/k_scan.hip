@@ -480,6 +480,10 @@ __device__ __forceinline__ void dc_combine(double m1, double d1, double& m2, dou
 // (S mtab[64 SC w + l]) mtab[64 k] scaled by the linear magnitude model.
 template <int SC>
 __device__ __forceinline__ int posS(int e) { return e + static_cast<int>(static_cast<unsigned>(e) / SC); }
+// posS(e0 + R k) for e0 >= 0 and SC | R: posS(e0) + k (R + R / SC), so that the row
+// offset folds into the LDS instruction's immediate (the division is not redone per row)
+template <int SC, int R>
+__device__ __forceinline__ int posS_row(int pe0, int k) { return pe0 + k * (R + R / SC); }
 __device__ __forceinline__ void wave_order() { asm volatile("" ::: "memory"); }
 template <Pre PR, int SC>
 __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long base, int cnt, float* sb) {
@@ -496,7 +500,7 @@ __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long ba
       v[k] = e < cnt ? xr[e] : 0.0f;
     }
 #pragma unroll
-    for (int k = 0; k < SC; ++k) sb[posS<SC>(e0 + 64 * k)] = v[k];
+    for (int k = 0; k < SC; ++k) sb[posS_row<SC, 64>(posS<SC>(e0), k)] = v[k];
     return;
   }
   const f2* __restrict__ x = static_cast<const f2*>(a.x) + ch * a.x_stride + base;
@@ -510,8 +514,9 @@ __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long ba
     // the BFO's outputs over the chunk: one tile-uniform branch per form, so only one
     // form's temporaries are live beside v[]
     const OscRun R = osc_run(a.osc, static_cast<uint64_t>(a.k0 + base), cnt);
+    const int pe0 = posS<SC>(e0);
     auto put = [&](int k, f2 p) {
-      sb[posS<SC>(e0 + 64 * k)] = __builtin_fmaf(v[k].x, p.x, v[k].y * p.y);  // ssb.rs:37
+      sb[posS_row<SC, 64>(pe0, k)] = __builtin_fmaf(v[k].x, p.x, v[k].y * p.y);  // ssb.rs:37
     };
     if (R.kind == 0) {
 #pragma unroll
@@ -537,7 +542,7 @@ __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long ba
     } else {
       o = __builtin_fmaf(a.c.k1, fabsf(z.x), a.c.k2 * fabsf(z.y));  // am.rs:238
     }
-    sb[posS<SC>(e0 + 64 * k)] = o;
+    sb[posS_row<SC, 64>(posS<SC>(e0), k)] = o;
   }
 }
 
@@ -845,12 +850,12 @@ __global__ __launch_bounds__(NT, SC > 16 ? kSpMinW : kSpMinW16) void k_lpdc_sp(c
     const int kmin = (warm - wave * (64 * SC)) >> 6;  // wave-uniform: the warm-up is whole rows of 64
 #pragma unroll
     for (int k = 0; k < SC; ++k)
-      if (k >= kmin) yo[e0 + 64 * k - warm] = sb[posS<SC>(e0 + 64 * k)];
+      if (k >= kmin) yo[e0 + 64 * k - warm] = sb[posS_row<SC, 64>(posS<SC>(e0), k)];
   } else {
 #pragma unroll
     for (int k = 0; k < SC; ++k) {
       const int e2 = e0 + 64 * k;
-      if (e2 >= warm && e2 < cnt) yo[e2 - warm] = sb[posS<SC>(e2)];
+      if (e2 >= warm && e2 < cnt) yo[e2 - warm] = sb[posS_row<SC, 64>(posS<SC>(e0), k)];
     }
   }
 }
@@ -943,7 +948,7 @@ __global__ __launch_bounds__(NT, kScanSpMinW) void k_scan_sp(const ScanArgs a, i
       } else {
         o = premap_v<PR>(a, ch, base + e, base, Ro, z[j], zp[j]);
       }
-      if (!G || e < cnt) sb[posS<SC>(e)] = o;
+      if (!G || e < cnt) sb[posS_row<SC, NT>(posS<SC>(t), k0 + j)] = o;  // e = t + (k0 + j) NT
     }
   }
   };
@@ -1097,7 +1102,7 @@ __global__ __launch_bounds__(NT, kScanSpMinW) void k_scan_sp(const ScanArgs a, i
   float* y = static_cast<float*>(a.y) + ch * a.y_stride + base;
   if (fast) {
 #pragma unroll
-    for (int k = 0; k < SC; ++k) y[t + k * NT] = sb[posS<SC>(t + k * NT)];
+    for (int k = 0; k < SC; ++k) y[t + k * NT] = sb[posS_row<SC, NT>(posS<SC>(t), k)];
   } else {
     for (int e2 = t; e2 < cnt; e2 += NT) y[e2] = sb[posS<SC>(e2)];
   }
