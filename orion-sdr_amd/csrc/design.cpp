@@ -141,6 +141,20 @@ Oscillator oscillator(float freq_hz, float fs) {  // rotator.rs:17-18
   return o;
 }
 
+std::vector<float> phasor_table_q64(uint64_t step_q64, size_t n) {
+  // the angle of output k reduced exactly (k step mod 2^64, a Q0.64 turn count), then one
+  // double sincos: ~20 ns per entry (a long double sin/cos of k theta: ~200)
+  std::vector<float> t(2 * n);
+  constexpr double kTurn = 6.283185307179586476925286766559 / 18446744073709551616.0;  // 2 pi / 2^64
+  for (size_t k = 0; k < n; ++k) {
+    const uint64_t ph = static_cast<uint64_t>(k) * step_q64;
+    const double a = static_cast<double>(static_cast<int64_t>(ph)) * kTurn;  // (-pi, pi]
+    t[2 * k] = static_cast<float>(std::cos(a));
+    t[2 * k + 1] = static_cast<float>(std::sin(a));
+  }
+  return t;
+}
+
 std::vector<float> phasor_table(double theta, size_t n) {
   std::vector<float> t(2 * n);
   for (size_t k = 0; k < n; ++k) {
@@ -190,14 +204,33 @@ inline uint64_t state_key(const RecState& s) {
 template <class Fma>
 uint64_t rec_run(float wr, float wi, RecState& s, uint64_t k0, uint64_t k1, std::vector<float>& z,
                  std::unordered_map<uint64_t, uint64_t>& seen, Fma fma) {
-  for (uint64_t k = k0; k < k1; ++k) {
-    rec_step(s, wr, wi, fma);
-    z[2 * k] = s.zr;
-    z[2 * k + 1] = s.zi;
+  float* __restrict__ zp = z.data();
+  for (uint64_t k = k0; k < k1;) {
+    // the steps up to the next renorm point: the rotation alone (no per-step tests)
+    const uint64_t to_renorm = 1024u - (s.ctr & 0x3FFu);
+    const uint64_t m = std::min<uint64_t>(to_renorm - 1, k1 - k);
+    float zr = s.zr, zi = s.zi;
+    for (uint64_t i = 0; i < m; ++i) {
+      const float nr = fma(zr, wr, -zi * wi);
+      const float ni = fma(zi, wr, zr * wi);
+      zr = nr;
+      zi = ni;
+      zp[2 * (k + i)] = zr;
+      zp[2 * (k + i) + 1] = zi;
+    }
+    s.zr = zr;
+    s.zi = zi;
+    s.ctr += static_cast<uint32_t>(m);
+    k += m;
+    if (k == k1) break;
+    rec_step(s, wr, wi, fma);  // the renorm step
+    zp[2 * k] = s.zr;
+    zp[2 * k + 1] = s.zi;
+    ++k;
     if ((s.ctr & 0x3FFu) == 0) {
-      const auto ins = seen.emplace(state_key(s), k + 1);
+      const auto ins = seen.emplace(state_key(s), k);
       if (!ins.second) {
-        z.resize(static_cast<size_t>(2 * (k + 1)));
+        z.resize(static_cast<size_t>(2 * k));
         return ins.first->second;
       }
     }

@@ -45,6 +45,8 @@ Oscillator oscillator(float freq_hz, float fs);
 
 // Phasor e^{j*theta*k} for k = 0..n-1, computed in f64 and rounded to f32 pairs.
 std::vector<float> phasor_table(double theta, size_t n);
+// The same for a Q0.64 step (turns): e^{j 2 pi k step / 2^64}, k < n.
+std::vector<float> phasor_table_q64(uint64_t step_q64, size_t n);
 
 // ---- the reference's phasor recurrence (rotator.rs:44-62, nco.rs:42-58) ----------
 // z <- (fma(z.re, w.re, -(z.im w.im)), fma(z.im, w.re, z.re w.im)) in f32, then when

@@ -923,4 +923,25 @@ void launch_hist_update_r(const float* x, long long n, const float* old_h, float
   ORION_LAUNCH_CHECK();
 }
 
+namespace {
+// e^{j 2 pi k step / 2^64}, k < n (the oscillator model's step table, osc.cpp): the angle
+// reduced exactly as a Q0.64 turn count, then an f64 sincos; built on the device at a
+// (re)tune instead of on the host (~1-4 ms there) and uploaded
+__global__ __launch_bounds__(NT) void k_phasor_q64(f2* __restrict__ out, uint64_t step_q64, int n) {
+  const int k = static_cast<int>(blockIdx.x) * NT + static_cast<int>(threadIdx.x);
+  if (k >= n) return;
+  const uint64_t ph = static_cast<uint64_t>(k) * step_q64;
+  const double a = static_cast<double>(static_cast<int64_t>(ph)) * (6.283185307179586476925286766559 / 18446744073709551616.0);
+  double sn, cs;
+  sincos(a, &sn, &cs);
+  out[k] = f2{static_cast<float>(cs), static_cast<float>(sn)};
+}
+}  // namespace
+
+void launch_phasor_table_q64(f2* out, uint64_t step_q64, int n, hipStream_t s) {
+  if (n <= 0) return;
+  k_phasor_q64<<<(n + NT - 1) / NT, NT, 0, s>>>(out, step_q64, n);
+  ORION_LAUNCH_CHECK();
+}
+
 }  // namespace orion

@@ -77,6 +77,8 @@ void launch_hist_update_c(const f2* x_dev, long long n, const f2* old_dev, f2* n
                           int hist_len, hipStream_t s, int nch = 1, long long x_stride = 0);
 void launch_hist_update_r(const float* x_dev, long long n, const float* old_dev, float* new_dev,
                           int hist_len, hipStream_t s);
+// out[k] = e^{j 2 pi k step / 2^64}, k < n (device-built oscillator model step table)
+void launch_phasor_table_q64(f2* out, uint64_t step_q64, int n, hipStream_t s);
 
 // ------------------------------------------------------------ WBFM chain --
 // Default: one launch per call (k_wbfm_seg, see k_wbfm.hip). The two-kernel path

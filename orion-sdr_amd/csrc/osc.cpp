@@ -1,6 +1,8 @@
 // osc.cpp — RefOsc (osc.hpp): the reference's phasor recurrence, tabulated per tune.
 #include "osc.hpp"
 
+#include "kernels.hpp"
+
 #include <cmath>
 #include <stdexcept>
 #include <vector>
@@ -19,7 +21,11 @@ Oscillator checked_oscillator(float f, float fs) {
 }
 }  // namespace
 
-constexpr uint64_t kOscFirst = 16384;  // outputs tabulated at a (re)tune before any call asks
+constexpr uint64_t kOscFirst = 4096;   // outputs tabulated at a (re)tune before any call asks
+// Outputs tabulated past a call's last one while the table grows: the longest tile a
+// kernel forms one cursor for (kRotTile; k_mod's tiles are shorter, the scans' runs lie
+// inside the call), so every run of the call is table-only.
+constexpr uint64_t kOscMargin = static_cast<uint64_t>(kRotTile);
 
 RefOsc::RefOsc(float freq_hz, float fs, uint64_t budget)
     : fs_(fs), budget_(budget > kNcoTableMax ? kNcoTableMax : budget), osc_(checked_oscillator(freq_hz, fs)) {
@@ -91,7 +97,13 @@ void RefOsc::build(const RecState& st, uint64_t closed_anchor_q64) {
   mt_up_ = false;
   org_ = st;
   k_ = 0;
-  rb_ = RecBuilder(osc_.w_re, osc_.w_im, st, budget_, kOscSpan, osc_.step_q64);
+  pad_up_ = false;
+  {  // the previous tune's host table storage, reused (no page faults on the next extend)
+    std::vector<float> z = std::move(rb_.table().z);
+    z.clear();
+    rb_ = RecBuilder(osc_.w_re, osc_.w_im, st, budget_, kOscSpan, osc_.step_q64);
+    if (rb_.table().z.empty()) rb_.table().z.swap(z);
+  }
   if (budget_ == 0) {  // the closed form: no table, the model from this phase on
     rb_.table().ctr0 = st.ctr;
     rb_.table().mbase = closed_anchor_q64;
@@ -115,31 +127,36 @@ void RefOsc::upload(hipStream_t s) {
       dtab_[cur_].resize(cap * sizeof(f2));
     }
     const uint64_t n0 = up_ ? up_ : 0;
-    std::vector<float> pad(2 * static_cast<size_t>(kOscSpan));
-    for (uint64_t i = 0; i < static_cast<uint64_t>(kOscSpan); ++i) {
-      const uint64_t src = t.cyc_len ? t.cyc_start + i % t.cyc_len : t.n - 1;
-      pad[2 * i] = t.z[2 * src];
-      pad[2 * i + 1] = t.z[2 * src + 1];
-    }
     char* d = dtab_[cur_].as<char>();
     // pageable sources: the copy has read them when hipMemcpyAsync returns
     ORION_HIP(hipMemcpyAsync(d + n0 * sizeof(f2), t.z.data() + 2 * n0, (t.n - n0) * sizeof(f2),
                              hipMemcpyHostToDevice, s));
-    ORION_HIP(hipMemcpyAsync(d + t.n * sizeof(f2), pad.data(), pad.size() * sizeof(float), hipMemcpyHostToDevice, s));
     up_ = t.n;
   }
+  if (!pad_up_ && rb_.done() && t.cyc_len) {
+    // A final table with a cycle: the run past n continues the cycle (runs read tab[j + off]
+    // unwrapped). Without a cycle the entries past n are never used (the model serves
+    // them; reads there stay inside the allocation), so nothing is uploaded for them.
+    std::vector<float> pad(2 * static_cast<size_t>(kOscSpan));
+    for (uint64_t i = 0; i < static_cast<uint64_t>(kOscSpan); ++i) {
+      const uint64_t src = t.cyc_start + i % t.cyc_len;
+      pad[2 * i] = t.z[2 * src];
+      pad[2 * i + 1] = t.z[2 * src + 1];
+    }
+    ORION_HIP(hipMemcpyAsync(dtab_[cur_].as<char>() + t.n * sizeof(f2), pad.data(), pad.size() * sizeof(float),
+                             hipMemcpyHostToDevice, s));
+    pad_up_ = true;
+  }
   if (!mt_up_ && rb_.done()) {
-    const double th = static_cast<double>(static_cast<long double>(t.mstep) / 18446744073709551616.0L * kTwoPiL);
-    const auto mt = phasor_table(th, kOscSpan);
-    dmtab_[cur_].resize(mt.size() * sizeof(float));
-    ORION_HIP(hipMemcpyAsync(dmtab_[cur_].as<void>(), mt.data(), mt.size() * sizeof(float), hipMemcpyHostToDevice, s));
+    dmtab_[cur_].resize(2 * static_cast<size_t>(kOscSpan) * sizeof(float));
+    launch_phasor_table_q64(dmtab_[cur_].as<f2>(), t.mstep, kOscSpan, s);
     mt_up_ = true;
   }
 }
 
 OscDev RefOsc::dev(uint64_t n, hipStream_t s) {
-  // the launch's range plus one run past it (every run a kernel forms lies in the table)
-  if (!rb_.done()) rb_.extend(k_ + n + static_cast<uint64_t>(kOscSpan));
+  // the launch's range plus the longest tile past it (every run a kernel forms lies in the table)
+  if (!rb_.done()) rb_.extend(k_ + n + kOscMargin);
   upload(s);
   if (last_s_[cur_] && last_s_[cur_] != s) multi_[cur_] = true;
   last_s_[cur_] = s;

@@ -68,6 +68,7 @@ class RefOsc {
   int cur_ = 0;
   uint64_t up_ = 0;       // table entries uploaded to dtab_[cur_] (their padding included)
   bool mt_up_ = false;    // dmtab_[cur_] holds this tune's model steps
+  bool pad_up_ = false;   // dtab_[cur_] holds the cycle's continuation past n (final tables with a cycle)
 };
 
 }  // namespace orion
