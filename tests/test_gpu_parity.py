@@ -72,6 +72,25 @@ def ssb_truth(oracle, x, fs=48e3, bfo=1500.0, bw=2800.0):
     return sg.lfilter([1.0, -1.0], [1.0, -r], y)
 
 
+def lpdc_tol(oracle, x, fs, lp_fc, dc_cut, sqrt_map, got):
+    """LpDcCascade tolerance (iir.rs:151-165), as ssb_tol: max(1e-6, 2 x the 1-ulp floor,
+    5 x the reference's own distance from the same cascade in f64 with its f32
+    coefficients). Prints the GPU's own distance from f64 beside the reference's."""
+    import scipy.signal as sg
+
+    b0, b1, b2, a1, a2, r = (float(v) for v in oracle.lpdc_coeffs(fs, np.float32(lp_fc), dc_cut))
+    y = np.asarray(x, np.float64)
+    for _ in range(2):
+        y = sg.lfilter([b0, b1, b2], [1.0, a1, a2], y)
+    truth = sg.lfilter([1.0, -1.0], [1.0, -r], np.sqrt(y) if sqrt_map else y)
+    ref = oracle.lp_dc_cascade(x, fs, lp_fc, dc_cut, sqrt_map)
+    own = nrmse(ref, truth)
+    f = ulp_floor(lambda v: oracle.lp_dc_cascade(v, fs, lp_fc, dc_cut, sqrt_map), x)
+    print(f"[parity]   reference vs f64: {own:.3e}, gpu vs f64: {nrmse(np.asarray(got, np.float64), truth):.3e}, "
+          f"reference 1-ulp floor {f:.3e}")
+    return max(1e-6, 2.0 * f, 5.0 * own)
+
+
 def ssb_tol(oracle, x, fs=48e3, bfo=1500.0, bw=2800.0, got=None):
     """SSB tolerance: max(1e-6, 2 x the 1-ulp floor, 5 x the reference's own distance
     from exact arithmetic). The LpDcCascade is linear (the 1-ulp scaling floor is near
@@ -544,6 +563,44 @@ def test_single_pass_lpdc_geometry(gpu_lib, oracle):
     got = stream(gpu_lib.AmEnvelopeDemod(FS, 5000, abs_approx=True), am, 33_333)
     report("am abs single-pass streamed nrmse",
            nrmse(got, oracle.am_demod(am, FS, 5000.0, abs_approx=(0.9482, 0.3920))), 1e-5)
+
+
+def test_single_pass_lpdc_fronts(gpu_lib, oracle):
+    """k_lpdc_sp (32 samples per lane, 8192-sample chunks after a 256-sample warm-up)
+    for every front end on it: SSB, AM PowerSqrt and AbsApprox, LpDcCascade with and
+    without the sqrt map; chunk-boundary lengths and ragged streamed calls. The linear
+    cascades are judged against the same cascade in f64 (ssb_tol, lpdc_tol)."""
+    ch, out = 8192, 7936
+    a = real_tone(FS, 1200.0, 60_000, 0.4)
+    ssb_iq = oracle.add_awgn(oracle.ssb_mod(a, FS, 2800.0, 1500.0), 1e-3, 7)
+    am_iq = oracle.am_mod(real_tone(FS, 1000.0, 60_000, 0.5), FS, 0.0, 0.8, 0.5)
+    xr = (0.2 * np.abs(cnoise(60_000)) ** 2 + 2.0).astype(np.float32)
+    cases = [
+        ("ssb", lambda: gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0), ssb_iq,
+         lambda v: oracle.ssb_demod(v, FS, 1500.0, 2800.0), None),
+        ("am sqrt", lambda: gpu_lib.AmEnvelopeDemod(FS, 5000.0), am_iq, lambda v: oracle.am_demod(v, FS, 5000.0), 1e-5),
+        ("am abs", lambda: gpu_lib.AmEnvelopeDemod(FS, 5000.0, abs_approx=True), am_iq,
+         lambda v: oracle.am_demod(v, FS, 5000.0, abs_approx=(0.9482, 0.3920)), 1e-5),
+        ("lp_dc", lambda: gpu_lib.LpDcCascade(FS, 2520.0, 2.0), xr,
+         lambda v: oracle.lp_dc_cascade(v, FS, 2520.0, 2.0, False), None),
+        ("lp_dc sqrt", lambda: gpu_lib.LpDcCascade(FS, 2520.0, 2.0, sqrt_map=True), xr,
+         lambda v: oracle.lp_dc_cascade(v, FS, 2520.0, 2.0, True), None),
+    ]
+
+    def tol_of(name, tol, ref_of, v, got):
+        if name == "ssb":
+            return ssb_tol(oracle, v, got=got)
+        if name.startswith("lp_dc"):
+            return lpdc_tol(oracle, v, FS, 2520.0, 2.0, name.endswith("sqrt"), got)
+        return floor_tol(tol, ref_of, v)
+
+    for name, mk, x, ref_of, tol in cases:
+        for n in (ch, ch + 1, ch + out + 1, ch + 3 * out, len(x)):
+            got = mk().process(x[:n])
+            assert np.all(np.isfinite(got))
+            report(f"{name} single-pass n={n} nrmse", nrmse(got, ref_of(x[:n])), tol_of(name, tol, ref_of, x[:n], got))
+        got = stream(mk(), x, 9001)
+        report(f"{name} single-pass streamed 9001 nrmse", nrmse(got, ref_of(x)), tol_of(name, tol, ref_of, x, got))
 
 
 def test_reference_roundtrips_on_gpu(gpu_lib, oracle):

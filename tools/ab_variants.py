@@ -3,6 +3,7 @@
 = lib/) is loaded as its own module, launches are interleaved A B C, B C A, ... so the
 chip's clock state hits every variant alike, one HIP event pair per launch.
   python tools/ab_variants.py --case c5 --rounds 4 --k 10 base v1 v2
+A name may carry engine options for its block: base@scan_path=2 (orion_block_configure).
 Cases: c2 (WBFM 2^26), c4 (WBFM 8 x 2^24), c5 (SSB 128 x 2^20), a10 (SSB 2^24), a11 / a11abs (AM PowerSqrt / AbsApprox 2^24), a7 (DcBlocker
 2^24), a6 (LpCascade 2^24), a9 (FM demod 2^24)."""
 import argparse
@@ -61,10 +62,17 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream(dev)
-    mods = {nm: load(nm) for nm in a.names}
+    libs = {}
     work = {}
-    for nm, m in mods.items():
+    for nm in a.names:
+        lib, *opts = nm.split("@")
+        if lib not in libs:
+            libs[lib] = load(lib)
+        m = libs[lib]
         blk, x = case(m, a.case, dev) if not work else (case(m, a.case, dev)[0], next(iter(work.values()))[1])
+        for o in opts:
+            k, v = o.split("=")
+            blk.configure_option(k, int(v))
         out = blk.process_device(x)
         work[nm] = (blk, x, out)
     for nm in a.names:
