@@ -424,6 +424,19 @@ def main():
         line["roofline"].update(bound="fp32", achieved=round(tflops, 2), peak=FP32_PEAK_TFLOPS, unit="TFLOP/s",
                                 frac=round(tflops / FP32_PEAK_TFLOPS, 4), hbm_gbs=round(achieved, 1),
                                 hbm_frac=round(achieved / HBM_PEAK_GBS, 4))
+    # per-launch spread (after the timed region): one event pair per launch,
+    # so the clock's step-down across back-to-back launches is visible beside the average
+    pairs = []
+    for _ in range(max(args.steps, 10)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        step()
+        e1.record(stream)
+        pairs.append((e0, e1))
+    torch.cuda.synchronize(dev)
+    per = sorted(e0.elapsed_time(e1) for e0, e1 in pairs)
+    line["roofline"]["per_launch_ms"] = {"min": round(per[0], 4), "median": round(per[len(per) // 2], 4),
+                                         "max": round(per[-1], 4), "launches": len(per)}
     # on-box read ceiling (after the timed region): the library's streaming-read probe
     # over this rank's input, 10 launches between events. Diagnostic
     # only: a probe that cannot run (input below one tile per wave) leaves it null.

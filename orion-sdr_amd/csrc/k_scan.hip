@@ -17,8 +17,6 @@ constexpr int kSpMinW16 = 6;     // the same at 16 samples per lane
 constexpr int kSpBatch = 8;      // k_scan_sp staging: loads issued together per thread (complex input)
 constexpr int kSpBatchReal = 8;  // (real input)
 constexpr int kScanSpMinW = 4;   // waves per SIMD k_scan_sp is compiled for (4: <= 128 VGPRs, spills 52-132 B)
-constexpr int kSpSsbMask = 6;    // k_lpdc_sp Ssb: which loops take the unguarded copies (1 LP re-run, 2 DC
-                                 // zero-state, 4 DC re-run, 8 stores); 6 measured best (r4_lpdc_guard_ab.txt)
 
 __device__ __forceinline__ int pos(int e) { return e + (e >> 4); }
 
@@ -581,16 +579,15 @@ __global__ __launch_bounds__(NT, SC > 16 ? kSpMinW : kSpMinW16) void k_lpdc_sp(c
   wave_order();  // wave-local staging
 
   // ---- LP4: zero-state lane aggregates, block scan, exact re-run ----
-  // Guards on the element range: the lane's valid samples are i < hi (the staged samples
-  // past cnt are zeros); `fast` (block-uniform: a full chunk that is not the call's last)
-  // selects unguarded copies of the per-sample loops — for Ssb (three phasor forms in its
-  // staging) only the DC loops': its LP4 re-run and store copies measured slower
-  // (r4_lpdc_guard_ab.txt).
+  // The per-sample loops run unguarded over the lane's C staged samples: the lane's valid
+  // samples are i < hi, the staged samples past cnt are zeros, and the recurrences are
+  // causal, so what runs past cnt reaches only outputs past cnt (never stored) and the
+  // pairs of lanes past cnt. The call's carried state, taken at sample cnt - 1, is
+  // re-derived by the lane holding it (last chunk only; `carry_lane`).
   const int hi = min(cnt - t * C, C);
   const bool full_nl = cnt == CH && !last;
-  const bool fast = PR != Pre::Ssb && full_nl;
-  // per loop for Ssb (A/B mask): 1 LP re-run, 2 DC zero-state, 4 DC re-run, 8 stores
-  auto fast_for = [&](int bit) { return PR == Pre::Ssb ? ((kSpSsbMask & bit) != 0 && full_nl) : fast; };
+  const int il = cnt - 1 - t * C;  // the call's last sample in this lane's run (last chunk)
+  const bool carry_lane = last && il >= 0 && il < C;
   float xs[C];
 #pragma unroll
   for (int i = 0; i < C; ++i) xs[i] = sb[posS<SC>(t * C + i)];
@@ -641,16 +638,19 @@ __global__ __launch_bounds__(NT, SC > 16 ? kSpMinW : kSpMinW16) void k_lpdc_sp(c
   }
 #pragma unroll
   for (int i = 0; i < S; ++i) ef[i] = static_cast<float>(e[i]);
-  auto lp_rerun = [&](auto guarded) {
+  if (carry_lane) {  // the LP4 state after sample cnt - 1 (the staged inputs are still in sb)
+    float e2[S] = {ef[0], ef[1], ef[2], ef[3]};
+#pragma unroll 1
+    for (int i = 0; i <= il; ++i) (void)lp.step(e2, sb[posS<SC>(t * C + i)]);
+    float* co = a.carry_out + ch * kScanCarry;
 #pragma unroll
-    for (int i = 0; i < C; ++i)
-      if (!decltype(guarded)::value || i < hi) {
-        xs[i] = lp.step(ef, xs[i]);  // LP output x (f32, reference update)
-        if constexpr (PR == Pre::AmSqrt || PR == Pre::RealLpSqrt) xs[i] = sqrtf(xs[i]);  // process_mapped(.., f32::sqrt)
-      }
-  };
-  if (fast_for(1)) lp_rerun(std::false_type{});
-  else lp_rerun(std::true_type{});
+    for (int i = 0; i < S; ++i) co[i] = e2[i];
+  }
+#pragma unroll
+  for (int i = 0; i < C; ++i) {
+    xs[i] = lp.step(ef, xs[i]);  // LP output x (f32, reference update)
+    if constexpr (PR == Pre::AmSqrt || PR == Pre::RealLpSqrt) xs[i] = sqrtf(xs[i]);  // process_mapped(.., f32::sqrt)
+  }
   wave_order();  // (the wave's own inputs: read before they are overwritten, in order)
 #pragma unroll
   for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
@@ -673,16 +673,14 @@ __global__ __launch_bounds__(NT, SC > 16 ? kSpMinW : kSpMinW16) void k_lpdc_sp(c
   const bool lane_on = t * C >= warm;
   {
     float y = 0.0f;
-    auto dc_zero = [&](auto guarded) {
+    {
       float xp = xprev0;
 #pragma unroll
       for (int i = 0; i < C; ++i) {
-        if (!decltype(guarded)::value || i < hi) y = (xs[i] - xp) + r * y;
+        y = (xs[i] - xp) + r * y;
         xp = xs[i];
       }
-    };
-    if (fast_for(2)) dc_zero(std::false_type{});
-    else dc_zero(std::true_type{});
+    }
     d = lane_on ? static_cast<double>(y) : 0.0;
     // r^v over the lane's v valid samples by squaring (equal to the running product to
     // f64 rounding, ~1e-15 relative: far below the f32 outputs)
@@ -810,43 +808,32 @@ __global__ __launch_bounds__(NT, SC > 16 ? kSpMinW : kSpMinW16) void k_lpdc_sp(c
   }
   dc_combine(wm, wd, em, ed);  // waves before, then lanes before
   float y = static_cast<float>(__builtin_fma(em, excl_sh, ed));
-  auto dc_rerun = [&](auto guarded) {  // (warm-up lanes' outputs are not stored)
+  {  // (warm-up lanes' outputs are not stored)
     float xp = xprev0;
 #pragma unroll
     for (int i = 0; i < C; ++i) {
-      float out = 0.0f;
-      if (!decltype(guarded)::value || i < hi) {
-        y = (xs[i] - xp) + r * y;  // dsp/iir.rs:161 (y1 - dc_x1) + r * dc_y1
-        out = y;
-      }
+      y = (xs[i] - xp) + r * y;  // dsp/iir.rs:161 (y1 - dc_x1) + r * dc_y1
       xp = xs[i];
-      xs[i] = out;
+      xs[i] = y;
     }
-  };
-  if (fast_for(4)) dc_rerun(std::false_type{});
-  else dc_rerun(std::true_type{});
-  if (last && t * C <= cnt - 1 && cnt - 1 < t * C + C) {  // carried state of the next call
-    float* co = a.carry_out + ch * kScanCarry;
-    if constexpr (LP)
-#pragma unroll
-      for (int i = 0; i < S; ++i) co[i] = ef[i];  // ef ran to the lane's last valid sample
-    const int il = cnt - 1 - t * C;
-    float xl = 0.0f;
-#pragma unroll
-    for (int i = 0; i < C; ++i)
-      if (i == il) xl = sb[posS<SC>(t * C + i)];
-    co[DX] = xl;
-    co[DY] = y;
-    co[6] = ci[6];
-    co[7] = ci[7];
   }
+  // carried state of the next call: x1 = the LP output at sample cnt - 1 (still in sb),
+  // y1 = the output there
+  const float xl = carry_lane ? sb[posS<SC>(cnt - 1)] : 0.0f;
   wave_order();  // output staging, wave-local (every cross-wave read of sb was before the last barrier)
 #pragma unroll
   for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
   wave_order();
+  if (carry_lane) {
+    float* co = a.carry_out + ch * kScanCarry;
+    co[DX] = xl;
+    co[DY] = sb[posS<SC>(cnt - 1)];
+    co[6] = ci[6];
+    co[7] = ci[7];
+  }
   float* yo = static_cast<float*>(a.y) + ch * a.y_stride + o0;
   const int e0 = wave * (64 * SC) + lane;
-  if (fast_for(8)) {
+  if (full_nl) {
     const int kmin = (warm - wave * (64 * SC)) >> 6;  // wave-uniform: the warm-up is whole rows of 64
 #pragma unroll
     for (int k = 0; k < SC; ++k)
@@ -948,7 +935,7 @@ __global__ __launch_bounds__(NT, kScanSpMinW) void k_scan_sp(const ScanArgs a, i
       } else {
         o = premap_v<PR>(a, ch, base + e, base, Ro, z[j], zp[j]);
       }
-      if (!G || e < cnt) sb[posS_row<SC, NT>(posS<SC>(t), k0 + j)] = o;  // e = t + (k0 + j) NT
+      sb[posS_row<SC, NT>(posS<SC>(t), k0 + j)] = !G || e < cnt ? o : 0.0f;  // e = t + (k0 + j) NT
     }
   }
   };
@@ -956,8 +943,11 @@ __global__ __launch_bounds__(NT, kScanSpMinW) void k_scan_sp(const ScanArgs a, i
   else stage(std::true_type{});
   __syncthreads();
 
-  // `fast` (block-uniform: a full chunk that is not the call's last) selects unguarded
-  // copies of the per-sample loops (as k_lpdc_sp)
+  // The per-sample loops run unguarded (as k_lpdc_sp): samples past cnt are staged as
+  // zeros, and what the causal recurrence computes past cnt reaches only outputs past cnt
+  // (never stored); the lane holding sample cnt - 1 re-derives the carried state.
+  const int il = cnt - 1 - t * C;
+  const bool carry_lane = last && il >= 0 && il < C;
   float xs[C];
 #pragma unroll
   for (int i = 0; i < C; ++i) xs[i] = sb[posS<SC>(t * C + i)];
@@ -970,16 +960,10 @@ __global__ __launch_bounds__(NT, kScanSpMinW) void k_scan_sp(const ScanArgs a, i
     // chunk enter as zeros: only the last partial lane differs, whose state reaches no
     // valid output)
     const float* __restrict__ E = a.zmap;
-    auto zs = [&](auto guarded) {
 #pragma unroll
-      for (int i = 0; i < C; ++i) {
-        const float xv = !decltype(guarded)::value || t * C + i < cnt ? xs[i] : 0.0f;
+    for (int i = 0; i < C; ++i)
 #pragma unroll
-        for (int k = 0; k < S; ++k) s0[k] = __builtin_fmaf(E[i * S + k], xv, s0[k]);
-      }
-    };
-    if (fast) zs(std::false_type{});
-    else zs(std::true_type{});
+      for (int k = 0; k < S; ++k) s0[k] = __builtin_fmaf(E[i * S + k], xs[i], s0[k]);
   }
   double q[S];
 #pragma unroll
@@ -1072,18 +1056,15 @@ __global__ __launch_bounds__(NT, kScanSpMinW) void k_scan_sp(const ScanArgs a, i
     ef[i] = static_cast<float>(lane == 0 ? cw[i] : o);
   }
   }  // TR
-  auto rerun = [&](auto guarded) {
+  if (carry_lane) {  // carried state of the next call: the state after sample cnt - 1
+    float e2[S];
 #pragma unroll
-    for (int i = 0; i < C; ++i)
-      if (!decltype(guarded)::value || t * C + i < cnt)
-        xs[i] = postmap<PO>(a, rr.step(ef, xs[i]));  // the reference's f32 update
-  };
-  if (fast) rerun(std::false_type{});
-  else rerun(std::true_type{});
-  if (last && t * C <= cnt - 1 && cnt - 1 < t * C + C) {  // carried state of the next call
+    for (int i = 0; i < S; ++i) e2[i] = ef[i];
+#pragma unroll 1
+    for (int i = 0; i <= il; ++i) (void)rr.step(e2, sb[posS<SC>(t * C + i)]);
     float* co = a.carry_out + ch * kScanCarry;
 #pragma unroll
-    for (int i = 0; i < S; ++i) co[i] = ef[i];  // ef ran to the lane's last valid sample
+    for (int i = 0; i < S; ++i) co[i] = e2[i];
     for (int i = S; i < 6; ++i) co[i] = 0.0f;
     if constexpr (PR == Pre::Fm || PR == Pre::Pm) {
       const f2* x = static_cast<const f2*>(a.x) + ch * a.x_stride;
@@ -1095,6 +1076,8 @@ __global__ __launch_bounds__(NT, kScanSpMinW) void k_scan_sp(const ScanArgs a, i
       co[7] = ci[7];
     }
   }
+#pragma unroll
+  for (int i = 0; i < C; ++i) xs[i] = postmap<PO>(a, rr.step(ef, xs[i]));  // the reference's f32 update
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < C; ++i) sb[posS<SC>(t * C + i)] = xs[i];
