@@ -40,6 +40,15 @@ __device__ __forceinline__ void lds_barrier() {
 // in order); also a compiler fence. For hand-offs inside one wave: no barrier.
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// A read-only table the host wrote before the launch, read at wave-uniform indices: in
+// the constant address space the compiler reads it with scalar loads (one s_load per
+// 4-16 dwords for the wave) instead of a vector load per use whose 64 lanes each
+// return the same bytes through the CU's load-return path.
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* uniform_table(const T* p) {
+  return (const __attribute__((address_space(4))) T*)(p);
+}
+
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 splat2(float x) { return f2{x, x}; }
 

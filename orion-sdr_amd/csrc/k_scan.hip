@@ -595,7 +595,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? kSpMinW : kSpMinW16) void k_lpdc_sp(c
   if constexpr (LP) {
   float s0[S] = {0, 0, 0, 0};
   {  // the lane run's zero-state end state as the linear map (k_scan_sp)
-    const float* __restrict__ E = a.zmap;
+    const auto E = uniform_table(a.zmap);
 #pragma unroll
     for (int i = 0; i < C; ++i)
 #pragma unroll
@@ -959,7 +959,7 @@ __global__ __launch_bounds__(NT, kScanSpMinW) void k_scan_sp(const ScanArgs a, i
     // (independent FMAs instead of the recurrence's dependent chain; samples past the
     // chunk enter as zeros: only the last partial lane differs, whose state reaches no
     // valid output)
-    const float* __restrict__ E = a.zmap;
+    const auto E = uniform_table(a.zmap);
 #pragma unroll
     for (int i = 0; i < C; ++i)
 #pragma unroll
