@@ -150,8 +150,16 @@ orion_block* orion_biquad_new(float b0, float b1, float b2, float a1, float a2);
 /* dsp/iir.rs:111-137 LpDcCascade::design(fs, lp_fc, dc_cut_hz); process :151-165 (LP4 then
  * the DC blocker). f32->f32 */
 orion_block* orion_lp_dc_cascade_new(float fs, float lp_fc, float dc_cut_hz);
-/* on = 1: process_mapped(x, f32::sqrt) (iir.rs:170-186: sqrt between the LP4 and the DC
- * blocker, the AM-PowerSqrt use) instead of process; set before the first call. */
+/* LpDcCascade::process_mapped(x, f) (iir.rs:170-186: f between the LP4 and the DC blocker)
+ * instead of process (:151-165), for the maps a C caller can name: ORION_MAP_IDENTITY
+ * (|v| v, the same as process), ORION_MAP_SQRT (f32::sqrt, the AM-PowerSqrt use,
+ * demodulate/am.rs:55) or ORION_MAP_ABS (f32::abs). Set before the first call.
+ * ORION_E_ARG for another value, ORION_E_TYPE for another block. */
+#define ORION_MAP_IDENTITY 0
+#define ORION_MAP_SQRT 1
+#define ORION_MAP_ABS 2
+int orion_lp_dc_cascade_set_map(orion_block* b, int map);
+/* on = 1: orion_lp_dc_cascade_set_map(b, ORION_MAP_SQRT); on = 0: ORION_MAP_IDENTITY. */
 int orion_lp_dc_cascade_set_sqrt_map(orion_block* b, int on);
 /* dsp/dc.rs:15-21 DcBlocker::new(fs, cut_hz); Block impl :40-58. f32->f32 */
 orion_block* orion_dc_blocker_new(float fs, float cut_hz);

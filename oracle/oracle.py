@@ -172,10 +172,15 @@ def biquad(x, b0, b1, b2, a1, a2):
     return out
 
 
-def lp_dc_cascade(x, fs, lp_fc, dc_cut, sqrt_map=False):
+_LPDC_MAPS = {None: -1, "identity": 0, "sqrt": 1, "abs": 2}
+
+
+def lp_dc_cascade(x, fs, lp_fc, dc_cut, sqrt_map=False, map=None):
+    """iir.rs:151-165 process, or :170-186 process_mapped(x, f) with map "identity" /
+    "sqrt" / "abs" (sqrt_map=True: "sqrt")."""
     x = _f32(x)
     out = np.zeros_like(x)
-    lib().o_run_lpdc(fs, lp_fc, dc_cut, 1 if sqrt_map else 0, x, out, len(x))
+    lib().o_run_lpdc(fs, lp_fc, dc_cut, _LPDC_MAPS["sqrt" if sqrt_map else map], x, out, len(x))
     return out
 
 

@@ -372,6 +372,21 @@ float o_lpdc_process(o_lpdc *c, float x) {
     return y;
 }
 /* dsp/iir.rs:170-186 process_mapped with f = f32::sqrt (am.rs:54) */
+/* iir.rs:170-186 process_mapped(x, f) for the maps the engine exposes (ORION_MAP_*):
+ * 0 identity (|v| v: the same as process), 1 f32::sqrt, 2 f32::abs. */
+float o_lpdc_process_mapped(o_lpdc *c, float x, int map) {
+    float y0 = fmaf(x, c->b0, c->z0_1);
+    c->z0_1 = fmaf(x, c->b1, c->z0_2) - c->a1 * y0;
+    c->z0_2 = x * c->b2 - c->a2 * y0;
+    float y1 = fmaf(y0, c->b0, c->z1_1);
+    c->z1_1 = fmaf(y0, c->b1, c->z1_2) - c->a1 * y1;
+    c->z1_2 = y0 * c->b2 - c->a2 * y1;
+    float mapped = map == 1 ? sqrtf(y1) : map == 2 ? fabsf(y1) : y1;
+    float y = mapped - c->dc_x1 + c->r * c->dc_y1;
+    c->dc_x1 = mapped;
+    c->dc_y1 = y;
+    return y;
+}
 float o_lpdc_process_mapped_sqrt(o_lpdc *c, float x) {
     float y0 = fmaf(x, c->b0, c->z0_1);
     c->z0_1 = fmaf(x, c->b1, c->z0_2) - c->a1 * y0;
@@ -695,9 +710,10 @@ size_t o_run_biquad(float b0, float b1, float b2, float a1, float a2, const floa
 }
 /* LpDcCascade::design(fs, lp_fc, dc_cut) (iir.rs:111-137): process (:151-165), or
  * process_mapped(x, f32::sqrt) (:170-186) when sqrt_map. */
-size_t o_run_lpdc(float fs, float lp_fc, float dc_cut, int sqrt_map, const float *in, float *out, size_t n) {
+/* map: -1 process (:151-165), else process_mapped with map 0 identity, 1 sqrt, 2 abs */
+size_t o_run_lpdc(float fs, float lp_fc, float dc_cut, int map, const float *in, float *out, size_t n) {
     o_lpdc c; o_lpdc_design(&c, fs, lp_fc, dc_cut);
-    for (size_t i = 0; i < n; i++) out[i] = sqrt_map ? o_lpdc_process_mapped_sqrt(&c, in[i]) : o_lpdc_process(&c, in[i]);
+    for (size_t i = 0; i < n; i++) out[i] = map < 0 ? o_lpdc_process(&c, in[i]) : o_lpdc_process_mapped(&c, in[i], map);
     return n;
 }
 size_t o_run_fir(float fs, float pass_hz, float trans_hz, const float *in, float *out, size_t n, size_t chunk) {

@@ -93,6 +93,7 @@ typedef struct { float z0_1, z0_2, z1_1, z1_2, dc_x1, dc_y1, b0, b1, b2, a1, a2,
 void o_lpdc_design(o_lpdc *c, float fs, float lp_fc, float dc_cut_hz);
 float o_lpdc_process(o_lpdc *c, float x);
 float o_lpdc_process_mapped_sqrt(o_lpdc *c, float x);
+float o_lpdc_process_mapped(o_lpdc *c, float x, int map);
 
 /* ---- dsp/dc.rs:8-59 (DcBlocker) ---- */
 typedef struct { float r, x1, y1; } o_dc;
@@ -165,7 +166,7 @@ size_t o_run_rotator_retune(float f1, float fs, int mode, const oc32 *in, void *
                             float f2, float fs2, int reset_at_switch);
 size_t o_run_nco(float f1, float fs, int mode, const oc32 *in, oc32 *out, size_t n, size_t n_switch, float f2);
 size_t o_run_biquad(float b0, float b1, float b2, float a1, float a2, const float *in, float *out, size_t n);
-size_t o_run_lpdc(float fs, float lp_fc, float dc_cut, int sqrt_map, const float *in, float *out, size_t n);
+size_t o_run_lpdc(float fs, float lp_fc, float dc_cut, int map, const float *in, float *out, size_t n);
 size_t o_run_fir(float fs, float pass_hz, float trans_hz, const float *in, float *out, size_t n, size_t chunk);
 size_t o_run_firiq(const float *taps, size_t ntaps, const oc32 *in, oc32 *out, size_t n, size_t chunk);
 void   o_run_firiq_aligned(const float *taps, size_t ntaps, oc32 *io, size_t n);

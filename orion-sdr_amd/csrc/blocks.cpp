@@ -153,7 +153,9 @@ class CopyPool {
     for (;;) {
       const size_t i = next_.fetch_add(1);
       if (i >= pieces_) return;
-      const size_t per = (bytes_ / pieces_ + 63) & ~size_t(63);
+      // ceiling division before the 64-B round-up: the pieces always cover bytes_
+      // (a floor here dropped the last few bytes when bytes_ % pieces_ != 0)
+      const size_t per = ((bytes_ + pieces_ - 1) / pieces_ + 63) & ~size_t(63);
       const size_t off = std::min(bytes_, i * per), len = std::min(per, bytes_ - off);
       std::memcpy(dst_ + off, src_ + off, len);
       if (done_.fetch_add(1) + 1 == pieces_) {
@@ -222,10 +224,16 @@ struct Block::HostPipe {
     }
     pin_bytes = 0;
   }
-  // Called at the start of a host call (no copy of this pipe is in flight then).
+  // Grows the pinned buffers. A DMA of this pipe may still be queued (process_host's
+  // d2h_staged runs after h2d_staged without a sync), so every copy that
+  // reads or writes the old buffers is waited for before they are freed.
   void pins(size_t bytes) {
     bytes = std::min(kPinBytes, (bytes + 4095) & ~size_t(4095));
     if (bytes <= pin_bytes) return;
+    for (int b = 0; b < 2; ++b) {
+      ORION_HIP(hipEventSynchronize(ev_in[b]));
+      ORION_HIP(hipEventSynchronize(ev_out[b]));
+    }
     free_pins();
     for (int b = 0; b < 2; ++b) {
       ORION_HIP(hipHostMalloc(&pin_in[b], bytes, hipHostMallocDefault));
@@ -839,6 +847,7 @@ class WbfmBlock final : public Block {
     if (path == kPathGraph) {
       graph(static_cast<const f2*>(in), n, static_cast<float*>(out), out_cap, n_dec, s);
       k0_ += n;
+      processed_ = true;
       return {n, n_dec};
     }
     const int nxt = cur_ ^ 1;
@@ -906,6 +915,7 @@ class WbfmBlock final : public Block {
     }
     cur_ = nxt;
     k0_ += n;
+    processed_ = true;
     return {n, n_dec};
   }
   void reset() override {
@@ -917,21 +927,62 @@ class WbfmBlock final : public Block {
     }
     ORION_HIP(hipDeviceSynchronize());
     cur_ = 0;
-    k0_ = 0;
+    // Every path restarts at the seek origin (0 unless orion_wbfm_chain_seek set one):
+    // the graph path's Rotator is re-sought there when its stages are rebuilt.
+    k0_ = seek_;
+    processed_ = false;
     stages_.clear();  // the graph path's blocks restart from their constructors' state
   }
   std::vector<float> taps(int which) const override { return which == 0 ? h_dec_ : h_aud_; }
+  // The graph path's stages are blocks with error words of their own (the FM demod's
+  // cross-workgroup scan): a timeout in any of them invalidates the chain's output.
+  void check_device_errors() override {
+    Block::check_device_errors();
+    for (Stages& st : stages_)
+      for (Block* b : {st.rot.get(), st.dec.get(), st.fm.get(), st.aud.get()}) {
+        try {
+          b->check_device_errors();
+        } catch (const HipError& e) {
+          throw HipError(std::string(name()) + " (graph path stage): " + e.what());
+        }
+      }
+  }
+  // Moves the NCO phase origin only; the carried filter state (decimator and FIR
+  // history, discriminator sample, LpCascade) is kept on every path, as the fused
+  // paths keep their carry.
+  // On the fused paths the decimator history is kept as RAW input and re-mixed by each
+  // call at its own indices (phasor e^{j k step}); a mid-stream seek therefore rotates it
+  // by e^{j (k_old - k_new) step}, so that it re-mixes to the samples it was mixed to
+  // before: what the graph path's decimator (which holds mixed samples) keeps.
   void seek(uint64_t index) {
+    if (processed_ && fused_ok_ && resolved_path() != kPathGraph && index != k0_) rebase_history(index);
     k0_ = index;
-    stages_.clear();
     seek_ = index;
+    for (Stages& st : stages_) osc_seek(st.rot.get(), index);
+  }
+  void rebase_history(uint64_t index) {
+    std::vector<f2> h(static_cast<size_t>(nch_) * kWbfmHist);
+    ORION_HIP(hipDeviceSynchronize());  // the last call has written hist_[cur_]
+    ORION_HIP(hipMemcpy(h.data(), hist_[cur_].as<void>(), h.size() * sizeof(f2), hipMemcpyDeviceToHost));
+    for (int ch = 0; ch < nch_; ++ch) {
+      const uint64_t q = (k0_ - index) * steps_h_[ch];  // mod 2^64: the phase difference as Q0.64
+      const long double a = static_cast<long double>(q) / 18446744073709551616.0L * 6.283185307179586476925L;
+      const long double c = std::cos(a), sn = std::sin(a);
+      for (int t = 0; t < kWbfmHist; ++t) {
+        f2& v = h[static_cast<size_t>(ch) * kWbfmHist + t];
+        const long double re = v.x, im = v.y;
+        v.x = static_cast<float>(re * c - im * sn);
+        v.y = static_cast<float>(re * sn + im * c);
+      }
+    }
+    ORION_HIP(hipMemcpy(hist_[cur_].as<void>(), h.data(), h.size() * sizeof(f2), hipMemcpyHostToDevice));
   }
   int set_path(int path, int max_seg) {
     if ((path != kPathAuto && path != kPathSeg && path != kPathSplit && path != kPathGraph) || max_seg < 0) return -3;
     if (path == kPathSeg && !seg_ok_) return -3;
     if (path == kPathSplit && !split_ok_) return -3;
     if (path != path_) {
-      if (k0_ != 0) return -3;  // the paths carry their state differently: choose before the first call
+      if (processed_) return -3;  // the paths carry their state differently: choose before the first call
       stages_.clear();
     }
     path_ = path;
@@ -1009,6 +1060,7 @@ class WbfmBlock final : public Block {
       tabs.insert(tabs.end(), t.begin(), t.end());
     }
     step_.upload(steps.data(), steps.size() * sizeof(uint64_t));
+    steps_h_ = steps;
     tab_.upload(tabs.data(), tabs.size() * sizeof(float));
   }
   // The segmented chain's audio FIR runs on f16 matrix cores with hi + lo parts
@@ -1080,8 +1132,10 @@ class WbfmBlock final : public Block {
   DevBuf step_, tab_, carry_[2], hist_[2], lanemats_, phi_, hand_, flags_, trace_, afrag_, mixed_, dec_, mats_;
   std::vector<Stages> stages_;
   uint64_t seek_ = 0;
+  std::vector<uint64_t> steps_h_;  // the fused paths' per-channel mixer steps (Q0.64)
   int cur_ = 0;
   uint64_t k0_ = 0;
+  bool processed_ = false;  // a call has run since construction or reset()
 };
 
 }  // namespace

@@ -80,8 +80,9 @@ class Block {
   // Errors a kernel flagged in the handle's device error word (a cross-workgroup
   // wait that timed out): throws HipError and clears the word if one is set. The
   // word is host-visible (pinned, coherent), so this needs no sync; it sees every
-  // kernel of the handle that has finished (orion_block_status).
-  void check_device_errors();
+  // kernel of the handle that has finished (orion_block_status). A composite block
+  // (the WBFM chain's graph path) also polls the words of the blocks it owns.
+  virtual void check_device_errors();
   virtual void reset() = 0;
   virtual int channels() const { return 1; }
   // process_device may be given overlapping in/out ranges (the block stages its

@@ -365,12 +365,17 @@ orion_block* orion_biquad_new(float b0, float b1, float b2, float a1, float a2) 
 orion_block* orion_lp_dc_cascade_new(float fs, float lp_fc, float dc_cut_hz) {
   return make([&] { return orion::make_lp_dc_cascade(fs, lp_fc, dc_cut_hz); });
 }
-int orion_lp_dc_cascade_set_sqrt_map(orion_block* b, int on) {
+int orion_lp_dc_cascade_set_map(orion_block* b, int map) {
   if (!b) return fail(ORION_E_NULL, "null handle");
   return guarded([&] {
-    if (orion::lp_dc_cascade_set_sqrt(b->impl.get(), on != 0)) return fail(ORION_E_TYPE, "not an LpDcCascade");
+    const int rc = orion::lp_dc_cascade_set_map(b->impl.get(), map);
+    if (rc == -4) return fail(ORION_E_TYPE, "not an LpDcCascade");
+    if (rc == -3) return fail(ORION_E_ARG, "unknown process_mapped map (ORION_MAP_IDENTITY / SQRT / ABS)");
     return ORION_OK;
   });
+}
+int orion_lp_dc_cascade_set_sqrt_map(orion_block* b, int on) {
+  return orion_lp_dc_cascade_set_map(b, on ? ORION_MAP_SQRT : ORION_MAP_IDENTITY);
 }
 orion_block* orion_dc_blocker_new(float fs, float cut_hz) {
   return make([&] { return orion::make_dc_blocker(fs, cut_hz); });

@@ -183,6 +183,7 @@ __device__ __forceinline__ void stage(const ScanArgs& a, int ch, long long base,
 template <Post PO>
 __device__ __forceinline__ float postmap(const ScanArgs& a, float y) {
   if constexpr (PO == Post::Sqrt) return sqrtf(y);  // am.rs:54 process_mapped(.., f32::sqrt)
+  else if constexpr (PO == Post::Abs) return fabsf(y);  // process_mapped(.., f32::abs) (iir.rs:170-186)
   else if constexpr (PO == Post::Gain) return y * a.c.gain;  // cw.rs:41
   else return y;
 }
@@ -489,7 +490,7 @@ __device__ __forceinline__ void stage_sp(const ScanArgs& a, int ch, long long ba
   static_assert(kScanCH % WR == 0 && SC * NT <= 2 * kScanCH, "wave ranges inside one phasor table span");
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int e0 = w * WR + l;
-  if constexpr (PR == Pre::Real || PR == Pre::RealLp || PR == Pre::RealLpSqrt) {  // f32 input
+  if constexpr (PR == Pre::Real || PR == Pre::RealLp || PR == Pre::RealLpSqrt || PR == Pre::RealLpAbs) {  // f32 input
     const float* __restrict__ xr = static_cast<const float*>(a.x) + ch * a.x_stride + base;
     float v[SC];
 #pragma unroll
@@ -650,6 +651,7 @@ __global__ __launch_bounds__(NT, SC > 16 ? kSpMinW : kSpMinW16) void k_lpdc_sp(c
   for (int i = 0; i < C; ++i) {
     xs[i] = lp.step(ef, xs[i]);  // LP output x (f32, reference update)
     if constexpr (PR == Pre::AmSqrt || PR == Pre::RealLpSqrt) xs[i] = sqrtf(xs[i]);  // process_mapped(.., f32::sqrt)
+    if constexpr (PR == Pre::RealLpAbs) xs[i] = fabsf(xs[i]);                          // process_mapped(.., f32::abs)
   }
   wave_order();  // (the wave's own inputs: read before they are overwritten, in order)
 #pragma unroll
@@ -1288,6 +1290,8 @@ void launch_lpdc_sp(Pre pre, const ScanArgs& a, const double* mats_lp, int nch, 
     k_lpdc_sp<Pre::RealLp, kLpdcSC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else if (pre == Pre::RealLpSqrt) {
     k_lpdc_sp<Pre::RealLpSqrt, kLpdcSC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
+  } else if (pre == Pre::RealLpAbs) {
+    k_lpdc_sp<Pre::RealLpAbs, kLpdcSC><<<g, NT, 0, s>>>(a, mats_lp, nch, rec, epoch);
   } else {
     throw std::invalid_argument("single-pass LpDc scan: unsupported front end");
   }
@@ -1334,6 +1338,7 @@ void launch_scan(RecK rec, Pre pre, Post post, const ScanArgs& a, int nch, hipSt
   if (rec == RecK::RK && pre == Pre::PR && post == Post::PO) return run3<RecK::RK, Pre::PR, Post::PO>(a, nch, s);
   ORION_SCAN(LP4, Real, Id)
   ORION_SCAN(LP4, Real, Sqrt)
+  ORION_SCAN(LP4, Real, Abs)
   ORION_SCAN(BQ, Real, Id)
   ORION_SCAN(LPDC, Real, Id)
   ORION_SCAN(DC, Real, Id)

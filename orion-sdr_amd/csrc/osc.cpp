@@ -158,7 +158,9 @@ OscDev RefOsc::dev(uint64_t n, hipStream_t s) {
   // the launch's range plus the longest tile past it (every run a kernel forms lies in the table)
   if (!rb_.done()) rb_.extend(k_ + n + kOscMargin);
   upload(s);
-  if (last_s_[cur_] && last_s_[cur_] != s) multi_[cur_] = true;
+  // used_ (not a non-null last stream) says a stream was seen: the null stream is a
+  // stream of its own here (null then a non-blocking stream is two streams)
+  if (used_[cur_] && last_s_[cur_] != s) multi_[cur_] = true;
   last_s_[cur_] = s;
   used_[cur_] = true;
   const RecTable& t = tab();

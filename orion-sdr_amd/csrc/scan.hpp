@@ -38,8 +38,9 @@ enum class Pre : int {
   Cw = 6,      // demodulate/cw.rs:38-39
   RealLp = 7,      // f32 input through the LP4 (+ DC) of LpDcCascade::process (iir.rs:151-165)
   RealLpSqrt = 8,  // the same with sqrt between LP4 and DC: process_mapped(x, f32::sqrt) (iir.rs:170-186)
+  RealLpAbs = 9,   // the same with abs: process_mapped(x, f32::abs)
 };
-enum class Post : int { Id = 0, Sqrt = 1, Gain = 2 };
+enum class Post : int { Id = 0, Sqrt = 1, Gain = 2, Abs = 3 };
 enum class RecK : int { LP4 = 0, LPDC = 1, DC = 2, ONEPOLE = 3, BQ = 4 };
 
 // Matrices of the chunk transition, all S x S row-major f32, in one device buffer.

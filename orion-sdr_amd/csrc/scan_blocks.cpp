@@ -50,7 +50,7 @@ class ScanStage {
       dc_only_ = true;
     }
     if (rec == RecK::LPDC && (pre == Pre::Ssb || pre == Pre::AmAbs || pre == Pre::AmSqrt || pre == Pre::RealLp ||
-                              pre == Pre::RealLpSqrt)) {
+                              pre == Pre::RealLpSqrt || pre == Pre::RealLpAbs)) {
       const StateSpace lp = lp_cascade_ss(BiquadCoeffs{c.b0, c.b1, c.b2, c.a1, c.a2});
       const auto m = mat_pow(lp.A, 4, kSpWarm);
       double fro = 0.0;
@@ -322,10 +322,12 @@ class AmBlock final : public ScanBlock {
   DevBuf tmp_;
 };
 
-// dsp/iir.rs:86-187 LpDcCascade as an f32 block: process (LP4 -> DC blocker) or, with
-// the sqrt map, process_mapped(x, f32::sqrt) (LP4 -> sqrt -> DC, the AM-PowerSqrt use).
-// One pass (k_lpdc_sp<RealLp / RealLpSqrt>) when the LP4 forgets within the warm-up;
-// otherwise the three-kernel LpDc scan, or (sqrt map) an LP4 scan and a DC scan.
+// dsp/iir.rs:86-187 LpDcCascade as an f32 block: process (LP4 -> DC blocker) or
+// process_mapped(x, f) (LP4 -> f -> DC) with f one of the maps the ABI names: identity
+// (== process), f32::sqrt (the AM-PowerSqrt use, am.rs:55) or f32::abs.
+// One pass (k_lpdc_sp<RealLp / RealLpSqrt / RealLpAbs>) when the LP4 forgets within the
+// warm-up; otherwise the three-kernel LpDc scan, or (sqrt / abs) an LP4 scan with the map
+// as its post-stage and a DC scan.
 class LpDcBlock final : public ScanBlock {
  public:
   LpDcBlock(float fs, float lp_fc, float dc_cut) : ScanBlock("LpDcCascade", Dt::F32, 1) {
@@ -334,18 +336,21 @@ class LpDcBlock final : public ScanBlock {
     c.r = d_.r;
     sp_ = std::make_unique<ScanStage>(RecK::LPDC, Pre::RealLp, Post::Id, lpdc_ss(d_), c, 1);
     sq_ = std::make_unique<ScanStage>(RecK::LPDC, Pre::RealLpSqrt, Post::Id, lpdc_ss(d_), c, 1);
+    ab_ = std::make_unique<ScanStage>(RecK::LPDC, Pre::RealLpAbs, Post::Id, lpdc_ss(d_), c, 1);
     full_ = std::make_unique<ScanStage>(RecK::LPDC, Pre::Real, Post::Id, lpdc_ss(d_), c, 1);
     lp_ = std::make_unique<ScanStage>(RecK::LP4, Pre::Real, Post::Sqrt, lp_cascade_ss(d_.bq), c, 1);
+    lpa_ = std::make_unique<ScanStage>(RecK::LP4, Pre::Real, Post::Abs, lp_cascade_ss(d_.bq), c, 1);
     dc_ = std::make_unique<ScanStage>(RecK::DC, Pre::Real, Post::Id, dc_ss(d_.r), c, 1);
     reset_state();
   }
-  // process_mapped with f32::sqrt (iir.rs:170-186) from now on: before the first call.
-  void set_sqrt(bool on) { sqrt_ = on; }
+  // process_mapped with map (kMapIdentity / kMapSqrt / kMapAbs, iir.rs:170-186) from now
+  // on: before the first call. Identity is process itself (:151-165 == :170-186 with |v| v).
+  void set_map(int map) { map_ = map; }
   int configure(int option, long long value) override {
     if (option != kOptScanPath) return -4;
     if (value != 0 && value != 1) return -3;
     three_ = value == 1;
-    for (auto* st : {lp_.get(), dc_.get(), full_.get()}) st->set_mode(static_cast<int>(value));
+    for (auto* st : {lp_.get(), lpa_.get(), dc_.get(), full_.get()}) st->set_mode(static_cast<int>(value));
     return 0;
   }
   std::vector<float> taps(int) const override { return {d_.bq.b0, d_.bq.b1, d_.bq.b2, d_.bq.a1, d_.bq.a2, d_.r}; }
@@ -354,27 +359,30 @@ class LpDcBlock final : public ScanBlock {
   void run(const void* in, size_t stride, size_t n, void* out, size_t out_stride, hipStream_t s) override {
     const long long st = static_cast<long long>(stride), nn = static_cast<long long>(n),
                     os = static_cast<long long>(out_stride), k0 = static_cast<long long>(k0_);
-    if (!sqrt_) {
+    if (map_ == kMapIdentity) {
       if (sp_->lpdc_single_pass() && !three_) sp_->run(in, st, nn, out, os, k0, dev_err(), s);
       else full_->run(in, st, nn, out, os, k0, dev_err(), s);
       return;
     }
-    if (sq_->lpdc_single_pass() && !three_) {
-      sq_->run(in, st, nn, out, os, k0, dev_err(), s);
+    ScanStage* one = map_ == kMapSqrt ? sq_.get() : ab_.get();
+    if (one->lpdc_single_pass() && !three_) {
+      one->run(in, st, nn, out, os, k0, dev_err(), s);
       return;
     }
     tmp_.resize(n * sizeof(float) + 16);
-    lp_->run(in, st, nn, tmp_.as<void>(), nn, k0, dev_err(), s);
+    (map_ == kMapSqrt ? lp_ : lpa_)->run(in, st, nn, tmp_.as<void>(), nn, k0, dev_err(), s);
     dc_->run(tmp_.as<void>(), nn, nn, out, os, k0, dev_err(), s);
   }
   void reset_state() override {
-    for (auto* st : {sp_.get(), sq_.get(), full_.get(), lp_.get(), dc_.get()}) st->set_carry(carry_zero());
+    for (auto* st : {sp_.get(), sq_.get(), ab_.get(), full_.get(), lp_.get(), lpa_.get(), dc_.get()})
+      st->set_carry(carry_zero());
   }
 
  private:
   LpDcCoeffs d_;
-  bool sqrt_ = false, three_ = false;
-  std::unique_ptr<ScanStage> sp_, sq_, full_, lp_, dc_;
+  int map_ = kMapIdentity;
+  bool three_ = false;
+  std::unique_ptr<ScanStage> sp_, sq_, ab_, full_, lp_, lpa_, dc_;
   DevBuf tmp_;
 };
 
@@ -488,10 +496,11 @@ std::unique_ptr<Block> make_lp_dc_cascade(float fs, float lp_fc, float dc_cut_hz
   return std::make_unique<LpDcBlock>(fs, lp_fc, dc_cut_hz);
 }
 
-int lp_dc_cascade_set_sqrt(Block* b, bool on) {
+int lp_dc_cascade_set_map(Block* b, int map) {
   auto* l = dynamic_cast<LpDcBlock*>(b);
   if (!l) return -4;
-  l->set_sqrt(on);
+  if (map != kMapIdentity && map != kMapSqrt && map != kMapAbs) return -3;
+  l->set_map(map);
   return 0;
 }
 

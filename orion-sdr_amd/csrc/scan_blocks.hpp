@@ -9,7 +9,10 @@ namespace orion {
 std::unique_ptr<Block> make_lp_cascade(float fs, float fc);                  // dsp/iir.rs:49-83
 std::unique_ptr<Block> make_biquad(float b0, float b1, float b2, float a1, float a2);  // dsp/iir.rs:15-41
 std::unique_ptr<Block> make_lp_dc_cascade(float fs, float lp_fc, float dc_cut_hz);     // dsp/iir.rs:86-187
-int lp_dc_cascade_set_sqrt(Block* b, bool on);  // process_mapped(x, f32::sqrt), iir.rs:170-186; -4 other blocks
+// process_mapped(x, f) (iir.rs:170-186) with f = identity / f32::sqrt / f32::abs
+// (include/orion_sdr_amd.h ORION_MAP_*); -4 other blocks, -3 an unknown map.
+enum : int { kMapIdentity = 0, kMapSqrt = 1, kMapAbs = 2 };
+int lp_dc_cascade_set_map(Block* b, int map);
 // modulate/ssb.rs:9-114 (SsbPhasingMod::new(fs, audio_bw, audio_if, rf, usb)). F32 -> C32.
 std::unique_ptr<Block> make_ssb_mod(float fs, float audio_bw, float audio_if_hz, float rf_hz, bool usb);
 std::unique_ptr<Block> make_dc_blocker(float fs, float cut_hz);              // dsp/dc.rs:8-59

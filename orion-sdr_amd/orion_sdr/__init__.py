@@ -91,6 +91,7 @@ def _load():
         "orion_fir_lowpass_iq_group_delay": (i, [vp, C.POINTER(sz)]),
         "orion_biquad_new": (vp, [f, f, f, f, f]),
         "orion_lp_dc_cascade_new": (vp, [f, f, f]), "orion_lp_dc_cascade_set_sqrt_map": (i, [vp, i]),
+        "orion_lp_dc_cascade_set_map": (i, [vp, i]),
         "orion_pm_direct_phase_mod_new": (vp, [f, f, f]), "orion_pm_direct_phase_mod_set_gain": (i, [vp, f]),
         "orion_pm_direct_phase_mod_set_sensitivity": (i, [vp, f]),
         "orion_cw_keyed_mod_new": (vp, [f, f, f, f]), "orion_cw_keyed_mod_set_gain": (i, [vp, f]),
@@ -368,12 +369,24 @@ class Biquad(_Block):
 
 class LpDcCascade(_Block):
     """dsp/iir.rs:111 LpDcCascade::design(fs, lp_fc, dc_cut_hz); process (:151-165), or
-    with sqrt_map=True process_mapped(x, f32::sqrt) (:170-186)."""
+    process_mapped(x, f) (:170-186) with map "identity" / "sqrt" / "abs"
+    (sqrt_map=True: "sqrt", the AM-PowerSqrt use)."""
 
-    def __init__(self, fs: float, lp_fc: float, dc_cut_hz: float, sqrt_map: bool = False):
+    MAPS = {"identity": 0, "sqrt": 1, "abs": 2}
+
+    def __init__(self, fs: float, lp_fc: float, dc_cut_hz: float, sqrt_map: bool = False, map: str | None = None):
         super().__init__(_L.orion_lp_dc_cascade_new(fs, lp_fc, dc_cut_hz))
         if sqrt_map:
             _check(_L.orion_lp_dc_cascade_set_sqrt_map(self._h, 1))
+        if map is not None:
+            self.set_map(map)
+
+    def set_map(self, map: str):
+        """process_mapped's f from the next call on (before the first call)."""
+        if map not in self.MAPS:
+            raise ValueError(f"LpDcCascade map must be one of {sorted(self.MAPS)}, got {map!r}")
+        _check(_L.orion_lp_dc_cascade_set_map(self._h, self.MAPS[map]))
+        return self
 
 
 class FirDecimator(_Block):
