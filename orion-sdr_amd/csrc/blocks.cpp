@@ -1074,15 +1074,21 @@ class WbfmBlock final : public Block {
     (void)std::frexp(amax, &e);  // amax < 2^e
     const int st2 = amax > 0.0f ? std::max(-100, std::min(100, 15 - e)) : 0;
     cs_.tscale = std::ldexp(1.0f, -st2);
+    // r[u] = a[127 - u] 2^st for u in [0, 128), 0 elsewhere; A[I][kap] = a[I + 128 - kap]
+    // = r[kap - I - 1] (kernels.hpp kAudTapWords)
+    auto r = [&](int u, int part) -> _Float16 {
+      const int k = 127 - u;
+      const float v = (u >= 0 && u < 128 && k < static_cast<int>(a.size())) ? std::ldexp(a[k], st2) : 0.0f;
+      const _Float16 h = static_cast<_Float16>(v);
+      return part == 0 ? h : static_cast<_Float16>(v - static_cast<float>(h));
+    };
     std::vector<_Float16> fr(kAudFragBytes / 2);
-    for (int s = 0; s < 5; ++s)
-      for (int l = 0; l < 64; ++l)
-        for (int j = 0; j < 8; ++j) {
-          const int I = l & 15, kap = 32 * s + 8 * (l >> 4) + j, k = I + 128 - kap;
-          const float v = (k >= 0 && k < static_cast<int>(a.size())) ? std::ldexp(a[k], st2) : 0.0f;
-          const _Float16 h = static_cast<_Float16>(v);
-          fr[((2 * s) * 64 + l) * 8 + j] = h;
-          fr[((2 * s + 1) * 64 + l) * 8 + j] = static_cast<_Float16>(v - static_cast<float>(h));
+    for (int part = 0; part < 2; ++part)
+      for (int p = 0; p < 2; ++p)
+        for (int w = 0; w < kAudTapWords; ++w) {
+          _Float16* d = fr.data() + ((part * 2 + p) * kAudTapWords + w) * 2;
+          d[0] = r(2 * w - 16 - p, part);
+          d[1] = r(2 * w - 15 - p, part);
         }
     afrag_.upload(fr.data(), kAudFragBytes);
   }

@@ -1080,26 +1080,18 @@ __device__ __forceinline__ void publish_end(const WbfmArgs& a, int r, const doub
 }
 
 __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc, int ch, long long A0, int Lr,
-                                     bool chan_last, const float* Phi, void* Pv, int l, double (&sw)[4],
-                                     float (&hist)[2], int publish_r = -1, int trace_r = -1) {
+                                     bool chan_last, const float* Phi, void* Pv, const uint32_t* __restrict__ Aw,
+                                     int l, double (&sw)[4], float (&hist)[2], int publish_r = -1,
+                                     int trace_r = -1) {
   const Biquad2 bq{splat2(Bc.b0), splat2(Bc.b1), splat2(Bc.b2), splat2(Bc.a1), splat2(Bc.a2)};
   _Float16* __restrict__ Fh = static_cast<_Float16*>(Pv);
   _Float16* __restrict__ Fl = Fh + kFpN;
   float* __restrict__ Tx = reinterpret_cast<float*>(static_cast<unsigned char*>(Pv) + kTxOff);
-  h8 afr[2];  // the audio FIR's A fragments of one K-step (hi, lo)
   f2 xs[CH];
   {  // lane l: samples 16l .. 16l+15 (iir16); f replaces x in xs (zeros past Lr)
     f2 ef[4];
     double send[4];
     iir16(Bc, Phi, l, sw, xs, ef, send);
-    // the audio FIR's first A fragments (L2-resident), requested now: their latency hides
-    // behind the recurrence and the plane writes; later steps' one step ahead (loaded at
-    // their own step they cost ~5 L2 round trips per back)
-    {
-      const h8* __restrict__ af = static_cast<const h8*>(a.afrag);
-      afr[0] = af[l];
-      afr[1] = af[64 + l];
-    }
     if (trace_r >= 0) fu::trace(a, trace_r, 10);
     const int jl = Lr - 1;
     float cap[4] = {0, 0, 0, 0};
@@ -1197,16 +1189,23 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
     f4v acc[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) acc[g] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-    // per K-step: the eight plane reads issued together, then the four groups' MFMAs
-    // interleaved (independent accumulators back to back)
-    const h8* __restrict__ af = static_cast<const h8*>(a.afrag);
+    // per K-step: the A fragments (8 consecutive reversed taps r[kap0 - I - 1 ..], four
+    // aligned words of the parity copy, LDS) and the eight plane reads issued together,
+    // then the four groups' MFMAs interleaved (independent accumulators back to back).
+    // (The fragments from global memory, L2-resident, cost ~0.5 us per step under the
+    // fronts' HBM load: the trace's FIR phase, round 6.)
+    const int I = l & 15;
 #pragma unroll 1
     for (int st = 0; st < 5; ++st) {
-      const h8 ah = afr[0], al = afr[1];
-      {  // the next step's fragments, one step ahead (step 5 reads step 0's again: unused)
-        const int sn = st < 4 ? st + 1 : 0;
-        afr[0] = af[(2 * sn) * 64 + l];
-        afr[1] = af[(2 * sn + 1) * 64 + l];
+      h8 ah, al;
+      {
+        const int o = 32 * st + 8 * kg - I - 1, p = o & 1;
+        const uint32_t* wh = Aw + p * kAudTapWords + ((o + 16 + p) >> 1);
+        const uint32_t* wl = wh + 2 * kAudTapWords;
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const u4 vh = u4{wh[0], wh[1], wh[2], wh[3]}, vl = u4{wl[0], wl[1], wl[2], wl[3]};
+        ah = __builtin_bit_cast(h8, vh);
+        al = __builtin_bit_cast(h8, vl);
       }
       h8 bh[4], bl[4];
 #pragma unroll
@@ -1222,7 +1221,9 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
 #pragma unroll
       for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[g], acc[g], 0, 0, 0);
       asm volatile("" ::: "memory");  // the next step's plane reads stay behind these MFMAs (registers)
+      if (trace_r >= 0 && st == 0) fu::trace(a, trace_r, 13);  // debug: step 0's operands arrived, MFMAs issued
     }
+    if (trace_r >= 0) fu::trace(a, trace_r, 14);  // debug: every MFMA issued
     // lane (J, kg) holds outputs 256 g + 16 J + 4 kg + r, r < 4
     float* __restrict__ y = a.y + ch * a.y_stride + A0;
     const float ys = __builtin_amdgcn_ldexpf(Bc.tscale, -sf);  // 2^-(sf + st)
@@ -1242,7 +1243,7 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
     }
   }
   lds_order();
-  if (trace_r >= 0) fu::trace(a, trace_r, 12);  // debug: audio FIR done
+  if (trace_r >= 0) fu::trace(a, trace_r, 12);  // debug: audio FIR done (stores issued)
 }
 
 }  // namespace sg
@@ -1255,11 +1256,17 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
   __shared__ __attribute__((aligned(16))) f2 U[g8::LDS_F2];
   __shared__ __attribute__((aligned(16))) unsigned char wreg[sg::WBytes];
   __shared__ __attribute__((aligned(16))) float Gt[128];
+  __shared__ __attribute__((aligned(16))) uint32_t Aw[kAudFragBytes / 4];  // audio FIR taps (sg::back)
   float* Phi = reinterpret_cast<float*>(wreg);
   f2* P = reinterpret_cast<f2*>(wreg);
   const int l = threadIdx.x & 63;
   Gt[l] = C.g[l];
   Gt[l + 64] = C.g[l + 64];
+  {
+    const uint32_t* __restrict__ aw = static_cast<const uint32_t*>(a.afrag);
+#pragma unroll
+    for (int i = 0; i < kAudFragBytes / 4 / 64; ++i) Aw[l + 64 * i] = aw[l + 64 * i];
+  }
   FuRange g;
   // Segment r = blockIdx.x: a segment's predecessor (whose end state it waits for) has
   // the smaller blockIdx, so it was dispatched first whatever else holds the CUs (an
@@ -1358,7 +1365,7 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
     } else {
       const bool lastsub = sub == nsub - 1;
       if (sub <= 3) fu::trace(a, g.r, 3 + sub);
-      sg::back(a, Bc, g.ch, A0, Lr, g.last && lastsub, Phi, P, l, sw, hist, lastsub && !g.last ? g.r : -1,
+      sg::back(a, Bc, g.ch, A0, Lr, g.last && lastsub, Phi, P, Aw, l, sw, hist, lastsub && !g.last ? g.r : -1,
                sub == 1 ? g.r : -1);
       if (sub <= 3) fu::trace(a, g.r, 6 + sub);
     }
@@ -1389,7 +1396,7 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
   }
   lds_order();
   fu::trace(a, g.r, 2);
-  sg::back(a, Bc, g.ch, g.A, min(sg::L, g.Lr), g.last && nsub == 1, Phi, P, l, sw, hist);
+  sg::back(a, Bc, g.ch, g.A, min(sg::L, g.Lr), g.last && nsub == 1, Phi, P, Aw, l, sw, hist);
   fu::trace(a, g.r, 3);
 }
 

@@ -139,9 +139,14 @@ struct WbfmArgs {
   uint32_t spin;                                    // polls before a wait times out (kernels.hpp kSpinDefault)
   uint32_t epoch;                                   // this launch's tag (never 0)
   long long* trace;                                 // debug: per-wave phase timestamps (or null)
-  const void* afrag;                                // audio FIR A fragments (k_wbfm.hip sg::back)
+  const void* afrag;                                // audio FIR reversed f16 tap words (k_wbfm.hip sg::back)
 };
-constexpr int kAudFragBytes = 5 * 2 * 64 * 16;     // 5 K-steps x (hi, lo) x 64 lanes x 8 halves
+// The audio FIR's taps as the A operand source: r[m] = a[127 - m] 2^st (zero outside
+// [0, 128)) as f16 hi and lo parts, each in two parity copies of 96 words (copy p, word w:
+// halves r[2w - 16 - p], r[2w - 15 - p]), so that any 8 consecutive halves are 4 aligned
+// words of one copy (k_wbfm.hip sg::back keeps them in LDS).
+constexpr int kAudTapWords = 96;
+constexpr int kAudFragBytes = 2 * 2 * kAudTapWords * 4;  // (hi, lo) x 2 parity copies
 constexpr int kFuTracePoints = 16;
 void launch_wbfm(const WbfmArgs& a, const WbfmFrontConst& f, const WbfmBackConst& b, int nch,
                  hipStream_t s);

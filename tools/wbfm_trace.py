@@ -39,6 +39,9 @@ def main():
         ("sub-range 1: IIR (iir16)", t[:, 10] - t[:, 4]),
         ("sub-range 1: f32 recurrence + f16 planes", t[:, 11] - t[:, 10]),
         ("sub-range 1: audio FIR (MFMA) + stores", t[:, 12] - t[:, 11]),
+        ("  FIR: to step 0's MFMAs issued (frags, planes)", t[:, 13] - t[:, 11]),
+        ("  FIR: steps 1-4 issued", t[:, 14] - t[:, 13]),
+        ("  FIR: results, scale, stores issued", t[:, 12] - t[:, 14]),
         ("sub-range 1: whole back", t[:, 7] - t[:, 4]),
         ("sub-range 2: 8 front tiles", t[:, 5] - t[:, 7]),
         ("sub-range 3: 8 front tiles", t[:, 6] - t[:, 8]),
