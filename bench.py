@@ -21,10 +21,16 @@ At N = 1 the C2 line also carries "host_fed" (SURVEY §8d's H2D-inclusive figure
 same chain driven from host memory through orion_block_process, pinned and pageable,
 beside the box's raw pinned H2D rate. It is never `value`.
 
-Other workloads (--config c1|c3|c4|c5) are available for DESIGN.md tables; the
+Other workloads (--config c1|c3|c4|c5|c5f) are available for DESIGN.md tables; the
 driver's default line is c2. C1 (BASELINE configs[0], the reference's CPU block
 graph: 127-tap FirLowpassIq over 2^20 cf32) is compute-bound (508 flop per 16 B),
-so its roofline is priced against packed FP32 (157.3 TFLOP/s), not HBM.
+so its roofline is priced against packed FP32 (157.3 TFLOP/s), not HBM. C5F is
+BASELINE configs[4] with its channel filter: a batched 127-tap FirLowpassIq in front
+of the batched SsbProductDemod (a two-block device graph), priced on the FIR (FP32).
+
+Multi-process rehearsal on one GPU: --dist-backend gloo and
+--device-map 0,0 let two ranks share device 0; --check-shards (C2 stream shards)
+gathers every rank's audio to rank 0 and compares it with one call over the stream.
 """
 import argparse
 import json
@@ -48,9 +54,16 @@ METRICS = {  # the non-default configs name what they measure
     "c1": "Msamples/s through 127-tap FirLowpassIq (1 channel, 2^20 cf32 per pass) per MI355X",
     "c3": "Msamples/s through batched 255-tap decimating FIR (256 channels, M=8) per MI355X",
     "c5": "Msamples/s through SSB product demod (128 channels @ 48 ksps) per MI355X",
+    "c5f": "Msamples/s through 127-tap channel FIR + SSB product demod (128 channels @ 48 ksps) per MI355X",
 }
-KERNELS = {"c1": "k_fir_iq8", "c2": "k_wbfm_seg", "c3": "k_decim_w4q", "c4": "k_wbfm_seg", "c5": "k_lpdc_sp"}
-CHANNELS_PER_GPU = {"c3": 256, "c4": 8, "c5": 128}
+KERNELS = {"c1": "k_fir_iq8", "c2": "k_wbfm_seg", "c3": "k_decim_w4q", "c4": "k_wbfm_seg", "c5": "k_lpdc_sp",
+           "c5f": "k_fir_iq8"}
+CHANNELS_PER_GPU = {"c3": 256, "c4": 8, "c5": 128, "c5f": 128}
+C3_DESIGN = (10e6, 8, 200e3, 39370.0)  # FirDecimator(10e6, 8, 200e3, 39370) = 255 taps
+C5F_FIR = (127, 3000.0 / 48e3, 60.0)  # FirLowpassIq::design: +-3 kHz around the SSB channel, 60 dB
+NOISE = ("complex AWGN from splitmix64(seed, sample index) + Box-Muller: every sample a function of its "
+         "index, so a time shard with its halo is the stream's slice (the reference's add_awgn "
+         "sequence, seed 0x1234_5678_ABCD_EF00, cannot be cut that way)")
 
 
 _M64 = (1 << 64) - 1
@@ -120,22 +133,35 @@ def channel_plan(cfg, rank, world):
         nch = CHANNELS_PER_GPU["c4"]
         return [(OFFSETS[(rank * nch + c) % len(OFFSETS)] * (1 + 0.01 * c), 0x1234 + rank * nch + c)
                 for c in range(nch)]
-    if cfg in ("c3", "c5"):
+    if cfg in ("c3", "c5", "c5f"):
         nch = CHANNELS_PER_GPU[cfg]
         base = 77 if cfg == "c3" else 99
         return [(rank * nch + c, (base << 20) ^ (rank * nch + c)) for c in range(nch)]
     raise ValueError(cfg)
 
 
+_SSB_TONE = {}
+
+
+def ssb_tone(n, dev):
+    """SsbPhasingMod(48e3, 2800, 1500, 0, usb) of a 1.2 kHz tone (0.5
+    peak), on the device (the engine's own modulator, the reference's recurrences)."""
+    key = (n, str(dev))
+    if key not in _SSB_TONE:
+        a = (0.5 * torch.sin(2 * np.pi * 1200.0 * torch.arange(n, device=dev, dtype=torch.float64) / 48e3)).float()
+        _SSB_TONE[key] = orion_sdr.SsbPhasingMod(48e3, 2800.0, 1500.0).process_device(a.contiguous()).clone()
+    return _SSB_TONE[key]
+
+
 def channel_input(cfg, n, seed, dev):
-    """One C3 / C5 channel's synthetic input (complex64, on `dev`), from its seed."""
+    """One C3 / C5 channel's synthetic input (complex64, on `dev`), from its seed: C3
+    unit-power complex noise; C5 the SSB tone plus AWGN (P = 1e-3) of its own seed."""
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
     if cfg == "c3":
         return torch.randn(n, dtype=torch.complex64, device=dev, generator=g)
-    t = torch.arange(n, device=dev, dtype=torch.float64) / 48e3  # C5: USB voice-band tone + noise
-    base = torch.polar(torch.ones_like(t), 2 * np.pi * 2700.0 * t).to(torch.complex64) * 0.4
-    return (base + 0.03 * torch.randn(n, dtype=torch.complex64, device=dev, generator=g)).contiguous()
+    w = torch.randn(n, dtype=torch.complex64, device=dev, generator=g)
+    return (ssb_tone(n, dev) + np.float32(np.sqrt(1e-3)) * w).contiguous()
 
 
 def c1_input(n, dev, seed=0x1234_5678):
@@ -148,12 +174,49 @@ def c1_input(n, dev, seed=0x1234_5678):
 
 
 def max_over_ranks(elapsed, dist, device):
-    """Whole-job time: the slowest rank's (the driver's contract)."""
+    """Whole-job time: the slowest rank's (the driver's contract). The gloo backend
+    reduces host tensors, nccl (RCCL) device tensors."""
     if dist is None:
         return elapsed
-    tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dv = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=dv)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     return float(tt.item())
+
+
+def check_shards(x, desc, dist, world, rank, dev):
+    """--check-shards (C2 stream shards): each rank runs a FRESH chain, sought to its halo
+    start, over its input (the timed handle has run the same samples many times), and
+    its audio for [start, stop) is gathered to rank 0 (host tensors over the process
+    group), concatenated in rank order and compared with ONE call of a fresh chain over
+    the whole stream (generated by the same index-addressed function). Returns the
+    comparison on rank 0, None elsewhere."""
+    sh = desc["shard"]
+    m = 8
+    y = orion_sdr.WbfmChain(f_off=OFFSETS[0]).seek(sh["halo_start"]).process_device(x)
+    mine = y[(sh["start"] - sh["halo_start"]) // m:].float().cpu()
+    parts = [torch.empty(0)] * world
+    if dist is not None:
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([mine.numel()], dtype=torch.int64))
+        mx = int(max(s.item() for s in sizes))
+        buf = torch.zeros(mx)
+        buf[: mine.numel()] = mine
+        got = [torch.zeros(mx) for _ in range(world)]
+        dist.all_gather(got, buf)
+        parts = [g[: int(s.item())] for g, s in zip(got, sizes)]
+    else:
+        parts = [mine]
+    if rank != 0:
+        return None
+    cat = torch.cat(parts).numpy()
+    n_all = desc["stream_samples"]
+    full = orion_sdr.WbfmChain(f_off=OFFSETS[0]).process_device(
+        wbfm_iq(n_all, OFFSETS[0], dev, 0x1234)).cpu().numpy()
+    err = float(np.sqrt(np.mean((cat.astype(np.float64) - full) ** 2)) / np.sqrt(np.mean(full.astype(np.float64) ** 2)))
+    return {"ranks": world, "stream_samples": n_all, "audio_samples": int(cat.size),
+            "one_call_samples": int(full.size), "nrmse_vs_one_call": err,
+            "ok": bool(cat.size == full.size and err <= 1e-5)}
 
 
 def make_workload(cfg, rank, dev, n_override=None, world=1, shard="stream"):
@@ -169,7 +232,8 @@ def make_workload(cfg, rank, dev, n_override=None, world=1, shard="stream"):
         desc = dict(workload="C2 WBFM chain on ONE stream cut in time: Rotator(-f_off) -> FirDecimator(10e6, 8, "
                     "200e3, 79e3; 127 taps) -> FmQuadratureDemod(1.25e6, 75e3, 15e3) -> FirLowpass(1.25e6, 15e3, "
                     "10e3; 125 taps)", fs_hz=10e6, stream_samples=world * n, samples_per_step_per_gpu=stop - start,
-                    halo_samples=start - h, channels_per_gpu=1)
+                    halo_samples=start - h, channels_per_gpu=1, noise=NOISE,
+                    shard=dict(start=start, stop=stop, halo_start=h))
         return blk, x, stop - start, 8.5, desc
     if cfg == "c2":
         n = n_override or (1 << 26)
@@ -178,7 +242,7 @@ def make_workload(cfg, rank, dev, n_override=None, world=1, shard="stream"):
         x = wbfm_iq(n, f_off, dev, seed)
         desc = dict(workload="C2 WBFM chain: Rotator(-f_off) -> FirDecimator(10e6, 8, 200e3, 79e3; 127 taps) -> "
                     "FmQuadratureDemod(1.25e6, 75e3, 15e3) -> FirLowpass(1.25e6, 15e3, 10e3; 125 taps)",
-                    fs_hz=10e6, samples_per_step_per_gpu=n, channels_per_gpu=1)
+                    fs_hz=10e6, samples_per_step_per_gpu=n, channels_per_gpu=1, noise=NOISE)
         return blk, x, n, 8.5, desc
     if cfg == "c4":
         plan = channel_plan(cfg, rank, world)
@@ -186,7 +250,7 @@ def make_workload(cfg, rank, dev, n_override=None, world=1, shard="stream"):
         blk = orion_sdr.WbfmChain(f_off=[f for f, _ in plan])
         x = torch.stack([wbfm_iq(n, f, dev, seed) for f, seed in plan]).contiguous()
         desc = dict(workload="C4 WBFM chain, 8 independent channels per GPU", samples_per_step_per_gpu=nch * n,
-                    channels_per_gpu=nch)
+                    channels_per_gpu=nch, noise=NOISE)
         return blk, x, nch * n, 8.5, desc
     if cfg == "c1":
         n = n_override or (1 << 20)
@@ -199,20 +263,56 @@ def make_workload(cfg, rank, dev, n_override=None, world=1, shard="stream"):
     if cfg == "c3":
         plan = channel_plan(cfg, rank, world)
         nch, n = len(plan), n_override or (1 << 20)
-        blk = orion_sdr.FirDecimator(10e6, 8, 190e3, 39370.0, channels=nch)
+        blk = orion_sdr.FirDecimator(*C3_DESIGN, channels=nch)
         x = torch.stack([channel_input(cfg, n, seed, dev) for _, seed in plan]).contiguous()
-        desc = dict(workload="C3 batched FirDecimator, 256 channels x 255 taps, M=8", samples_per_step_per_gpu=nch * n,
-                    channels_per_gpu=nch, channels=[plan[0][0], plan[-1][0] + 1])
+        desc = dict(workload="C3 batched FirDecimator(10e6, 8, 200e3, 39370), 256 channels x 255 taps, M=8",
+                    samples_per_step_per_gpu=nch * n, channels_per_gpu=nch, channels=[plan[0][0], plan[-1][0] + 1],
+                    input="unit-power complex Gaussian noise per channel (torch generator, seed per channel)")
         return blk, x, nch * n, 9.0, desc
     if cfg == "c5":
         plan = channel_plan(cfg, rank, world)
         nch, n = len(plan), n_override or (1 << 20)
         blk = orion_sdr.SsbProductDemod(48e3, 1500.0, 2800.0, channels=nch)
         x = torch.stack([channel_input(cfg, n, seed, dev) for _, seed in plan]).contiguous()
-        desc = dict(workload="C5 SsbProductDemod, 128 channels per GPU @ 48 ksps (1024 on 8 GPUs)",
-                    samples_per_step_per_gpu=nch * n, channels_per_gpu=nch, channels=[plan[0][0], plan[-1][0] + 1])
+        desc = dict(workload="C5 SsbProductDemod(48e3, 1500, 2800), 128 channels per GPU @ 48 ksps (1024 on 8 GPUs)",
+                    samples_per_step_per_gpu=nch * n, channels_per_gpu=nch, channels=[plan[0][0], plan[-1][0] + 1],
+                    input="SsbPhasingMod(48e3, 2800, 1500, 0, usb) of a 1.2 kHz tone (on the device) + AWGN P=1e-3 "
+                          "per channel")
         return blk, x, nch * n, 12.0, desc
+    if cfg == "c5f":
+        plan = channel_plan(cfg, rank, world)
+        nch, n = len(plan), n_override or (1 << 20)
+        blk = SsbChannelGraph(nch, dev)
+        x = torch.stack([channel_input(cfg, n, seed, dev) for _, seed in plan]).contiguous()
+        desc = dict(workload="C5 with its channel filter: FirLowpassIq::design(127, 3000/48000, 60 dB) -> "
+                    "SsbProductDemod(48e3, 1500, 2800), 128 channels per GPU @ 48 ksps, a two-block device graph "
+                    "(the filtered IQ through HBM)", samples_per_step_per_gpu=nch * n, channels_per_gpu=nch,
+                    channels=[plan[0][0], plan[-1][0] + 1], flop_per_sample=4 * C5F_FIR[0],
+                    input="SsbPhasingMod(48e3, 2800, 1500, 0, usb) of a 1.2 kHz tone (on the device) + AWGN P=1e-3 "
+                          "per channel")
+        return blk, x, nch * n, 28.0, desc
     raise SystemExit(f"unknown --config {cfg}")
+
+
+class SsbChannelGraph:
+    """C5F: the batched channel filter then the batched SSB demodulator on the device,
+    the filtered IQ in an HBM buffer between them (two launches per step). The same
+    process_device / out_len surface as a block, for the bench loop."""
+
+    def __init__(self, nch, dev):
+        self.fir = orion_sdr.FirLowpassIq.design(*C5F_FIR, channels=nch)
+        self.ssb = orion_sdr.SsbProductDemod(48e3, 1500.0, 2800.0, channels=nch)
+        self.mid = None
+        self.dev = dev
+
+    def out_len(self, n):
+        return n
+
+    def process_device(self, x, out=None, stream=None):
+        if self.mid is None or self.mid.shape != x.shape:
+            self.mid = torch.empty_like(x)
+        self.fir.process_device(x, self.mid, stream)
+        return self.ssb.process_device(self.mid, out, stream)
 
 
 def cpu_baseline_channels(x_dev, cfg, seconds_target, f_offs=None):
@@ -227,7 +327,14 @@ def cpu_baseline_channels(x_dev, cfg, seconds_target, f_offs=None):
     nch, n_all = x_dev.shape
     thr = max(1, min(nch, 16, os.cpu_count() or 1))
     if cfg == "c3":
-        run, what = (lambda xh: O.decim_channels(xh, 10e6, 8, 190e3, 39370.0, thr)), "o_run_decim_channels"
+        run, what = (lambda xh: O.decim_channels(xh, *C3_DESIGN, thr)), "o_run_decim_channels"
+    elif cfg == "c5f":
+        taps = O.kaiser_lowpass_taps(*C5F_FIR)
+
+        def run(xh):
+            f = np.stack([O.fir_lowpass_iq(xh[c], taps) for c in range(xh.shape[0])])
+            return O.ssb_demod_channels(f, 48e3, 1500.0, 2800.0, thr)
+        what = "o_fir_lowpass_iq (1 thread) + o_run_ssb_demod_channels"
     elif cfg == "c4":
         run, what = (lambda xh: O.wbfm_channels(xh, np.asarray(f_offs, np.float32), thr)), "o_run_wbfm_channels"
     else:
@@ -342,7 +449,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c5f"])
     ap.add_argument("--n", type=int, default=0, help="override samples per channel")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-max-samples", type=int, default=1 << 24)
@@ -351,6 +458,13 @@ def main():
     ap.add_argument("--rest", type=float, default=0.0, help="idle seconds between input synthesis and the warm-up")
     ap.add_argument("--shard", default="stream", choices=["stream", "channels"],
                     help="C2 on several GPUs: one stream cut in time (with a halo), or a channel per GPU")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for the timing barrier / max (nccl = RCCL; gloo: host tensors, "
+                         "several ranks may share a device)")
+    ap.add_argument("--device-map", default="",
+                    help="comma list: the device of each local rank (default: local rank i on device i)")
+    ap.add_argument("--check-shards", action="store_true",
+                    help="C2 stream shards: gather the ranks' audio and compare with one call over the stream")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -359,21 +473,32 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N > 1 as "
                          f"python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dmap = [int(v) for v in args.device_map.split(",")] if args.device_map else None
+    if dmap is not None and len(dmap) <= local:
+        raise SystemExit(f"bench.py: --device-map {args.device_map} has no entry for local rank {local}")
+    gpu = dmap[local] if dmap is not None else local
+    if args.dist_backend == "nccl" and dmap is not None and len(set(dmap)) != len(dmap):
+        raise SystemExit("bench.py: ranks sharing a device need --dist-backend gloo (RCCL wants one rank per GPU)")
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     stream = torch.cuda.current_stream(dev)
 
     blk, x, samples, bps, desc = make_workload(args.config, rank, dev, args.n or None, world, args.shard)
     nout = blk.out_len(x.shape[-1])
     out_shape = (nout,) if x.dim() == 1 else (x.shape[0], nout)
     out_dtype = torch.complex64 if args.config in ("c1", "c3") else torch.float32
+    if args.check_shards and "shard" not in desc:
+        raise SystemExit("bench.py: --check-shards needs --config c2 on several ranks with --shard stream")
     out = torch.empty(out_shape, dtype=out_dtype, device=dev)
     torch.cuda.synchronize(dev)
     if args.rest > 0:
@@ -413,13 +538,37 @@ def main():
            if args.config in ("c2", "c4") else {}),
         "config": dict(desc, parallelism=(f"stream time-sharded x{world} (halo {orion_sdr.STREAM_HALO} samples), no "
                                           "data-path collective" if "halo_samples" in desc
-                                          else f"channel-sharded x{world}, no data-path collective")),
+                                          else f"channel-sharded x{world}, no data-path collective"),
+                       **({"dist_backend": args.dist_backend} if world > 1 else {}),
+                       **({"device_map": args.device_map} if dmap is not None else {})),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": KERNELS[args.config],
                      "kernel_ms": round(kern_ms, 4), "bytes_per_sample": bps},
         "cpu_baseline": None,
     }
-    if args.config == "c1":  # compute-bound: packed FP32 is the roof (31.75 flop/B > the ~19.7 flop/B ridge)
+    if args.config == "c5f":
+        # the dominant kernel alone (the 127-tap FIR, FP32-bound: 508 flop per sample), one
+        # event pair around each FIR launch after the timed region; the SSB scan beside it
+        mid = torch.empty_like(x)
+        fe, se = [], []
+        for _ in range(max(args.steps, 10)):
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record(stream)
+            blk.fir.process_device(x, mid, stream.cuda_stream)
+            e1.record(stream)
+            blk.ssb.process_device(mid, out, stream.cuda_stream)
+            e2.record(stream)
+            fe.append((e0, e1))
+            se.append((e1, e2))
+        torch.cuda.synchronize(dev)
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in fe]))
+        ssb_ms = float(np.mean([a.elapsed_time(b) for a, b in se]))
+        line["roofline"]["kernel_ms"] = round(kern_ms, 4)
+        line["roofline"]["second_kernel"] = {"kernel": "k_lpdc_sp", "kernel_ms": round(ssb_ms, 4),
+                                             "hbm_gbs": round(samples * 12.0 / (ssb_ms * 1e-3) / 1e9, 1)}
+        del mid
+    if args.config in ("c1", "c5f"):  # compute-bound: packed FP32 is the roof (31.75 flop/B > the ~19.7 flop/B ridge)
+        achieved = samples * 16.0 / (kern_ms * 1e-3) / 1e9  # the FIR's own bytes: 8 B in + 8 B out
         tflops = samples * desc["flop_per_sample"] / (kern_ms * 1e-3) / 1e12
         line["roofline"].update(bound="fp32", achieved=round(tflops, 2), peak=FP32_PEAK_TFLOPS, unit="TFLOP/s",
                                 frac=round(tflops / FP32_PEAK_TFLOPS, 4), hbm_gbs=round(achieved, 1),
@@ -455,11 +604,17 @@ def main():
     except Exception as e:  # noqa: BLE001  (the bench line must still print)
         line["roofline"]["peak_measured"] = None
         line["roofline"]["probe_error"] = str(e)[:120]
+    # PMC traffic is collected in separate rocprofv3 --pmc passes (tools/traffic.py), never
+    # inside this run: the figure is the committed file's, and the line names it
     traffic_file = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(traffic_file):
         tr = json.load(open(traffic_file))
         if tr.get("samples_per_launch") == samples:
             line["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
+            line["roofline"]["traffic_source"] = f"profiles/traffic_{args.config}.json (rocprofv3 --pmc FETCH_SIZE + " \
+                                                 f"WRITE_SIZE, separate passes; not measured in this run)"
+    if args.check_shards:
+        line["shard_check"] = check_shards(x, desc, dist, world, rank, dev)
     if rank == 0 and world == 1 and args.config == "c2" and not args.no_h2d:
         try:
             line["host_fed"] = host_fed(x)

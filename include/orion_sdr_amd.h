@@ -132,6 +132,10 @@ orion_block* orion_fir_lowpass_new(float fs, float pass_hz, float trans_hz);
 orion_block* orion_fir_lowpass_iq_design(size_t num_taps, float cutoff_norm, float stopband_db);
 /* dsp/fir.rs:193-204 FirLowpassIq::from_taps(taps) (empty -> [1.0]). */
 orion_block* orion_fir_lowpass_iq_from_taps(const float* taps, size_t n);
+/* Batched FirLowpassIq: nch independent channels sharing the taps (a channel filter in
+ * front of a batched demodulator, BASELINE C5), [nch][n] in and out; filter_aligned is
+ * single-channel only (ORION_E_ARG here). */
+orion_block* orion_fir_lowpass_iq_batch_from_taps(const float* taps, size_t n, size_t nch);
 /* dsp/fir.rs:210-212 FirLowpassIq::num_taps, :216-218 group_delay = (num_taps - 1) / 2.
  * ORION_E_TYPE if b is not a FirLowpassIq. */
 int orion_fir_lowpass_iq_num_taps(const orion_block* b, size_t* num_taps);

@@ -731,7 +731,9 @@ class FirRealBlock final : public Block {
 // --------------------------------------------------------- FirLowpassIq ----
 class FirIqBlock final : public Block {
  public:
-  explicit FirIqBlock(std::vector<float> taps) : h_(std::move(taps)) {
+  // nch > 1: independent channels sharing the taps (one stream per channel, [nch][n]).
+  FirIqBlock(std::vector<float> taps, int nch) : h_(std::move(taps)), nch_(nch) {
+    if (nch_ < 1) throw std::invalid_argument("FirLowpassIq needs >= 1 channel");
     if (h_.empty()) h_.push_back(1.0f);  // fir.rs:195-197
     K_ = static_cast<int>(h_.size());
     hist_len_ = padded_hist(K_);
@@ -740,7 +742,7 @@ class FirIqBlock final : public Block {
     fast_ = taps256(gp);
     g_dev_.upload(h_.data(), h_.size() * sizeof(float));
     for (auto& h : hist_) {
-      h.resize(hist_len_ * sizeof(f2));
+      h.resize(static_cast<size_t>(nch_) * hist_len_ * sizeof(f2));
       h.zero();
     }
     zeros_.resize(hist_len_ * sizeof(f2));
@@ -750,13 +752,15 @@ class FirIqBlock final : public Block {
   const char* name() const override { return "FirLowpassIq"; }
   Dt in_type() const override { return Dt::C32; }
   Dt out_type() const override { return Dt::C32; }
+  int channels() const override { return nch_; }
   size_t chunk_quantum() const override { return 4096; }
   WorkReport process_device(const void* in, size_t n_in, void* out, size_t out_cap, hipStream_t s) override {
     const size_t n = std::min(n_in, out_cap);  // fir.rs:288
     if (n == 0) return {0, 0};
     const f2* x = static_cast<const f2*>(in);
     launch_fir_iq(x, static_cast<long long>(n), hist_[cur_].as<f2>(), hist_len_, static_cast<f2*>(out),
-                  static_cast<long long>(n), 0, K_, fast_, g_dev_.as<float>(), s, hist_[cur_ ^ 1].as<f2>());
+                  static_cast<long long>(n), 0, K_, fast_, g_dev_.as<float>(), s, hist_[cur_ ^ 1].as<f2>(), nch_,
+                  static_cast<long long>(n_in), static_cast<long long>(out_cap));
     cur_ ^= 1;
     return {n, n};
   }
@@ -767,6 +771,7 @@ class FirIqBlock final : public Block {
   std::vector<float> taps(int) const override { return h_; }
   // fir.rs:260-276: reset, then y[i] = streamed[i + d] over x padded with zeros.
   void aligned(void* io, size_t n, hipStream_t s) {
+    if (nch_ != 1) throw std::invalid_argument("filter_aligned: single-channel FirLowpassIq only");
     reset();
     if (n == 0) return;
     const long long d = (K_ - 1) / 2;
@@ -799,6 +804,7 @@ class FirIqBlock final : public Block {
   int K_ = 0, hist_len_ = 0;
   Taps256 fast_{};
   DevBuf g_dev_, hist_[2], zeros_, scratch_, tail_, edges_;
+  int nch_ = 1;
   int cur_ = 0;
 };
 
@@ -1217,8 +1223,8 @@ std::unique_ptr<Block> make_fir_decimator(float fs, size_t m, float cutoff, floa
 std::unique_ptr<Block> make_fir_lowpass(float fs, float pass, float trans) {
   return std::make_unique<FirRealBlock>(fs, pass, trans);
 }
-std::unique_ptr<Block> make_fir_lowpass_iq(const std::vector<float>& taps) {
-  return std::make_unique<FirIqBlock>(taps);
+std::unique_ptr<Block> make_fir_lowpass_iq(const std::vector<float>& taps, int nch) {
+  return std::make_unique<FirIqBlock>(taps, nch);
 }
 int fir_lowpass_iq_filter_aligned(Block* b, void* io, size_t n, hipStream_t s) {
   auto* f = dynamic_cast<FirIqBlock*>(b);

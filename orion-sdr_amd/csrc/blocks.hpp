@@ -140,8 +140,9 @@ std::unique_ptr<Block> make_fir_decimator(float fs, size_t m, float cutoff_hz, f
                                           int nch = 1);
 // dsp/fir.rs:7-67. F32 -> F32.
 std::unique_ptr<Block> make_fir_lowpass(float fs, float pass_hz, float trans_hz);
-// dsp/fir.rs:176-297 (from_taps; empty -> [1.0]). C32 -> C32.
-std::unique_ptr<Block> make_fir_lowpass_iq(const std::vector<float>& taps);
+// dsp/fir.rs:176-297 (from_taps; empty -> [1.0]). C32 -> C32. nch > 1: independent
+// channels sharing the taps (batched [nch][n], as the batched FirDecimator).
+std::unique_ptr<Block> make_fir_lowpass_iq(const std::vector<float>& taps, int nch = 1);
 // FirLowpassIq::filter_aligned (fir.rs:260-276) on device memory, in place allowed
 // via a scratch copy. Resets the block's streaming state first, like the reference.
 int fir_lowpass_iq_filter_aligned(Block* b, void* io_dev, size_t n, hipStream_t s);

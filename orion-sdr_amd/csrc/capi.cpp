@@ -244,6 +244,12 @@ orion_block* orion_fir_lowpass_iq_design(size_t num_taps, float cutoff_norm, flo
 orion_block* orion_fir_lowpass_iq_from_taps(const float* taps, size_t n) {
   return make([&] { return orion::make_fir_lowpass_iq(std::vector<float>(taps, taps + (taps ? n : 0))); });
 }
+orion_block* orion_fir_lowpass_iq_batch_from_taps(const float* taps, size_t n, size_t nch) {
+  return make([&] {
+    if (nch < 1 || nch > (1u << 16)) throw std::invalid_argument("FirLowpassIq batch: 1 <= nch <= 65536");
+    return orion::make_fir_lowpass_iq(std::vector<float>(taps, taps + (taps ? n : 0)), static_cast<int>(nch));
+  });
+}
 int orion_osc_table_phasors(float freq_hz, float fs, uint64_t max_out, void* out, size_t n, uint64_t* cyc_start,
                             uint64_t* cyc_len, uint64_t* n_tab) {
   if (!out && n) return fail(ORION_E_NULL, "null buffer");

@@ -628,13 +628,23 @@ __global__ __launch_bounds__(NT) void k_fir_real_generic(const float* __restrict
 // per lane; the tile plus its KP-sample halo is staged once in LDS (padded 2 per 8
 // against bank conflicts) behind one barrier. INPLACE (y == x): the halo comes from
 // boundary copies E taken before the launch, so no tile reads a neighbour's output.
+// Channels (batched FirLowpassIq, independent streams): channel blockIdx.y reads
+// x + ch x_stride, writes y + ch y_stride, and keeps its own history at ch hist_len.
 template <int KP, bool INPLACE = false, int R = 8>
 __global__ __launch_bounds__(NT) void k_fir_iq8(const f2* x, long long n,
                                                 const f2* __restrict__ hist, int hist_len,
                                                 f2* y, long long n_out, long long off,
                                                 const Taps256 g, const f2* __restrict__ E = nullptr,
-                                                f2* __restrict__ hist_out = nullptr) {
-  if constexpr (!INPLACE) hist_next(x, n, hist, hist_out, hist_len);
+                                                f2* __restrict__ hist_out = nullptr, long long x_stride = 0,
+                                                long long y_stride = 0) {
+  if constexpr (!INPLACE) {
+    const int ch = blockIdx.y;
+    x += ch * x_stride;
+    y += ch * y_stride;
+    hist += static_cast<long long>(ch) * hist_len;
+    if (hist_out) hist_out += static_cast<long long>(ch) * hist_len;
+    hist_next(x, n, hist, hist_out, hist_len);
+  }
   static_assert(R == 8 || R == 4, "outputs per lane");
   constexpr int TT = R * NT;
   constexpr int W = TT + KP + 2, PER = (W + NT - 1) / NT;
@@ -860,26 +870,31 @@ void launch_fir_real(const float* x, long long n, const float* hist, int hist_le
 }
 
 void launch_fir_iq(const f2* x, long long n, const f2* hist, int hist_len, f2* y, long long n_out,
-                   long long off, int K, const Taps256& g, const float* g_dev, hipStream_t s, f2* hist_out) {
-  if (n_out <= 0) return;
+                   long long off, int K, const Taps256& g, const float* g_dev, hipStream_t s, f2* hist_out,
+                   int nch, long long x_stride, long long y_stride) {
+  if (n_out <= 0 || nch <= 0) return;
   if (K <= 256 && hist_len >= (K <= 64 ? 64 : K <= 128 ? 128 : 256)) {
     // calls that fill fewer than kFir4TilesPerCu tiles of 8 outputs per lane per CU
     // take four outputs per lane (twice the waves; the FMA work is the same)
-    const bool four = n_out < static_cast<long long>(kFir4TilesPerCu) * device_cus() * 8 * NT;
+    const bool four = n_out * nch < static_cast<long long>(kFir4TilesPerCu) * device_cus() * 8 * NT;
     if (four) {
-      const int g4 = grid_for(n_out, 4 * NT);
-      if (K <= 64) k_fir_iq8<64, false, 4><<<g4, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
-      else if (K <= 128) k_fir_iq8<128, false, 4><<<g4, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
-      else k_fir_iq8<256, false, 4><<<g4, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
+      const dim3 g4(grid_for(n_out, 4 * NT), nch);
+      if (K <= 64) k_fir_iq8<64, false, 4><<<g4, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out, x_stride, y_stride);
+      else if (K <= 128) k_fir_iq8<128, false, 4><<<g4, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out, x_stride, y_stride);
+      else k_fir_iq8<256, false, 4><<<g4, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out, x_stride, y_stride);
     } else {
-      const int g8 = grid_for(n_out, 8 * NT);
-      if (K <= 64) k_fir_iq8<64><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
-      else if (K <= 128) k_fir_iq8<128><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
-      else k_fir_iq8<256><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out);
+      const dim3 g8(grid_for(n_out, 8 * NT), nch);
+      if (K <= 64) k_fir_iq8<64><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out, x_stride, y_stride);
+      else if (K <= 128) k_fir_iq8<128><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out, x_stride, y_stride);
+      else k_fir_iq8<256><<<g8, NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, g, nullptr, hist_out, x_stride, y_stride);
     }
   } else {
-    k_fir_iq_generic<<<grid_for(n_out, NT), NT, 0, s>>>(x, n, hist, hist_len, y, n_out, off, K, g_dev);
-    if (hist_out) launch_hist_update_c(x, n, hist, hist_out, hist_len, s);
+    for (int ch = 0; ch < nch; ++ch) {
+      const f2* xc = x + ch * x_stride;
+      const f2* hc = hist + static_cast<long long>(ch) * hist_len;
+      k_fir_iq_generic<<<grid_for(n_out, NT), NT, 0, s>>>(xc, n, hc, hist_len, y + ch * y_stride, n_out, off, K, g_dev);
+      if (hist_out) launch_hist_update_c(xc, n, hc, hist_out + static_cast<long long>(ch) * hist_len, hist_len, s);
+    }
   }
   ORION_LAUNCH_CHECK();
 }

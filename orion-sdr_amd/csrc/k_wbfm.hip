@@ -1372,14 +1372,12 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
   }
   fu::trace(a, g.r, 1);
   // ---- deferred: sub-range 0 from the predecessor's end state ----
-  {
-    const f4* gs = reinterpret_cast<const f4*>(myslot + kFuSlot);
-    f4 u[sg::L / 256];
+  // The parked phi's loads are issued first and written to LDS after the predecessor's
+  // record has arrived, so that their round trip overlaps the flag poll's.
+  const f4* gs = reinterpret_cast<const f4*>(myslot + kFuSlot);
+  f4 u[sg::L / 256];
 #pragma unroll
-    for (int i = 0; i < sg::L / 256; ++i) u[i] = __builtin_nontemporal_load(gs + l + 64 * i);
-#pragma unroll
-    for (int i = 0; i < sg::L / 256; ++i) *reinterpret_cast<f4*>(Phi + 4 * (l + 64 * i)) = u[i];
-  }
+  for (int i = 0; i < sg::L / 256; ++i) u[i] = __builtin_nontemporal_load(gs + l + 64 * i);
   if (g.first) {
     const float* __restrict__ ci = a.carry_in + g.ch * kWbfmCarry;
 #pragma unroll
@@ -1394,6 +1392,8 @@ __global__ __launch_bounds__(64, 2) void k_wbfm_seg(const WbfmArgs a, const Wbfm
     hist[0] = __uint_as_float(fu::ld_agent(ps + 16 + l));
     hist[1] = __uint_as_float(fu::ld_agent(ps + 16 + 64 + l));
   }
+#pragma unroll
+  for (int i = 0; i < sg::L / 256; ++i) *reinterpret_cast<f4*>(Phi + 4 * (l + 64 * i)) = u[i];
   lds_order();
   fu::trace(a, g.r, 2);
   sg::back(a, Bc, g.ch, g.A, min(sg::L, g.Lr), g.last && nsub == 1, Phi, P, Aw, l, sw, hist);

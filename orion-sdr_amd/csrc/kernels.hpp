@@ -63,9 +63,12 @@ void launch_fir_real(const float* x_dev, long long n, const float* hist_dev, int
 // Complex-sample real-tap FIR y[i] = sum_k g[k] x[i + off - k], i < n_out
 // (x[P<0] from hist, x[P>=n] = 0). off = 0: streaming; off = (K-1)/2 with an
 // all-zero history: FirLowpassIq::filter_aligned.
+// nch > 1: independent channels, channel ch at x + ch x_stride / y + ch y_stride, its
+// histories at ch hist_len of hist_dev / hist_out (batched FirLowpassIq).
 void launch_fir_iq(const f2* x_dev, long long n, const f2* hist_dev, int hist_len, f2* y_dev,
                    long long n_out, long long off, int K, const Taps256& g, const float* g_dev,
-                   hipStream_t s, f2* hist_out = nullptr);
+                   hipStream_t s, f2* hist_out = nullptr, int nch = 1, long long x_stride = 0,
+                   long long y_stride = 0);
 // Copy the last hist_len samples of [old_hist | x[0..n)] into new_hist.
 // FirLowpassIq::filter_aligned in place (k_fir_iq8 INPLACE + boundary copies);
 // writes the history the reference leaves (last hist_len of [x | 0^d]) to

@@ -108,6 +108,7 @@ def _load():
         "orion_fir_lowpass_new": (vp, [f, f, f]),
         "orion_fir_lowpass_iq_design": (vp, [sz, f, f]),
         "orion_fir_lowpass_iq_from_taps": (vp, [fp, sz]),
+        "orion_fir_lowpass_iq_batch_from_taps": (vp, [fp, sz, sz]),
         "orion_fir_lowpass_iq_filter_aligned_device": (i, [vp, vp, sz, vp]),
         "orion_fir_lowpass_iq_filter_aligned": (i, [vp, vp, sz]),
         "orion_lp_cascade_new": (vp, [f, f]),
@@ -413,13 +414,18 @@ class FirLowpassIq(_Block):
         super().__init__(handle)
 
     @classmethod
-    def design(cls, num_taps: int, cutoff_norm: float, stopband_db: float) -> "FirLowpassIq":
-        return cls(_L.orion_fir_lowpass_iq_design(num_taps, cutoff_norm, stopband_db))
+    def design(cls, num_taps: int, cutoff_norm: float, stopband_db: float, channels: int = 1) -> "FirLowpassIq":
+        """fir.rs:186-188; channels > 1: a batch of independent [channels, n] streams."""
+        if channels == 1:
+            return cls(_L.orion_fir_lowpass_iq_design(num_taps, cutoff_norm, stopband_db))
+        return cls.from_taps(cls.design(num_taps, cutoff_norm, stopband_db).taps(), channels)
 
     @classmethod
-    def from_taps(cls, taps) -> "FirLowpassIq":
+    def from_taps(cls, taps, channels: int = 1) -> "FirLowpassIq":
         t = np.ascontiguousarray(taps, np.float32)
-        return cls(_L.orion_fir_lowpass_iq_from_taps(_fptr(t) if t.size else None, t.size))
+        if channels == 1:
+            return cls(_L.orion_fir_lowpass_iq_from_taps(_fptr(t) if t.size else None, t.size))
+        return cls(_L.orion_fir_lowpass_iq_batch_from_taps(_fptr(t) if t.size else None, t.size, channels))
 
     def num_taps(self) -> int:
         """fir.rs:210-212."""
