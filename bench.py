@@ -59,7 +59,7 @@ METRICS = {  # the non-default configs name what they measure
 KERNELS = {"c1": "k_fir_iq8", "c2": "k_wbfm_seg", "c3": "k_decim_w4q", "c4": "k_wbfm_seg", "c5": "k_lpdc_sp",
            "c5f": "k_fir_iq8"}
 CHANNELS_PER_GPU = {"c3": 256, "c4": 8, "c5": 128, "c5f": 128}
-C3_DESIGN = (10e6, 8, 200e3, 39370.0)  # FirDecimator(10e6, 8, 200e3, 39370) = 255 taps
+C3_DESIGN = (10e6, 8, 190e3, 39370.0)  # BASELINE C3: 255 taps (SURVEY §8(d)'s 200e3 cutoff gives 251)
 C5F_FIR = (127, 3000.0 / 48e3, 60.0)  # FirLowpassIq::design: +-3 kHz around the SSB channel, 60 dB
 NOISE = ("complex AWGN from splitmix64(seed, sample index) + Box-Muller: every sample a function of its "
          "index, so a time shard with its halo is the stream's slice (the reference's add_awgn "
@@ -265,7 +265,7 @@ def make_workload(cfg, rank, dev, n_override=None, world=1, shard="stream"):
         nch, n = len(plan), n_override or (1 << 20)
         blk = orion_sdr.FirDecimator(*C3_DESIGN, channels=nch)
         x = torch.stack([channel_input(cfg, n, seed, dev) for _, seed in plan]).contiguous()
-        desc = dict(workload="C3 batched FirDecimator(10e6, 8, 200e3, 39370), 256 channels x 255 taps, M=8",
+        desc = dict(workload="C3 batched FirDecimator(10e6, 8, 190e3, 39370), 256 channels x 255 taps, M=8",
                     samples_per_step_per_gpu=nch * n, channels_per_gpu=nch, channels=[plan[0][0], plan[-1][0] + 1],
                     input="unit-power complex Gaussian noise per channel (torch generator, seed per channel)")
         return blk, x, nch * n, 9.0, desc

@@ -395,11 +395,31 @@ def test_decimator_batch_c3(gpu_lib, oracle):
     """C3 shape (255 taps, M = 8) on 16 channels x 2^16 (subset of 256 x 2^20)."""
     nch, n = 16, 1 << 16
     x = cnoise(nch * n).reshape(nch, n)
-    D = gpu_lib.FirDecimator(10e6, 8, 200e3, 39370.0, channels=nch)
+    D = gpu_lib.FirDecimator(10e6, 8, 190e3, 39370.0, channels=nch)
     assert len(D.taps()) == 255
     got = D.process(x)
-    ref = oracle.decim_channels(x, 10e6, 8, 200e3, 39370.0, 8)
+    ref = oracle.decim_channels(x, 10e6, 8, 190e3, 39370.0, 8)
     report("decim batch C3 nrmse", nrmse(got, ref), 1e-6)
+
+
+@pytest.mark.parametrize("nch,n,chunk", [(13, 50_001, 16_384), (8, 300, 104), (24, 2_000_000, 0), (9, 5000, 8)])
+def test_decimator_batch_geometries(gpu_lib, oracle, nch, n, chunk):
+    """The batched 255-tap decimator (C3's design; the matrix-core form k_decim_mx for
+    >= 8 channels) at ragged channel counts (a partial group of 8), a call shorter than
+    one 16-output block's window, many ranges per channel, and streamed calls (multiples
+    of m: the history carried per channel across calls, decim.rs:44-76)."""
+    x = cnoise(nch * n).reshape(nch, n)
+    D = gpu_lib.FirDecimator(10e6, 8, 190e3, 39370.0, channels=nch)
+    if chunk:
+        got = np.concatenate([D.process(np.ascontiguousarray(x[:, i: i + chunk])) for i in range(0, n, chunk)],
+                             axis=1)
+        ref = np.stack([oracle.fir_decimator(x[c], 10e6, 8, 190e3, 39370.0, chunk=chunk) for c in range(nch)])
+    else:
+        got = D.process(x)
+        ref = oracle.decim_channels(x, 10e6, 8, 190e3, 39370.0, 8)
+    assert got.shape == ref.shape
+    for c in sorted({0, nch // 2, nch - 1}):
+        report(f"decim batch {nch} ch n={n} chunk={chunk} ch={c} nrmse", nrmse(got[c], ref[c]), 1e-6)
 
 
 # ---- FirLowpass (a3), FirLowpassIq (a5) --------------------------------------------------

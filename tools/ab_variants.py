@@ -4,7 +4,7 @@
 chip's clock state hits every variant alike, one HIP event pair per launch.
   python tools/ab_variants.py --case c5 --rounds 4 --k 10 base v1 v2
 A name may carry engine options for its block: base@scan_path=2 (orion_block_configure).
-Cases: c2 (WBFM 2^26), c4 (WBFM 8 x 2^24), c5 (SSB 128 x 2^20; c5b: bench.py's tone + noise input), a4 (FirDecimator 127 taps 2^24), a10 (SSB 2^24), a11 / a11abs (AM PowerSqrt / AbsApprox 2^24), a7 (DcBlocker
+Cases: c2 (WBFM 2^26), c3 (FirDecimator 255 taps, 256 x 2^20), c4 (WBFM 8 x 2^24), c5 (SSB 128 x 2^20; c5b: bench.py's tone + noise input), a4 (FirDecimator 127 taps 2^24), a10 (SSB 2^24), a11 / a11abs (AM PowerSqrt / AbsApprox 2^24), a7 (DcBlocker
 2^24), a6 (LpCascade 2^24), a9 (FM demod 2^24)."""
 import argparse
 import importlib.util
@@ -40,6 +40,9 @@ def case(m, name, dev):
         tone = torch.polar(torch.ones_like(t), 2 * 3.141592653589793 * 2700.0 * t).to(torch.complex64) * 0.4
         x = tone + 0.03 * torch.randn(128, 1 << 20, dtype=torch.complex64, device=dev, generator=g)
         return m.SsbProductDemod(48e3, 1500.0, 2800.0, channels=128), x.contiguous()
+    if name == "c3":
+        return (m.FirDecimator(10e6, 8, 190e3, 39370.0, channels=256),
+                torch.randn(256, 1 << 20, dtype=torch.complex64, device=dev, generator=g))
     if name == "a4":
         return (m.FirDecimator(10e6, 8, 200e3, 79e3),
                 torch.randn(1 << 24, dtype=torch.complex64, device=dev, generator=g))
