@@ -26,7 +26,6 @@ constexpr int kMaxGrid = 2048;  // memory-bound: cap and grid-stride (2048 = 8 W
 enum : int { kRotate = 0, kUsb = 1, kNcoMix = 2, kNcoGen = 3 };
 constexpr int kRotMinW = 6;          // waves per SIMD k_rotator is compiled for (8: <= 64 VGPRs, 6 B of spills)
 constexpr int kFir4TilesPerCu = 4;   // k_fir_iq8 with 4 outputs per lane below this many 2048-output tiles per CU
-constexpr bool kDecimMx = false;      // batched 129..256-tap M = 8 decimator on the matrix cores (k_decim_mx)
 constexpr int kRotHp = 2;            // pairs per thread whose loads a full tile issues together
 template <bool A16, int MODE>
 __global__ __launch_bounds__(NT, kRotMinW) void k_rotator(const f2* __restrict__ x, void* __restrict__ yv, long long n,
@@ -427,172 +426,6 @@ __global__ __launch_bounds__(256, 3) void k_decim_w4q(const f2* __restrict__ x, 
   }
 }
 
-// ------------------------------------ batched decimator on the f32 matrix cores ---
-// k_decim_mx (C3: many channels sharing one 129..256-tap design, M = 8): one wave
-// per (group of 8 channels, range of outputs), 16 outputs of all 8 channels per block
-// as ONE Toeplitz product on v_mfma_f32_16x16x4_f32 (exact f32 products, the f32
-// accumulation an FMA chain's):
-//   C[i][n] = sum_j A[i][j] B[j][n],  i = output o0 + i (16 rows),
-//   n = 2 ch + c (8 channels x re/im: 16 columns), j = window entry (K' = 384),
-//   B[j][n] = x_ch[8 o0 - (K - 1) + j].c,   A[i][j] = g[8 i + K - 1 - j] (0 outside
-//   [0, K)): the taps are the same for every channel, so the A operand is a constant
-//   of the lane (96 VGPRs) and only B streams through LDS (a ring of 512 window
-//   entries per column: block b reads 384 of them, the staging writes the next 128).
-// The K order: step s = 4 s4 + t, lane quarter kg reads j = 16 s4 + 4 kg + t (one
-// ds_read_b128 per lane per four steps); ring rows pitched 520 floats, so the 16 lanes
-// of each gfx950 ds_read_b128 group (A = 0-3, 12-15, 20-27; B = 4-11, 16-19, 28-31;
-// C, D = A, B + 32) cover the 64 banks once. 1.5x the direct form's FMAs (K' = 384
-// window entries for 255 taps), all on the matrix pipe; the VALU only stages.
-namespace mx {
-constexpr int S = 96;        // MFMA steps per block (K' = 4 S = 384 >= 255 + 120)
-constexpr int RING = 512;    // window entries per column ring (block: 384 read + 128 staged)
-constexpr int RP = 520;      // ring pitch (floats): RP / 4 = 2 mod 16 (conflict-free b128 reads)
-constexpr int CHUNK = 128;   // new entries per block (16 outputs x M)
-static_assert(4 * S + CHUNK <= RING && (RP / 4) % 16 == 2, "ring geometry");
-}  // namespace mx
-
-// The chunk of 128 window entries starting at sample p0 of channel ch, this lane's 16
-// samples p0 + 2 seg + 16 k (+1), k < 8: each load instruction reads 128 contiguous
-// bytes per channel (8 lanes x 16 B); branch-free at a clamped address (a branchy load
-// makes the compiler wait for it at once, vmcnt(0), instead of a block later), the
-// chunks that reach before 0 (the call's history), past n (zeros) or a channel past nch
-// (zeros) rewritten exactly at staging time (mx_fix).
-template <bool A16>
-__device__ __forceinline__ void mx_issue(const f2* __restrict__ x, long long x_stride, long long n, int nch, int ch,
-                                         long long p0, int seg, f4 (&v)[8]) {
-  const long long p = min(max(p0, 0LL), max(n - 128, 0LL)) + 2 * seg;
-  const f2* __restrict__ xc = x + min(ch, nch - 1) * x_stride + p;
-  const bool in = n >= 128;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if constexpr (A16) {
-      v[k] = in ? __builtin_nontemporal_load(reinterpret_cast<const f4*>(xc + 16 * k)) : f4{0, 0, 0, 0};
-    } else {
-      const f2 a = in ? xc[16 * k] : f2{0, 0}, b = in ? xc[16 * k + 1] : f2{0, 0};
-      v[k] = f4{a.x, a.y, b.x, b.y};
-    }
-  }
-}
-__device__ __forceinline__ void mx_fix(const f2* __restrict__ x, long long x_stride, long long n,
-                                       const f2* __restrict__ hist, int hist_len, int nch, int ch, long long p0,
-                                       int seg, f4 (&v)[8]) {
-  if (ch < nch && p0 >= 0 && p0 + 128 <= n) return;
-  if (ch >= nch) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = f4{0, 0, 0, 0};
-    return;
-  }
-  const f2* __restrict__ xc = x + ch * x_stride;
-  const f2* __restrict__ hc = hist + static_cast<long long>(ch) * hist_len;
-#pragma unroll 1
-  for (int k = 0; k < 8; ++k) {
-    const long long p = p0 + 2 * seg + 16 * k;
-    const f2 a = load_hist(xc, n, hc, hist_len, p), b = load_hist(xc, n, hc, hist_len, p + 1);
-    v[k] = f4{a.x, a.y, b.x, b.y};
-  }
-}
-// Chunk c of the window into its ring slot: lane (ch, seg) holds samples 2 seg + 16 k
-// and + 1: their re parts into column 2 ch, im into 2 ch + 1 (eight ds_write_b64 each).
-__device__ __forceinline__ void mx_stage(float* __restrict__ Bs, int ch, int seg, int c, const f4 (&v)[8]) {
-  const int off = (mx::CHUNK * c + 2 * seg) & (mx::RING - 1);
-  float* re = Bs + (2 * ch) * mx::RP + off;
-  float* im = Bs + (2 * ch + 1) * mx::RP + off;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    *reinterpret_cast<f2*>(re + 16 * k) = f2{v[k].x, v[k].z};
-    *reinterpret_cast<f2*>(im + 16 * k) = f2{v[k].y, v[k].w};
-  }
-}
-
-template <bool A16>
-__global__ __launch_bounds__(64, 1) void k_decim_mx(const f2* __restrict__ x, long long x_stride, long long n,
-                                                   const f2* __restrict__ hist, int hist_len, f2* __restrict__ out,
-                                                   long long out_stride, long long n_out, int nch, int K,
-                                                   const float* __restrict__ g, int rpg, long long L,
-                                                   f2* __restrict__ hist_out) {
-  __shared__ __attribute__((aligned(16))) float Bs[16 * mx::RP];
-  const int l = threadIdx.x & 63;
-  const int grp = blockIdx.x / rpg, r = blockIdx.x - grp * rpg;
-  const long long A = static_cast<long long>(r) * L;
-  const long long B = min(A + L, n_out);
-  if (A >= B) return;
-  const int ch0 = 8 * grp;
-  if (A == 0 && hist_out) {  // the next call's histories of the group's channels
-    for (int c = 0; c < 8 && ch0 + c < nch; ++c)
-      dw_hist_next(x + (ch0 + c) * x_stride, n, hist + static_cast<long long>(ch0 + c) * hist_len, hist_out, ch0 + c,
-                   hist_len, l);
-  }
-  // the lane's A operand: a[s] = g[8 i + K - 1 - j(s)], j(s) = 16 (s >> 2) + 4 kg + (s & 3)
-  const int i = l & 15, kg = l >> 4;
-  float a[mx::S];
-#pragma unroll
-  for (int s = 0; s < mx::S; ++s) {
-    const int k = 8 * i + K - 1 - (16 * (s >> 2) + 4 * kg + (s & 3));
-    a[s] = (k >= 0 && k < K) ? g[k] : 0.0f;
-  }
-  const int sch = l >> 3, seg = l & 7;  // staging role: channel ch0 + sch, samples 16 seg ..
-  const long long W0 = 8 * A - (K - 1);  // window entry 0 of block 0
-  const int nb = static_cast<int>((B - A + 15) / 16);
-  f4 v[8];
-#pragma unroll 1
-  for (int c = 0; c < 3; ++c) {  // blocks 0's three chunks
-    mx_issue<A16>(x, x_stride, n, nch, ch0 + sch, W0 + mx::CHUNK * c, seg, v);
-    mx_fix(x, x_stride, n, hist, hist_len, nch, ch0 + sch, W0 + mx::CHUNK * c, seg, v);
-    mx_stage(Bs, sch, seg, c, v);
-  }
-  mx_issue<A16>(x, x_stride, n, nch, ch0 + sch, W0 + 3 * mx::CHUNK, seg, v);  // chunk 3
-  const int n_col = l & 15;  // this lane's B / C column
-  const float* __restrict__ Bcol = Bs + n_col * mx::RP;
-  typedef float f4v __attribute__((ext_vector_type(4)));
-#pragma unroll 1
-  for (int b = 0; b < nb; ++b) {
-    // the block's 24 B reads first (their latency is exposed once per block, not once
-    // per four steps), then chunk b + 3 into the slot block b - 1 read last (a wave's
-    // LDS operations run in order), then its successor's loads (dummy past the range:
-    // the range's own first chunk again, L2-resident)
-    const int base = mx::CHUNK * b;
-    f4 wb[mx::S / 4];
-#pragma unroll
-    for (int s4 = 0; s4 < mx::S / 4; ++s4)
-      wb[s4] = *reinterpret_cast<const f4*>(Bcol + ((base + 16 * s4 + 4 * kg) & (mx::RING - 1)));
-    asm volatile("" ::: "memory");
-    mx_fix(x, x_stride, n, hist, hist_len, nch, ch0 + sch, W0 + mx::CHUNK * (b + 3), seg, v);
-    mx_stage(Bs, sch, seg, b + 3, v);
-    asm volatile("" ::: "memory");
-    const long long pn = b + 1 < nb ? W0 + mx::CHUNK * (b + 4) : W0;
-    mx_issue<A16>(x, x_stride, n, nch, ch0 + sch, pn, seg, v);
-    f4v acc[2] = {f4v{0, 0, 0, 0}, f4v{0, 0, 0, 0}};
-#pragma unroll
-    for (int s4 = 0; s4 < mx::S / 4; ++s4) {
-      const f4 w = wb[s4];
-      acc[s4 & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * s4], w.x, acc[s4 & 1], 0, 0, 0);
-      acc[s4 & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * s4 + 1], w.y, acc[s4 & 1], 0, 0, 0);
-      acc[s4 & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * s4 + 2], w.z, acc[s4 & 1], 0, 0, 0);
-      acc[s4 & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[4 * s4 + 3], w.w, acc[s4 & 1], 0, 0, 0);
-    }
-    // lane (n, kg): column n = 2 ch + c, rows 4 kg .. 4 kg + 3. Adjacent lanes (re, im)
-    // trade halves: the even lane stores outputs 4 kg, 4 kg + 1, the odd one 4 kg + 2, + 3
-    const f4v cv = acc[0] + acc[1];
-    float p[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      p[q] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(cv[q]), 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
-    const bool odd = n_col & 1;
-    const int ch = ch0 + (n_col >> 1);
-    const long long o = A + 16LL * b + 4 * kg + (odd ? 2 : 0);
-    const f4 st = odd ? f4{p[2], cv[2], p[3], cv[3]} : f4{cv[0], p[0], cv[1], p[1]};
-    if (ch < nch) {
-      f2* __restrict__ oc = out + ch * out_stride;
-      if (o + 1 < B && (reinterpret_cast<uintptr_t>(oc + o) & 15) == 0) {
-        __builtin_nontemporal_store(st, reinterpret_cast<f4*>(oc + o));
-      } else {
-        if (o < B) oc[o] = f2{st.x, st.y};
-        if (o + 1 < B) oc[o + 1] = f2{st.z, st.w};
-      }
-    }
-  }
-}
-
 __global__ __launch_bounds__(NT) void k_decim_generic(const f2* __restrict__ x, long long x_stride,
                                                       long long n, const f2* __restrict__ hist,
                                                       int hist_len, f2* __restrict__ out,
@@ -964,21 +797,6 @@ void launch_decim_batch(const f2* x, long long x_stride, long long n, const f2* 
                         const Taps256& g, const float* g_dev, hipStream_t s, f2* hist_out) {
   if (n_out <= 0 || nch <= 0) return;
   const bool a16 = reinterpret_cast<uintptr_t>(x) % 16 == 0 && x_stride % 2 == 0;
-  // M = 8 with 129..256 taps over >= 8 channels: the matrix-core form (k_decim_mx)
-  if (kDecimMx && M == 8 && K > 128 && K <= 256 && hist_len >= K - 1 && nch >= 8 && g_dev) {
-    const int groups = (nch + 7) / 8;
-    const int cap = resident_per_cu(reinterpret_cast<const void*>(k_decim_mx<true>), 64) * device_cus();
-    long long rpg = std::max(1, cap / groups);
-    long long L = ((n_out + rpg - 1) / rpg + 15) / 16 * 16;
-    rpg = (n_out + L - 1) / L;
-    const long long grid = rpg * groups;
-    if (grid > (1LL << 31) - 1) throw HipError("decimator grid too large");
-    const int gi = static_cast<int>(grid), ri = static_cast<int>(rpg);
-    if (a16) k_decim_mx<true><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, nch, K, g_dev, ri, L, hist_out);
-    else k_decim_mx<false><<<gi, 64, 0, s>>>(x, x_stride, n, hist, hist_len, out, out_stride, n_out, nch, K, g_dev, ri, L, hist_out);
-    ORION_LAUNCH_CHECK();
-    return;
-  }
   // M = 8 with 129..256 taps (C3): k_decim_w4q, four waves per workgroup sharing one
   // tap table (three waves per SIMD); M = 8 with <= 128 taps: k_decim_w4.
   if (M == 8 && K > 128 && K <= 256 && hist_len >= 8 * 32) {
