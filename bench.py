@@ -450,7 +450,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c5f"])
-    ap.add_argument("--n", type=int, default=0, help="override samples per channel")
+    ap.add_argument("--n", "--samples", dest="n", type=int, default=0,
+                    help="override samples per channel (under torch.distributed.run use --samples: its own "
+                         "parser reads --n as an abbreviation of its options)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-max-samples", type=int, default=1 << 24)
     ap.add_argument("--no-cpu", action="store_true")
