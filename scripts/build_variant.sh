@@ -13,4 +13,4 @@ if [ "$rev" = "." ]; then
 else
   git -C "$ROOT" archive "$rev" orion-sdr_amd/csrc orion-sdr_amd/Makefile include | tar -x -C "$src"
 fi
-make -s -C "$src/orion-sdr_amd" -j8 LIB="$ROOT/orion-sdr_amd/exp/$name/liborion_sdr_amd.so"
+make -s -C "$src/orion-sdr_amd" -j8 DEFS="${DEFS:-}" LIB="$ROOT/orion-sdr_amd/exp/$name/liborion_sdr_amd.so"
