@@ -1074,6 +1074,16 @@ class WbfmBlock final : public Block {
   // by 2^st so that max |a| 2^st lies in [2^14, 2^15) (a power of two: exact). The f
   // scale is the kernel's, per sub-range.
   void build_audio_frags(const std::vector<float>& a) {
+#if ORION_WBFM_EXACT_FIR
+    cs_.tscale = 1.0f;
+    std::vector<float> at(kAudFragBytes / 4, 0.0f);
+    for (int m = 0; m < 176; ++m) {
+      const int k = m - 31;
+      if (k >= 0 && k < 128 && k < static_cast<int>(a.size())) at[m] = a[k];
+    }
+    afrag_.upload(at.data(), kAudFragBytes);
+    return;
+#endif
     float amax = 0.0f;
     for (float v : a) amax = std::max(amax, std::fabs(v));
     int e = 0;

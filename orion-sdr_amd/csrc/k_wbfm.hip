@@ -1033,7 +1033,21 @@ __device__ __forceinline__ void zs_only16(const WbfmFusedConst& Bc, const float*
 // (pe: the 16 column reads of one ds_read_b128 hit distinct banks).
 __host__ __device__ constexpr int pe(int e) { return e + ((e >> 7) << 3); }
 constexpr int kFpN = pe(128 + 1024 + 16) + 8;  // halves per plane
+#ifndef ORION_WBFM_EXACT_FIR
+#define ORION_WBFM_EXACT_FIR 0
+#endif
+#if ORION_WBFM_EXACT_FIR
+// Build option (make DEFS=-DORION_WBFM_EXACT_FIR=1): the audio FIR on
+// v_mfma_f32_16x16x4_f32, exact f32 operands and an FMA chain per output: one f32 plane,
+// 4 pad floats per 64 (the 16 columns x 4 k of a read hit distinct banks), taps
+// At[m] = a[m - 31] (host). Measured round 6: +21 us per C2 launch, and the chain's
+// error against the oracle unchanged to three digits at every signal level
+// (profiles/r6_wbfm_ab_f32fir.txt), so the split-f16 form stays the default.
+__host__ __device__ constexpr int pf(int e) { return e + 4 * (e >> 6); }
+constexpr int kTxOff = pf(128 + 1024 + 16) * 4;
+#else
 constexpr int kTxOff = 2 * kFpN * 2;           // bytes: the exact next history (128 f32) after the planes
+#endif
 static_assert(kTxOff % 16 == 0 && kTxOff + 128 * 4 <= WBytes, "f planes + exact history fit the sub-range region");
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ _Float16 hi16(float x) { return static_cast<_Float16>(x); }
@@ -1135,6 +1149,20 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
       if (t >= 0) Tx[t] = hist[r2];
     }
   }
+#if ORION_WBFM_EXACT_FIR
+  const int sf = 0;
+  {
+    float* __restrict__ Fp = static_cast<float*>(Pv);
+    const int e0 = pf(128 + 16 * l);
+    *reinterpret_cast<f4*>(Fp + e0) = f4{xs[0].x, xs[1].x, xs[2].x, xs[3].x};
+    *reinterpret_cast<f4*>(Fp + e0 + 4) = f4{xs[4].x, xs[5].x, xs[6].x, xs[7].x};
+    *reinterpret_cast<f4*>(Fp + e0 + 8) = f4{xs[0].y, xs[1].y, xs[2].y, xs[3].y};
+    *reinterpret_cast<f4*>(Fp + e0 + 12) = f4{xs[4].y, xs[5].y, xs[6].y, xs[7].y};
+#pragma unroll
+    for (int r2 = 0; r2 < 2; ++r2) Fp[pf(l + 64 * r2)] = hist[r2];
+    if (l < 4) *reinterpret_cast<f4*>(Fp + pf(128 + 1024 + 4 * l)) = f4{0, 0, 0, 0};
+  }
+#else
   // this sub-range's f scale: max |f| over the FIR's window (outputs and history)
   float mx = fmaxf(fabsf(hist[0]), fabsf(hist[1]));
 #pragma unroll
@@ -1174,6 +1202,7 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
     *reinterpret_cast<h8*>(Fh + pe(128 + 1024 + 8 * l)) = z;
     *reinterpret_cast<h8*>(Fl + pe(128 + 1024 + 8 * l)) = z;
   }
+#endif
   lds_order();
 #pragma unroll
   for (int r2 = 0; r2 < 2; ++r2) hist[r2] = Tx[l + 64 * r2];  // f[Lr - 128 + t]: the next history
@@ -1194,6 +1223,23 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
     // then the four groups' MFMAs interleaved (independent accumulators back to back).
     // (The fragments from global memory, L2-resident, cost ~0.5 us per step under the
     // fronts' HBM load: the trace's FIR phase, round 6.)
+#if ORION_WBFM_EXACT_FIR
+    {
+      const float* __restrict__ Fp = static_cast<const float*>(Pv);
+      const float* __restrict__ At = reinterpret_cast<const float*>(Aw);
+      const int I = l & 15;
+#pragma unroll 4
+      for (int st = 0; st < 40; ++st) {
+        const float av = At[I - 4 * st - kg + 159];
+        const int p = pf(16 * J + 4 * st + kg);
+        float b[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) b[g] = Fp[p + 272 * g];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[g], acc[g], 0, 0, 0);
+      }
+    }
+#else
     const int I = l & 15;
 #pragma unroll 1
     for (int st = 0; st < 5; ++st) {
@@ -1223,6 +1269,7 @@ __device__ __forceinline__ void back(const WbfmArgs& a, const WbfmFusedConst& Bc
       asm volatile("" ::: "memory");  // the next step's plane reads stay behind these MFMAs (registers)
       if (trace_r >= 0 && st == 0) fu::trace(a, trace_r, 13);  // debug: step 0's operands arrived, MFMAs issued
     }
+#endif
     if (trace_r >= 0) fu::trace(a, trace_r, 14);  // debug: every MFMA issued
     // lane (J, kg) holds outputs 256 g + 16 J + 4 kg + r, r < 4
     float* __restrict__ y = a.y + ch * a.y_stride + A0;
