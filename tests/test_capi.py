@@ -1,6 +1,8 @@
 """CPU: the C-ABI library loads, exports every symbol include/orion_sdr_amd.h
-declares, and its host-side designs equal the reference designs bit for bit.
-No kernel is launched here (no GPU in the CPU container)."""
+declares, and its host-side designs equal the reference designs bit for bit; a
+plain-C program (tests/c_abi) compiles against the header and links the library.
+No kernel is launched by the CPU tests; the one `gpu` test runs that C program's
+WBFM chain on the device against the oracle."""
 import ctypes
 import os
 import re
@@ -118,3 +120,46 @@ def test_osc_drift_model_past_the_budget(oracle, f, fs):
     err = float(np.max(np.abs(got[b:].astype(np.complex128) - ref[b:])))
     print(f"[parity] osc drift model {f}/{fs}: max |model - reference| over {n - b} outputs past the budget {err:.3e}")
     assert err < 2e-4
+
+
+C_CONSUMER = os.path.join(ROOT, "tests", "c_abi", "wbfm_c_consumer")
+
+
+def _c_consumer():
+    """The plain-C consumer (tests/c_abi, built by __graft_entry__.build()): rebuilt here
+    when a C compiler is at hand, so this check follows the header."""
+    import shutil
+    import subprocess
+
+    if shutil.which("gcc"):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(C_CONSUMER)], check=True)
+    assert os.path.exists(C_CONSUMER), "tests/c_abi/wbfm_c_consumer not built (run __graft_entry__.build())"
+    return C_CONSUMER
+
+
+def test_c_consumer_links_and_fails_loudly_without_a_device():
+    """The header compiles as C11 and the library links into a C program with no C++
+    or Python around it. With no device visible the chain's constructor fails with
+    the library's message (exit 2), never a CPU fallback."""
+    import subprocess
+
+    import orion_sdr
+
+    r = subprocess.run([_c_consumer(), "4096"], capture_output=True, text=True, timeout=120)
+    if orion_sdr.device_count() > 0:
+        assert r.returncode == 0, r.stdout + r.stderr
+    else:
+        assert r.returncode == 2, r.stdout + r.stderr
+        assert "orion_wbfm_chain_new" in r.stderr and "device" in r.stderr
+
+
+@pytest.mark.gpu
+def test_c_consumer_wbfm_parity_on_the_gpu():
+    """The same C program on the GPU: the C2 design through orion_wbfm_chain_new and six
+    ragged orion_block_process host calls over 2^20 samples, against the oracle streamed
+    in the same calls (1e-5 nrmse, the WBFM tolerance)."""
+    import subprocess
+
+    r = subprocess.run([_c_consumer(), str(1 << 20)], capture_output=True, text=True, timeout=300)
+    print(r.stdout.strip())
+    assert r.returncode == 0, r.stdout + r.stderr
