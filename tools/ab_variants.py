@@ -5,7 +5,7 @@ chip's clock state hits every variant alike, one HIP event pair per launch.
   python tools/ab_variants.py --case c5 --rounds 4 --k 10 base v1 v2
 A name may carry engine options for its block: base@scan_path=2 (orion_block_configure).
 Cases: c1 (FirLowpassIq 127 taps 2^20), c2 (WBFM 2^26), c3 (FirDecimator 255 taps, 256 x 2^20), c4 (WBFM 8 x 2^24), c5 (SSB 128 x 2^20; c5b: bench.py's tone + noise input), a4 (FirDecimator 127 taps 2^24), a10 (SSB 2^24), a11 / a11abs (AM PowerSqrt / AbsApprox 2^24), a7 (DcBlocker
-2^24), a6 (LpCascade 2^24), a9 (FM demod 2^24), a3 (FirLowpass 125 taps 2^24)."""
+2^24), a6 (LpCascade 2^24), a9 (FM demod 2^24), a3 (FirLowpass 125 taps 2^24), fmmod (FmPhaseAccumMod 2^26)."""
 import argparse
 import importlib.util
 import os
@@ -49,6 +49,8 @@ def case(m, name, dev):
     if name == "c1":  # BASELINE configs[0]: FirLowpassIq 127 taps on 2^20 samples
         return (m.FirLowpassIq.design(127, 0.2, 60.0),
                 torch.randn(1 << 20, dtype=torch.complex64, device=dev, generator=g))
+    if name == "fmmod":  # FmPhaseAccumMod (10 MHz, 75 kHz, RF 1.5 MHz) on 2^26 audio samples
+        return m.FmPhaseAccumMod(10e6, 75e3, 1.5e6), torch.randn(1 << 26, dtype=torch.float32, device=dev, generator=g) * 0.5
     if name == "a3":
         return m.FirLowpass(1.25e6, 15e3, 10e3), torch.randn(1 << 24, dtype=torch.float32, device=dev, generator=g)
     if name == "a10":
