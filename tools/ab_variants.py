@@ -3,7 +3,8 @@
 = lib/) is loaded as its own module, launches are interleaved A B C, B C A, ... so the
 chip's clock state hits every variant alike, one HIP event pair per launch.
   python tools/ab_variants.py --case c5 --rounds 4 --k 10 base v1 v2
-A name may carry engine options for its block: base@scan_path=2 (orion_block_configure).
+A name may carry engine options for its block: base@scan_path=2 (orion_block_configure),
+base@wbfm_path=split (WbfmChain.configure).
 Cases: c1 (FirLowpassIq 127 taps 2^20), c2 (WBFM 2^26), c3 (FirDecimator 255 taps, 256 x 2^20), c4 (WBFM 8 x 2^24), c5 (SSB 128 x 2^20; c5b: bench.py's tone + noise input), a4 (FirDecimator 127 taps 2^24), a10 (SSB 2^24), a11 / a11abs (AM PowerSqrt / AbsApprox 2^24), a7 (DcBlocker
 2^24), a6 (LpCascade 2^24), a9 (FM demod 2^24), a3 (FirLowpass 125 taps 2^24), fmmod (FmPhaseAccumMod 2^26)."""
 import argparse
@@ -90,7 +91,10 @@ def main():
         blk, x = case(m, a.case, dev) if not work else (case(m, a.case, dev)[0], next(iter(work.values()))[1])
         for o in opts:
             k, v = o.split("=")
-            blk.configure_option(k, int(v))
+            if k == "wbfm_path":  # WbfmChain kernel path: segmented / split / graph
+                blk.configure(v)
+            else:
+                blk.configure_option(k, int(v))
         out = blk.process_device(x)
         work[nm] = (blk, x, out)
     for nm in a.names:
