@@ -275,6 +275,13 @@ int orion_block_process(orion_block* b, const void* in, size_t n_in, void* out, 
  * internal copy of the input). */
 int orion_block_process_device(orion_block* b, const void* in_dev, size_t n_in, void* out_dev,
                                size_t out_cap, void* stream, orion_work_report* wr);
+/* The batched entry SURVEY §8(b) names (no reference counterpart: the reference runs one
+ * channel per Block): n_ch channels of n_per_ch samples laid out [n_ch][n_per_ch] on the
+ * device, outputs [n_ch][out_cap]; the handle must have been built for n_ch channels
+ * (the *_batch_new constructors), else ORION_E_ARG. Equals orion_block_process_device
+ * on the same buffers; wr reports per-channel counts. */
+int orion_batch_process(orion_block* b, const void* in_dev, size_t n_ch, size_t n_per_ch, void* out_dev,
+                        size_t out_cap, void* stream, orion_work_report* wr);
 /* Device-side failures (no reference counterpart; the reference never fails on the
  * path, core.rs:12-22): kernels that wait on other workgroups (the WBFM segment
  * hand-off, the single-pass scans' decoupled look-back, FmPhaseAccumMod's phase

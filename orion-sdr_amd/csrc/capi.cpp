@@ -474,6 +474,13 @@ int orion_block_process_device(orion_block* b, const void* in, size_t n_in, void
     return ORION_OK;
   });
 }
+int orion_batch_process(orion_block* b, const void* in, size_t n_ch, size_t n_per_ch, void* out, size_t out_cap,
+                        void* stream, orion_work_report* wr) {
+  if (!b) return fail(ORION_E_NULL, "null handle");
+  if (n_ch != static_cast<size_t>(b->impl->channels()))
+    return fail(ORION_E_ARG, "n_ch differs from the handle's channel count (build it with a *_batch_new constructor)");
+  return orion_block_process_device(b, in, n_per_ch, out, out_cap, stream, wr);
+}
 int orion_block_configure(orion_block* b, int option, long long value) {
   if (!b) return fail(ORION_E_NULL, "null handle");
   return guarded([&] {

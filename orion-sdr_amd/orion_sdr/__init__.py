@@ -137,6 +137,7 @@ def _load():
         "orion_wbfm_chain_seek": (i, [vp, C.c_uint64]),
         "orion_block_process": (i, [vp, vp, sz, vp, sz, C.POINTER(WorkReport)]),
         "orion_block_process_device": (i, [vp, vp, sz, vp, sz, vp, C.POINTER(WorkReport)]),
+        "orion_batch_process": (i, [vp, vp, sz, sz, vp, sz, vp, C.POINTER(WorkReport)]),
         "orion_block_reset": (i, [vp]), "orion_block_free": (None, [vp]),
         "orion_block_configure": (i, [vp, i, C.c_longlong]),
         "orion_block_status": (i, [vp]),

@@ -1605,3 +1605,33 @@ def test_diag_stream_read(gpu_lib):
     assert torch.equal(x, torch.arange(1 << 22, dtype=torch.float32, device="cuda"))
     with pytest.raises(gpu_lib.OrionError):
         gpu_lib.diag_stream_read(x[1:])
+
+
+def test_batch_process_entry(gpu_lib):
+    """SURVEY §8(b)'s batched entry, orion_batch_process: [n_ch][n_per_ch] device input
+    through a handle built for n_ch channels equals orion_block_process_device bit for
+    bit (batched SSB demod and batched decimator); an n_ch that differs from the
+    handle's channels is ORION_E_ARG."""
+    import ctypes as C
+
+    import torch
+
+    nch, n = 8, 50001
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(nch, n, dtype=torch.complex64, device="cuda", generator=g)
+    for mk in (lambda: gpu_lib.SsbProductDemod(FS, 1500.0, 2800.0, channels=nch),
+               lambda: gpu_lib.FirDecimator(10e6, 8, 190e3, 39370.0, channels=nch)):
+        ref = mk().process_device(x)
+        torch.cuda.synchronize()
+        blk = mk()
+        cap = ref.shape[-1]
+        out = torch.empty_like(ref)
+        wr = gpu_lib.WorkReport()
+        s = torch.cuda.current_stream().cuda_stream
+        rc = gpu_lib._L.orion_batch_process(blk._h, x.data_ptr(), nch, n, out.data_ptr(), cap, s, C.byref(wr))
+        torch.cuda.synchronize()
+        assert rc == 0 and wr.in_read == n and wr.out_written == cap
+        assert torch.equal(out, ref)
+        assert gpu_lib._L.orion_batch_process(blk._h, x.data_ptr(), nch - 1, n, out.data_ptr(), cap, s,
+                                              C.byref(wr)) == -3
+        print(f"[parity] orion_batch_process {blk.name}: {nch} x {n} equals process_device bit for bit")
