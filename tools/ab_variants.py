@@ -6,7 +6,8 @@ chip's clock state hits every variant alike, one HIP event pair per launch.
 A name may carry engine options for its block: base@scan_path=2 (orion_block_configure),
 base@wbfm_path=split (WbfmChain.configure).
 Cases: c1 (FirLowpassIq 127 taps 2^20), c2 (WBFM 2^26), c3 (FirDecimator 255 taps, 256 x 2^20), c4 (WBFM 8 x 2^24), c5 (SSB 128 x 2^20; c5b: bench.py's tone + noise input), a4 (FirDecimator 127 taps 2^24), a10 (SSB 2^24), a11 / a11abs (AM PowerSqrt / AbsApprox 2^24), a7 (DcBlocker
-2^24), a6 (LpCascade 2^24), a9 (FM demod 2^24), a3 (FirLowpass 125 taps 2^24), fmmod (FmPhaseAccumMod 2^26)."""
+2^24), a6 (LpCascade 2^24), a9 (FM demod 2^24), a3 (FirLowpass 125 taps 2^24), fmmod (FmPhaseAccumMod 2^26), a5 (FirLowpassIq 127 taps 2^24), c5fir (batched
+FirLowpassIq 128 x 2^20)."""
 import argparse
 import importlib.util
 import os
@@ -52,6 +53,12 @@ def case(m, name, dev):
                 torch.randn(1 << 20, dtype=torch.complex64, device=dev, generator=g))
     if name == "fmmod":  # FmPhaseAccumMod (10 MHz, 75 kHz, RF 1.5 MHz) on 2^26 audio samples
         return m.FmPhaseAccumMod(10e6, 75e3, 1.5e6), torch.randn(1 << 26, dtype=torch.float32, device=dev, generator=g) * 0.5
+    if name == "a5":  # FirLowpassIq 127 taps on 2^24 samples
+        return (m.FirLowpassIq.design(127, 0.2, 60.0),
+                torch.randn(1 << 24, dtype=torch.complex64, device=dev, generator=g))
+    if name == "c5fir":  # C5F's channel filter: batched FirLowpassIq 127 taps, 128 x 2^20
+        return (m.FirLowpassIq.from_taps(m.FirLowpassIq.design(127, 3000.0 / 48e3, 60.0).taps(), channels=128),
+                torch.randn(128, 1 << 20, dtype=torch.complex64, device=dev, generator=g))
     if name == "a3":
         return m.FirLowpass(1.25e6, 15e3, 10e3), torch.randn(1 << 24, dtype=torch.float32, device=dev, generator=g)
     if name == "a10":
