@@ -17,8 +17,9 @@
 //     ratio from v_rcp_f32) writes 128 phi.
 //   sub-range back — LpCascade over 1024 phi (iir16: a zero-state packed pass,
 //     one f64 Kogge-Stone over the wave, then the reference's f32 TDF-II
-//     recurrence into the audio FIR's pair image (f[j], f[j+512])); audio FIR =
-//     125 taps in 8 blocks of 16, one v_pk_fma_f32 per tap for both halves.
+//     recurrence into f16 hi / lo planes scaled per sub-range); audio FIR = 125
+//     taps as Toeplitz products on v_mfma_f32_16x16x32_f16 (three products per
+//     K-step, f32 accumulation), A operands from LDS (sg::back).
 // Kernels:
 //   k_wbfm_seg (default) — one round of waves, each walking a segment of 1024-
 //     output sub-ranges (see the comment at the kernel).
