@@ -15,6 +15,7 @@ CFG = {  # samples per launch, input bytes, algorithmic bytes per sample, kernel
     "c3": (256 << 20, 8 * (256 << 20), 9.0, "k_decim_w4"),
     "c4": (8 << 24, 8 * (8 << 24), 8.5, "k_wbfm_seg"),
     "c5": (128 << 20, 8 * (128 << 20), 12.0, "k_lpdc_sp"),
+    "c5f": (128 << 20, 8 * (128 << 20), 16.0, "k_fir_iq8"),  # its dominant kernel: the channel FIR
     # block rows (tools/block_bench.py / mod_bench.py, scripts/traffic_rows.sh)
     "a9": (1 << 24, 8 * (1 << 24), 12.0, "k_scan_sp"),
     "fmmod": (1 << 26, 4 * (1 << 26), 12.0, "k_fm_mod_sp"),
