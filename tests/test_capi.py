@@ -163,3 +163,17 @@ def test_c_consumer_wbfm_parity_on_the_gpu():
     r = subprocess.run([_c_consumer(), str(1 << 20)], capture_output=True, text=True, timeout=300)
     print(r.stdout.strip())
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_batch_process_rejects_a_null_handle():
+    """orion_batch_process (SURVEY §8(b)'s batched entry) fails with ORION_E_NULL and a
+    message on a null handle, before touching any device."""
+    import orion_sdr
+
+    lib = ctypes.CDLL(orion_sdr.lib_path())
+    lib.orion_batch_process.restype = ctypes.c_int
+    lib.orion_batch_process.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    lib.orion_last_error.restype = ctypes.c_char_p
+    assert lib.orion_batch_process(None, None, 1, 0, None, 0, None, None) == -1
+    assert b"null" in lib.orion_last_error()
