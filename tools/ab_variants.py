@@ -100,6 +100,8 @@ def main():
             k, v = o.split("=")
             if k == "wbfm_path":  # WbfmChain kernel path: segmented / split / graph
                 blk.configure(v)
+            elif k == "wbfm_segs":  # the segmented kernel with this many segments (waves)
+                blk.configure("segmented", int(v))
             else:
                 blk.configure_option(k, int(v))
         out = blk.process_device(x)
